@@ -1,0 +1,94 @@
+"""Pin the CPU oracle (oracle/fjsp_oracle.c) against fixtures produced by the reference.
+
+Fixtures: tests/golden/gen_golden.py ran /root/reference (with stand-in SimPy/gymnasium/
+pettingzoo) — traces, scenarios, reset tables, 256-env digests and GAE vectors.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests import parity_util as P
+
+
+def _replay(tr):
+    env = O.OracleEnv(**tr.cfg)
+    r = env.reset(seed=tr.seed, num_orders=tr.num_orders)
+    assert P.bits_equal(r["obs_i32"], tr.init_i32)
+    assert P.bits_equal(r["masks"], tr.init_masks)
+    for t in range(tr.steps):
+        r = env.step(tr.actions[t])
+        assert r["status"] & O.ST_EXCEPTION == 0
+        for k in ("obs_i32", "obs_i8", "obs_f32", "masks", "rewards"):
+            assert P.bits_equal(r[k], getattr(tr, k)[t]), (tr.name, t, k, r[k], getattr(tr, k)[t])
+        assert r["term"] == tr.term[t] and r["trunc"] == tr.trunc[t], (tr.name, t)
+        assert r["sim_time"] == tr.sim_time[t]
+        assert r["orders_completed"] == tr.orders_completed[t]
+        assert r["packaged"] == tr.packaged[t]
+        assert P.bits_equal(r["results"], tr.results[t]), (tr.name, t, r["results"], tr.results[t])
+        if r["term"] or r["trunc"]:
+            r = env.reset(num_orders=tr.num_orders)   # seed=None continues the MT stream
+        assert P.bits_equal(r["obs_i32"], tr.reset_i32[t])
+        assert P.bits_equal(r["obs_i8"], tr.reset_i8[t])
+        assert P.bits_equal(r["obs_f32"], tr.reset_f32[t])
+        assert P.bits_equal(r["masks"], tr.reset_masks[t])
+
+
+@pytest.mark.parametrize("tr", P.load_traces(), ids=lambda t: t.name)
+def test_oracle_traces(tr):
+    _replay(tr)
+
+
+@pytest.mark.parametrize("tr", P.load_scenarios(), ids=lambda t: t.name)
+def test_oracle_scenarios(tr):
+    _replay(tr)
+
+
+def test_oracle_reset_tables(golden_dir):
+    d = np.load(f"{golden_dir}/reset_tables.npz")
+    env = O.OracleEnv()
+    for s in range(256):
+        env.reset(seed=s, num_orders=30)
+        o = env.orders()
+        got = np.stack([o & 15, (o >> 4) & 3, (o >> 6) & 3], 1).astype(np.uint8)
+        assert np.array_equal(got, d["seeded"][s]), s
+    for s in range(16):
+        for r in range(4):
+            env.reset(seed=s if r == 0 else None, num_orders=25)
+            o = env.orders()
+            got = np.stack([o & 15, (o >> 4) & 3, (o >> 6) & 3], 1).astype(np.uint8)
+            assert np.array_equal(got, d["continued"][s, r]), (s, r)
+
+
+def test_oracle_digests():
+    dg = P.load_digests()
+    n, steps, chunk = dg["n_envs"], dg["steps"], dg["chunk"]
+    rec, _, _ = O.rollout(n, steps, seeds=np.arange(n), gid0=0, num_orders=dg["num_orders"],
+                          action_seed=dg["action_seed"], policy=0)
+    for e in range(n):
+        row = P.chunk_digests(lambda t: (rec["obs_i32"][t, e], rec["obs_i8"][t, e], rec["obs_f32"][t, e],
+                                         rec["masks"][t, e], rec["rewards"][t, e], rec["term"][t, e],
+                                         rec["trunc"][t, e]), steps, chunk)
+        assert row == dg["digests"][e], e
+
+
+def test_oracle_gae(golden_dir):
+    d = np.load(f"{golden_dir}/gae.npz")
+    for c in range(3):
+        g, l = d[f"c{c}_gamma_lamb"]
+        ret, adv = O.gae(d[f"c{c}_rewards"], d[f"c{c}_values"], d[f"c{c}_boots"].astype(np.float64),
+                         d[f"c{c}_seg_end"], float(g), float(l))
+        assert P.bits_equal(ret, d[f"c{c}_returns"]), c
+        assert P.bits_equal(adv, d[f"c{c}_adv"]), c
+
+
+def test_action_rng_matches_generator():
+    from tests.golden.gen_golden import action_rng
+    rng = np.random.default_rng(5)
+    for _ in range(200):
+        seed, gid, step = int(rng.integers(0, 2**63)), int(rng.integers(0, 2**32)), int(rng.integers(0, 2**32))
+        assert O.actions(seed, gid, step).tolist() == action_rng(seed, gid, step)
+        masks = (rng.random(29) < 0.5).astype(np.int8)
+        for off in (0, 3, 11, 14, 17, 20, 23, 26):
+            masks[off] = 1
+        ml = [masks[0:3], masks[3:11]] + [masks[11 + 3 * i: 14 + 3 * i] for i in range(6)]
+        assert O.actions(seed, gid, step, masks).tolist() == action_rng(seed, gid, step, ml)
