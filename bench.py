@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/sec of the vectorised FJSP step on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], the metric's "4096 parallel envs on 1 MI355X"): 4096
+reference environments per GPU (num_orders=30, default CONFIG), synthetic uniformly random
+actions (action_space.sample() semantics) from the on-device counter RNG, auto-reset on
+truncation/termination (MT19937 stream continued like reset(seed=None)).  One bench "step" =
+one FJSPSimulation.step() of every env on this GPU; obs (reference dtypes), fp64 rewards,
+term and trunc of every step are written to an HBM trajectory slab.  Steps are executed by
+the fused kernel k_step_many in launches of --chunk steps.
+
+Multi-GPU (torchrun): one process per GPU, envs sharded by global id (rank * envs + e) with
+no data-path collective ("scaling": "weak"); the only collectives are the barrier and the
+max-over-ranks of the elapsed time.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes
+import importlib
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+ALGO_BYTES_FUSED = 145 + 64 + 2          # obs (reference dtypes) + f64 rewards[8] + term + trunc
+ALGO_BYTES_STEP = 8 + ALGO_BYTES_FUSED   # + u8 actions[8] read from HBM
+HBM_PEAK_GBS = 8000.0                     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--chunk", type=int, default=200, help="env steps per fused launch")
+    ap.add_argument("--num-orders", type=int, default=30)
+    ap.add_argument("--masked", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
+    ap.add_argument("--no-step-mode", action="store_true", help="skip the one-launch-per-step measurement")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, workers):
+    """The oracle (C port of the reference, kind='port') on the host cores, bounded sample."""
+    from oracle import oracle as O
+    O.lib()
+    steps = 200
+    t0 = time.perf_counter()
+    O.rollout(16, steps, num_orders=args.num_orders, record=False)
+    per_env_step = (time.perf_counter() - t0) / (16 * steps)
+    envs_per_thread = max(1, int(args.cpu_seconds / (per_env_step * steps)))
+    res = [None] * workers
+
+    def work(i):
+        t = time.perf_counter()
+        O.rollout(envs_per_thread, steps, seeds=np.arange(i * envs_per_thread, (i + 1) * envs_per_thread),
+                  gid0=i * envs_per_thread, num_orders=args.num_orders, record=False,
+                  policy=1 if args.masked else 0)
+        res[i] = time.perf_counter() - t
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(workers)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - t0
+    total = workers * envs_per_thread * steps
+    return {"value": total / wall, "unit": "env-steps/s", "cores": workers, "kind": "port",
+            "sample": f"{workers} threads x {envs_per_thread} envs x {steps} steps of the same workload "
+                      f"(oracle/fjsp_oracle.c, C restatement of FJSPSimulation.step with a SimPy event heap); "
+                      f"wall {wall:.2f}s",
+            "reference_python_1core": "8.0-9.0k env-steps/s (measured in the build container, BASELINE.md)"}
+
+
+def load_pmc(workload):
+    p = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    vec_env = importlib.import_module("multi-agent-rl-for-fjsp_amd.vec_env")
+
+    N = args.envs
+    base = rank * N
+    env = vec_env.FJSPVecEnv(N, device=dev, env_id_base=base)
+    env.reset(seeds=torch.arange(base, base + N), num_orders=args.num_orders)
+    chunk = max(1, min(args.chunk, args.steps))
+    buf = vec_env.Buffers(chunk, N, dev, infos=False)
+    stream = torch.cuda.current_stream(dev)
+
+    def run(nsteps, step0, timing=None):
+        done = 0
+        while done < nsteps:
+            k = min(chunk, nsteps - done)
+            if timing is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            env.rollout(k, action_seed=1234, step0=step0 + done, masked=args.masked, buffers=buf)
+            if timing is not None:
+                e1.record(stream)
+                timing.append((e0, e1, k))
+            done += k
+        return step0 + nsteps
+
+    s0 = run(args.warmup, 0)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timing = []
+    t0 = time.perf_counter()
+    run(args.steps, s0, timing)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = [a.elapsed_time(b) for a, b, _ in timing]
+    kern_steps = [k for _, _, k in timing]
+    full = [ms for ms, k in zip(kern_ms, kern_steps) if k == chunk] or kern_ms
+    avg_launch_ms = float(np.mean(full))
+    steps_per_launch = chunk
+    total_env_steps = args.steps * N * world
+    value = total_env_steps / elapsed
+    achieved = ALGO_BYTES_FUSED * N * steps_per_launch / (avg_launch_ms * 1e-3) / 1e9
+
+    # one-launch-per-step mode (actions resident in HBM, k_step): the RL-loop path
+    per_step = None
+    if not args.no_step_mode:
+        K = min(200, args.steps)
+        acts = torch.randint(0, 256, (K, 8, N), dtype=torch.int32, device=dev)
+        nact = torch.tensor([3, 8, 3, 3, 3, 3, 3, 3], dtype=torch.int32, device=dev).view(1, 8, 1)
+        acts = ((acts * nact) >> 8).to(torch.uint8).contiguous()
+        sbuf = vec_env.Buffers(1, N, dev, infos=False)
+        for t in range(20):
+            env.step(acts[t], buffers=sbuf)
+        torch.cuda.synchronize()
+        ev = []
+        t1 = time.perf_counter()
+        for t in range(K):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            env.step(acts[t], buffers=sbuf)
+            e1.record(stream)
+            ev.append((e0, e1))
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t1
+        kms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        per_step = {"value": K * N / wall, "unit": "env-steps/s", "n_gpus": 1, "avg_kernel_ms": kms,
+                    "kernel": "k_step<true>", "algo_bytes_per_env_step": ALGO_BYTES_STEP,
+                    "achieved_GBs": ALGO_BYTES_STEP * N / (kms * 1e-3) / 1e9,
+                    "note": "one launch per step, actions u8[8][N] resident in HBM (rank 0)"}
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        try:
+            workers = max(1, min(16, len(os.sched_getaffinity(0))))
+        except Exception:
+            workers = max(1, min(16, os.cpu_count() or 1))
+        cpu = cpu_baseline(args, workers)
+
+    workload = f"fjsp_step_{N}envs"
+    pmc = load_pmc(workload)
+    traffic = None
+    if pmc and pmc.get("steps_per_launch") == steps_per_launch and pmc.get("envs") == N:
+        traffic = pmc.get("hbm_bytes_per_launch")
+    if rank == 0:
+        out = {
+            "metric": "env-steps/sec (all agents) at N parallel envs, 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32+f64",
+            "data": "synthetic: random actions from the on-device counter RNG, envs seeded by global id",
+            "config": {"workload": workload, "envs_per_gpu": N, "global_envs": N * world,
+                       "num_orders": args.num_orders, "policy": "masked-random" if args.masked else "random",
+                       "steps_per_launch": steps_per_launch, "kernel": "k_step_many",
+                       "parallelism": f"env-shard x{world} (no data-path collective)"},
+            "agent_steps_per_s": value * 8,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_step_many", "avg_launch_ms": avg_launch_ms,
+                         "algo_bytes_per_env_step": ALGO_BYTES_FUSED,
+                         "env_steps_per_launch": N * steps_per_launch},
+            "cpu_baseline": cpu,
+            "per_step_launch": per_step,
+            "state_bytes_per_env": env.state_bytes_per_env(),
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,128 @@
+"""ctypes binding of libfjsp.so (C-ABI declared in include/fjsp.h).
+
+The library is the ONLY compute path of this package: every reset / step / GAE call goes to
+the HIP kernels for gfx950.  If the library is missing or no GPU is visible, the calls fail
+loudly (FjspNativeError) — there is no CPU fallback.
+"""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libfjsp.so")
+SRC = os.path.join(HERE, "csrc", "fjsp_hip.hip")
+HEADERS = [os.path.join(HERE, "csrc", "fjsp_env.h"), os.path.join(REPO, "include", "fjsp.h")]
+
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
+
+
+class FjspNativeError(RuntimeError):
+    pass
+
+
+class fjsp_config(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int32) for k in (
+        "num_trays", "tray_capacity", "mask_tray_capacity", "storage_capacity", "step_size",
+        "max_episode_steps", "agv_speed", "pt_small", "pt_big", "pt_packaging", "packaging_capacity")]
+
+
+OUT_FIELDS = ["obs_i32", "obs_i8", "obs_f32", "masks", "rewards", "term", "trunc", "results",
+              "orders_completed", "packaged", "sim_time", "status",
+              "next_i32", "next_i8", "next_f32", "next_masks"]
+
+
+class fjsp_out(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in OUT_FIELDS]
+
+
+class fjsp_env_view(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int32) for k in (
+        "current_step", "num_orders", "next_order", "orders_completed", "total_packaged",
+        "agv_row", "agv_col", "agv_carrying", "agv_tray_count")] + [
+        ("status", ctypes.c_uint32), ("orders", ctypes.c_uint32 * 64)]
+
+
+# every symbol include/fjsp.h declares (checked by tests/test_abi.py)
+EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_check_config",
+           "fjsp_create", "fjsp_destroy", "fjsp_set_stream", "fjsp_num_envs", "fjsp_state_bytes",
+           "fjsp_reset", "fjsp_step", "fjsp_step_many", "fjsp_gae", "fjsp_mt_get", "fjsp_mt_set",
+           "fjsp_read_env", "fjsp_sync", "fjsp_last_kernel_ms"]
+
+_lib = None
+
+
+def _stale():
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(p) > t for p in [SRC] + HEADERS)
+
+
+def build(force=False, verbose=False):
+    """Compile libfjsp.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    if not force and not _stale():
+        return LIB_PATH
+    cmd = ["hipcc"] + HIPCC_FLAGS + ["-o", LIB_PATH, SRC]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise FjspNativeError("hipcc failed:\n" + r.stderr[-4000:])
+    if verbose:
+        print(r.stderr)
+    return LIB_PATH
+
+
+def lib():
+    """Load libfjsp.so (after torch, so one HIP runtime serves both)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (loads torch's libamdhip64 first: same SONAME -> shared runtime)
+    if not os.path.exists(LIB_PATH):
+        raise FjspNativeError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, U32, U64, D = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double
+    sig = {
+        "fjsp_abi_version": (I, []),
+        "fjsp_last_error": (ctypes.c_char_p, []),
+        "fjsp_default_config": (I, [ctypes.POINTER(fjsp_config)]),
+        "fjsp_check_config": (I, [ctypes.POINTER(fjsp_config)]),
+        "fjsp_create": (I, [ctypes.POINTER(fjsp_config), I, I, P, ctypes.POINTER(P)]),
+        "fjsp_destroy": (I, [P]),
+        "fjsp_set_stream": (I, [P, P]),
+        "fjsp_num_envs": (I, [P]),
+        "fjsp_state_bytes": (ctypes.c_int64, [P]),
+        "fjsp_reset": (I, [P, P, P, I, ctypes.POINTER(fjsp_out)]),
+        "fjsp_step": (I, [P, P, P, I, ctypes.POINTER(fjsp_out)]),
+        "fjsp_step_many": (I, [P, I, U64, U32, U32, I, I, ctypes.POINTER(fjsp_out)]),
+        "fjsp_gae": (I, [P, P, P, P, I, I, I, D, D, P, P, P]),
+        "fjsp_mt_get": (I, [P, I, P, ctypes.POINTER(I)]),
+        "fjsp_mt_set": (I, [P, I, P, I]),
+        "fjsp_read_env": (I, [P, I, ctypes.POINTER(fjsp_env_view)]),
+        "fjsp_sync": (I, [P]),
+        "fjsp_last_kernel_ms": (I, [P, ctypes.POINTER(ctypes.c_float)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    if L.fjsp_abi_version() != 1:
+        raise FjspNativeError("libfjsp.so ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise FjspNativeError(lib().fjsp_last_error().decode())
+    return rc
+
+
+def default_config(**over):
+    c = fjsp_config()
+    lib().fjsp_default_config(ctypes.byref(c))
+    for k, v in over.items():
+        setattr(c, k, int(v))
+    return c

@@ -1,0 +1,668 @@
+// fjsp_hip.hip — HIP kernels (gfx950) and the C-ABI of libfjsp.so (include/fjsp.h).
+//
+// Layout in HBM (all SoA, N = number of envs, lane e of a wavefront = env e):
+//   words  u32 [NWORDS][N]        packed register state of fjsp::Env (pack/unpack below)
+//   orders u32 [64][N]            order table (processed/packaged masks, n, type, colour)
+//   scode  u16 [255][N]           tray-slot arena: tray code
+//   snext  u8  [255][N]           tray-slot arena: next slot of the FIFO the slot is in
+//   scstep u16 [255][N]           tray-slot arena: completion step of an in-flight run
+//   mt     u32 [624][N]           per-env MT19937 state (numpy legacy RandomState)
+// Kernels: one lane per env, 64-lane workgroups (one wavefront; 4096 envs -> 64 CUs).
+//   k_reset      FJSPSimulation.reset (FJSPSimulation.py:286-323)
+//   k_step       FJSPSimulation.step  (FJSPSimulation.py:144-242), actions from HBM
+//   k_step_many  K fused steps with on-device counter-RNG actions
+//   k_gae        transition_memory.py:83-105 (returns + GAE), one lane per (agent, env) column
+// Compiled with -ffp-contract=off: rewards and GAE follow Python's unfused fp64 op order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+
+#include "fjsp_env.h"
+#include "../../include/fjsp.h"
+
+using namespace fjsp;
+
+namespace {
+
+constexpr int BLOCK = 64;
+constexpr int MT_N = 624;
+
+struct DevState {
+    uint32_t* words;
+    uint32_t* orders;
+    uint16_t* scode;
+    uint8_t* snext;
+    uint16_t* scstep;
+    uint32_t* mt;
+    int n;
+};
+
+// ---------------------------------------------------------------- pack / unpack of Env
+__device__ __forceinline__ void env_load(Env& E, const uint32_t* __restrict__ w, int n, int e) {
+    auto W = [&](int i) { return w[i * n + e]; };
+    uint32_t x;
+    x = W(0); E.step = x & 0xFFFF; E.norders = (x >> 16) & 0xFF; E.next_order = x >> 24;
+    x = W(1); E.ncompleted = x & 0xFF; E.total_packaged = x >> 8;
+    E.status = W(2);
+    E.mti = W(3);
+    x = W(4);
+    E.cur_order = (x & 0xFF) == 0xFF ? -1 : (int)(x & 0xFF);
+    E.cur_idx = (x >> 8) & 15; E.cur_n = (x >> 12) & 15; E.cur_type = (x >> 16) & 3; E.cur_color = (x >> 18) & 3;
+    E.tray_valid = (x >> 20) & 1; E.tray_count = (x >> 21) & 7; E.tray_start = (x >> 24) & 15;
+    x = W(5); E.tray_order = x & 0xFF; E.pool = (x >> 8) & 0xFFFF; E.slot_next = x >> 24;
+    x = W(6);
+    E.loc = x & 7; E.carry = (x >> 3) & 0xFF; E.carry_code = (x >> 11) & 0x1FFF; E.carry_type = (x >> 24) & 3;
+    E.carry_color = (x >> 26) & 3; E.carry_np = (x >> 28) & 1; E.carry_nk = (x >> 29) & 1;
+#pragma unroll
+    for (int l = 0; l < NLIST; l++) {
+        x = W(7 + l); E.lh[l] = x & 0xFF; E.lt[l] = (x >> 8) & 0xFF; E.ll[l] = x >> 16;
+    }
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+        x = W(17 + m);
+        E.m_busy[m] = x & 1; E.m_cur[m] = (x >> 1) & 0xFF; E.m_code[m] = (x >> 9) & 0x1FFF;
+        E.m_prog[m] = (x >> 22) & 1; E.m_k[m] = (x >> 23) & 15;
+    }
+    x = W(19); E.m_next[0] = x & 0xFFFF; E.m_next[1] = x >> 16;
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        x = W(20 + s);
+        E.p_busy[s] = x & 1; E.p_hascur[s] = (x >> 1) & 1; E.p_qfirst[s] = (x >> 2) & 0xFF;
+        E.p_inflight[s] = (x >> 10) & 0xFF; E.p_queued[s] = (x >> 18) & 0x3FFF;
+    }
+    x = W(24); E.p_completed[0] = x & 0xFFFF; E.p_completed[1] = x >> 16;
+    x = W(25); E.p_completed[2] = x & 0xFFFF; E.p_completed[3] = x >> 16;
+#pragma unroll
+    for (int s = 0; s < 4; s++) E.p_prog[s] = __uint_as_float(W(26 + s));
+}
+
+__device__ __forceinline__ void env_store(const Env& E, uint32_t* __restrict__ w, int n, int e) {
+    auto W = [&](int i, uint32_t v) { w[i * n + e] = v; };
+    W(0, (uint32_t)E.step | ((uint32_t)E.norders << 16) | ((uint32_t)E.next_order << 24));
+    W(1, (uint32_t)E.ncompleted | ((uint32_t)E.total_packaged << 8));
+    W(2, E.status);
+    W(3, (uint32_t)E.mti);
+    W(4, (uint32_t)(E.cur_order < 0 ? 0xFF : E.cur_order) | ((uint32_t)E.cur_idx << 8) | ((uint32_t)E.cur_n << 12) |
+             ((uint32_t)E.cur_type << 16) | ((uint32_t)E.cur_color << 18) | ((uint32_t)E.tray_valid << 20) |
+             ((uint32_t)E.tray_count << 21) | ((uint32_t)E.tray_start << 24));
+    W(5, (uint32_t)E.tray_order | ((uint32_t)E.pool << 8) | ((uint32_t)E.slot_next << 24));
+    W(6, (uint32_t)E.loc | ((uint32_t)E.carry << 3) | ((uint32_t)E.carry_code << 11) | ((uint32_t)E.carry_type << 24) |
+             ((uint32_t)E.carry_color << 26) | ((uint32_t)E.carry_np << 28) | ((uint32_t)E.carry_nk << 29));
+#pragma unroll
+    for (int l = 0; l < NLIST; l++) W(7 + l, (uint32_t)E.lh[l] | ((uint32_t)E.lt[l] << 8) | ((uint32_t)E.ll[l] << 16));
+#pragma unroll
+    for (int m = 0; m < 2; m++)
+        W(17 + m, (uint32_t)E.m_busy[m] | ((uint32_t)E.m_cur[m] << 1) | ((uint32_t)E.m_code[m] << 9) |
+                      ((uint32_t)E.m_prog[m] << 22) | ((uint32_t)E.m_k[m] << 23));
+    W(19, (uint32_t)E.m_next[0] | ((uint32_t)E.m_next[1] << 16));
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+        W(20 + s, (uint32_t)E.p_busy[s] | ((uint32_t)E.p_hascur[s] << 1) | ((uint32_t)E.p_qfirst[s] << 2) |
+                      ((uint32_t)(E.p_inflight[s] & 0xFF) << 10) | ((uint32_t)(E.p_queued[s] & 0x3FFF) << 18));
+    W(24, (uint32_t)(E.p_completed[0] & 0xFFFF) | ((uint32_t)E.p_completed[1] << 16));
+    W(25, (uint32_t)(E.p_completed[2] & 0xFFFF) | ((uint32_t)E.p_completed[3] << 16));
+#pragma unroll
+    for (int s = 0; s < 4; s++) W(26 + s, __float_as_uint(E.p_prog[s]));
+}
+static_assert(NWORDS >= 30, "packed state needs 30 words");
+
+// ---------------------------------------------------------------- MT19937, lazily twisted
+// State word: mti (bits 0..9) | g (bits 16..25).  Words [0, g) of the array already hold the
+// current block, [g, 624) still the previous one; mti <= g is the next word to consume.
+// Word i of a new block is generated on demand with the same in-place recurrence as
+// numpy's sequential twist (mt[i+1] is still old, mt[i+397 mod 624] is new iff i >= 227),
+// so the k-th draw equals numpy's k-th draw while touching 3 words instead of 624.
+// Standard numpy (key, pos): pos == 624 <-> (mti, g) = (0, 0); pos < 624 <-> (pos, 624).
+__device__ __forceinline__ uint32_t mt_draw(uint32_t* __restrict__ mt, int n, int e, int& st) {
+    int i = st & 0x3FF, g = (st >> 16) & 0x3FF;
+    uint32_t v;
+    if (i < g) {
+        v = mt[i * n + e];
+    } else {
+        const int i1 = (i + 1 == MT_N) ? 0 : i + 1;
+        const int im = (i + 397 >= MT_N) ? i + 397 - MT_N : i + 397;
+        const uint32_t a = mt[i * n + e], b = mt[i1 * n + e], c = mt[im * n + e];
+        const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+        v = c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        mt[i * n + e] = v;
+        g = i + 1;
+    }
+    i += 1;
+    if (i == MT_N) { i = 0; g = 0; }
+    st = i | (g << 16);
+    uint32_t t = v;
+    t ^= t >> 11;
+    t ^= (t << 7) & 0x9d2c5680u;
+    t ^= (t << 15) & 0xefc60000u;
+    t ^= t >> 18;
+    return t;
+}
+// numpy masked-rejection bounded draw (rng <= 0xFFFFFFFF, use_masked=True)
+__device__ __forceinline__ int mt_bounded(uint32_t* mt, int n, int e, int& st, uint32_t rng, uint32_t mask) {
+    uint32_t v;
+    do { v = mt_draw(mt, n, e, st) & mask; } while (v > rng);
+    return (int)v;
+}
+
+__device__ void mt_seed(uint32_t* __restrict__ mt, int n, int e, uint32_t seed) {
+    uint32_t x = seed;
+    mt[e] = x;
+    for (int i = 1; i < MT_N; i++) {
+        x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
+        mt[i * n + e] = x;
+    }
+}
+
+// FJSPSimulation.reset body after the optional reseed (FJSPSimulation.py:301-320)
+__device__ void env_reset(Env& E, const Tables& T, const Cfg& C, const DevState& S, int e, int num_orders) {
+    env_clear(E, C);
+    E.norders = num_orders;
+    int mti = E.mti;
+    for (int o = 0; o < num_orders; o++) {     // generate_order (FJSPSimulation.py:101-131)
+        const int n = 1 + mt_bounded(S.mt, S.n, e, mti, 8u, 15u);    // randint(1, 10)
+        const int ty = 1 + mt_bounded(S.mt, S.n, e, mti, 2u, 3u);    // choice(list(ProductType))
+        const int co = 1 + mt_bounded(S.mt, S.n, e, mti, 2u, 3u);    // choice(list(PackagingColor))
+        T.orders[o * T.stride] = ow_make(n, ty, co);
+    }
+    E.mti = mti;
+}
+
+__device__ __forceinline__ Tables tables_of(const DevState& S, int e) {
+    Tables T;
+    T.orders = S.orders + e;
+    T.scode = S.scode + e;
+    T.snext = S.snext + e;
+    T.scstep = S.scstep + e;
+    T.stride = S.n;
+    return T;
+}
+
+__device__ __forceinline__ void write_obs(const Obs& o, int32_t* i32, int8_t* i8, float* f32, int8_t* mk, size_t base_t,
+                                          int n, int e) {
+    if (i32) {
+#pragma unroll
+        for (int f = 0; f < NI32; f++) i32[(base_t * NI32 + f) * n + e] = o.i32[f];
+    }
+    if (i8) {
+#pragma unroll
+        for (int f = 0; f < NI8; f++) i8[(base_t * NI8 + f) * n + e] = o.i8[f];
+    }
+    if (f32) {
+#pragma unroll
+        for (int f = 0; f < NF32; f++) f32[(base_t * NF32 + f) * n + e] = o.f32[f];
+    }
+    if (mk) {
+#pragma unroll
+        for (int f = 0; f < NMASK; f++) mk[(base_t * NMASK + f) * n + e] = o.mask[f];
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_seed(DevState S, const uint32_t* __restrict__ seeds, uint32_t seed_base) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= S.n) return;
+    mt_seed(S.mt, S.n, e, seeds ? seeds[e] : seed_base + (uint32_t)e);
+    S.words[3 * S.n + e] = 0;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_reset(DevState S, Cfg C, const uint32_t* __restrict__ seeds,
+                                                 const uint8_t* __restrict__ env_mask, int num_orders, fjsp_out out) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= S.n) return;
+    if (env_mask && !env_mask[e]) return;
+    Tables T = tables_of(S, e);
+    Env E;
+    int mti = (int)S.words[3 * S.n + e];
+    if (seeds) { mt_seed(S.mt, S.n, e, seeds[e]); mti = 0; }
+    E.mti = mti;
+    env_reset(E, T, C, S, e, num_orders);
+    env_store(E, S.words, S.n, e);
+    Obs o;
+    observe(E, C, o);
+    write_obs(o, out.obs_i32, out.obs_i8, out.obs_f32, out.masks, 0, S.n, e);
+    if (out.status) out.status[e] = E.status;
+}
+
+// fmix64 counter RNG for synthetic actions (oracle_actions spec)
+__device__ __forceinline__ uint64_t fmix64(uint64_t z) {
+    z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27; z *= 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return z;
+}
+
+__device__ __forceinline__ void synth_actions(uint64_t seed, uint32_t gid, uint32_t step, int mode, const Env& E,
+                                              const Cfg& C, int* act) {
+    const uint64_t h = fmix64(seed ^ fmix64(((uint64_t)gid << 32) | step));
+    const int nact[NA] = {3, 8, 3, 3, 3, 3, 3, 3};
+    if (mode == FJSP_ACTIONS_UNMASKED) {
+#pragma unroll
+        for (int a = 0; a < NA; a++) act[a] = (int)((((uint32_t)(h >> (8 * a)) & 0xFFu) * (uint32_t)nact[a]) >> 8);
+        return;
+    }
+    int8_t m[NMASK];
+    compute_masks(E, C, m);
+    const int moff[NA] = {0, 3, 11, 14, 17, 20, 23, 26};
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+        uint32_t bits = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+            if (i < nact[a] && m[moff[a] + i]) bits |= 1u << i;
+        const int cnt = __popc(bits);
+        int j = (int)((((uint32_t)(h >> (8 * a)) & 0xFFu) * (uint32_t)cnt) >> 8);
+        // j-th set bit
+        uint32_t b = bits;
+        for (int k = 0; k < j; k++) b &= b - 1u;
+        act[a] = __ffs(b) - 1;
+    }
+}
+
+// One full env step + outputs at trajectory index t; handles auto-reset.
+template <bool CANON>
+__device__ __forceinline__ void step_and_emit(Env& E, const Tables& T, const Cfg& C, const DevState& S, int e,
+                                              const int* act, const uint8_t* order, int autoreset, const fjsp_out& out,
+                                              size_t t) {
+    const int n = S.n;
+    uint32_t res[NA];
+    double rew[NA];
+    env_step<CANON>(E, T, C, act, order, res, rew);
+    Obs o;
+    observe(E, C, o);
+    const int all_done = E.ncompleted == E.norders && E.norders > 0 && E.next_order == E.norders;
+    const int truncated = E.step >= C.max_steps;
+    write_obs(o, out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, e);
+    if (out.rewards) {
+#pragma unroll
+        for (int a = 0; a < NA; a++) out.rewards[(t * NA + a) * n + e] = rew[a];
+    }
+    if (out.results) {
+#pragma unroll
+        for (int a = 0; a < NA; a++) out.results[(t * NA + a) * n + e] = res[a];
+    }
+    if (out.term) out.term[t * n + e] = (uint8_t)all_done;
+    if (out.trunc) out.trunc[t * n + e] = (uint8_t)truncated;
+    if (out.orders_completed) out.orders_completed[t * n + e] = E.ncompleted;
+    if (out.packaged) out.packaged[t * n + e] = E.total_packaged;
+    if (out.sim_time) out.sim_time[t * n + e] = (double)(E.step + 1) * (double)C.step_size;
+    if (out.status) out.status[t * n + e] = E.status;
+    E.step += 1;
+    if (autoreset && (all_done || truncated)) {
+        env_reset(E, T, C, S, e, E.norders);   // reset(seed=None) continues the MT stream
+        observe(E, C, o);
+    }
+    write_obs(o, out.next_i32, out.next_i8, out.next_f32, out.next_masks, t, n, e);
+}
+
+template <bool CANON>
+__global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t* __restrict__ actions, uint64_t order_packed,
+                                                int autoreset, fjsp_out out) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= S.n) return;
+    Tables T = tables_of(S, e);
+    Env E;
+    env_load(E, S.words, S.n, e);
+    int act[NA];
+#pragma unroll
+    for (int a = 0; a < NA; a++) act[a] = actions[a * S.n + e];
+    uint8_t order[NA];
+#pragma unroll
+    for (int i = 0; i < NA; i++) order[i] = (uint8_t)(order_packed >> (8 * i));
+    step_and_emit<CANON>(E, T, C, S, e, act, order, autoreset, out, 0);
+    env_store(E, S.words, S.n, e);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0,
+                                                     int mode, int autoreset, fjsp_out out) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= S.n) return;
+    Tables T = tables_of(S, e);
+    Env E;
+    env_load(E, S.words, S.n, e);
+    for (int k = 0; k < K; k++) {
+        int act[NA];
+        synth_actions(seed, gid0 + (uint32_t)e, step0 + (uint32_t)k, mode, E, C, act);
+        step_and_emit<true>(E, T, C, S, e, act, nullptr, autoreset, out, (size_t)k);
+    }
+    env_store(E, S.words, S.n, e);
+}
+
+// transition_memory.py:83-105 over a [T][M] rollout buffer; column m = a*N + e
+__global__ void __launch_bounds__(256) k_gae(const double* __restrict__ r, const float* __restrict__ v,
+                                             const uint8_t* __restrict__ done, const double* __restrict__ boot, int T,
+                                             int N, int M, double gamma, double lamb, double* __restrict__ ret,
+                                             double* __restrict__ adv) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= M) return;
+    const int e = m % N;
+    const double gl = gamma * lamb;
+    double nv = 0.0, rr = 0.0, gae = 0.0;
+    for (int t = T - 1; t >= 0; t--) {
+        const size_t i = (size_t)t * M + m;
+        if (t == T - 1 || done[(size_t)t * N + e]) {   // a trajectory ends at t
+            nv = (t == T - 1 && !done[(size_t)t * N + e]) ? boot[m] : 0.0;
+            rr = nv;
+            gae = 0.0;
+        }
+        const double rt = r[i];
+        const double vt = (double)v[i];
+        rr = rt + gamma * rr;
+        ret[i] = rr;
+        const double td = rt + gamma * nv - vt;
+        gae = td + gl * gae;
+        adv[i] = gae;
+        nv = vt;
+    }
+}
+
+}  // namespace
+
+// ================================================================ C-ABI
+struct fjsp_handle {
+    fjsp_config cfg;
+    Cfg dcfg;
+    int n;
+    int device;
+    hipStream_t stream;
+    DevState S;
+    void* base;
+    size_t bytes;
+    int has_reset;
+    hipEvent_t ev0, ev1;
+    int timed;
+};
+
+static thread_local std::string g_err;
+
+static int fail(const char* msg) {
+    g_err = msg;
+    return -1;
+}
+static int hip_fail(const char* what, hipError_t e) {
+    char buf[256];
+    snprintf(buf, sizeof(buf), "%s: %s", what, hipGetErrorString(e));
+    g_err = buf;
+    return -2;
+}
+#define HIPCHK(x)                                 \
+    do {                                          \
+        hipError_t _e = (x);                      \
+        if (_e != hipSuccess) return hip_fail(#x, _e); \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+extern "C" {
+
+int fjsp_abi_version(void) { return FJSP_ABI_VERSION; }
+const char* fjsp_last_error(void) { return g_err.c_str(); }
+
+int fjsp_default_config(fjsp_config* c) {
+    if (!c) return fail("null config");
+    c->num_trays = 1000;
+    c->tray_capacity = 5;
+    c->mask_tray_capacity = 5;
+    c->storage_capacity = 100;
+    c->step_size = 10;
+    c->max_episode_steps = 200;
+    c->agv_speed = 1;
+    c->pt_small = 60;
+    c->pt_big = 120;
+    c->pt_packaging = 30;
+    c->packaging_capacity = 20;
+    return 0;
+}
+
+int fjsp_check_config(const fjsp_config* c) {
+    if (!c) return fail("null config");
+    if (c->step_size <= 0) return fail("step_size must be > 0");
+    if (c->agv_speed <= 0 || 8 >= c->step_size * c->agv_speed)
+        return fail("AGV moves must finish inside one step: 8 / agv_speed < step_size");
+    if (c->pt_small <= 0 || c->pt_small % c->step_size) return fail("pt_small must be a positive multiple of step_size");
+    if (c->pt_big <= 0 || c->pt_big % c->step_size) return fail("pt_big must be a positive multiple of step_size");
+    if (c->pt_packaging <= 0 || c->pt_packaging % c->step_size)
+        return fail("pt_packaging must be a positive multiple of step_size");
+    if (c->tray_capacity < 1 || c->tray_capacity > 7) return fail("tray_capacity must be in 1..7");
+    if (c->max_episode_steps < 0 || c->max_episode_steps > 253) return fail("max_episode_steps must be in 0..253");
+    if (c->packaging_capacity < 1 || c->packaging_capacity > 255) return fail("packaging_capacity must be in 1..255");
+    if (c->storage_capacity < 0 || c->num_trays < 0) return fail("negative capacity");
+    return 0;
+}
+
+int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* hip_stream, fjsp_handle** out) {
+    if (!out) return fail("null out");
+    *out = nullptr;
+    fjsp_config c;
+    if (cfg) c = *cfg; else fjsp_default_config(&c);
+    if (fjsp_check_config(&c)) return -1;
+    if (num_envs <= 0) return fail("num_envs must be > 0");
+    DeviceGuard g(device);
+    fjsp_handle* h = new fjsp_handle();
+    h->cfg = c;
+    h->n = num_envs;
+    h->device = device;
+    h->stream = (hipStream_t)hip_stream;
+    h->dcfg.step_size = c.step_size;
+    h->dcfg.max_steps = c.max_episode_steps;
+    h->dcfg.tray_cap = c.tray_capacity;
+    h->dcfg.mask_tray_cap = c.mask_tray_capacity;
+    h->dcfg.storage_cap = c.storage_capacity;
+    h->dcfg.pool0 = c.num_trays < 1000 ? c.num_trays : 1000;
+    h->dcfg.pkg_cap = c.packaging_capacity;
+    h->dcfg.ptk_small = c.pt_small / c.step_size;
+    h->dcfg.ptk_big = c.pt_big / c.step_size;
+    h->dcfg.ptk_pack = c.pt_packaging / c.step_size;
+    const size_t n = (size_t)num_envs;
+    const size_t b_words = (size_t)NWORDS * n * 4, b_orders = (size_t)MAX_ORDERS * n * 4;
+    const size_t b_scode = (size_t)MAX_SLOTS * n * 2, b_snext = (size_t)MAX_SLOTS * n, b_scstep = (size_t)MAX_SLOTS * n * 2;
+    const size_t b_mt = (size_t)MT_N * n * 4;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    h->bytes = al(b_words) + al(b_orders) + al(b_scode) + al(b_snext) + al(b_scstep) + al(b_mt);
+    hipError_t e = hipMalloc(&h->base, h->bytes);
+    if (e != hipSuccess) { delete h; return hip_fail("hipMalloc(state)", e); }
+    char* p = (char*)h->base;
+    h->S.words = (uint32_t*)p; p += al(b_words);
+    h->S.orders = (uint32_t*)p; p += al(b_orders);
+    h->S.scode = (uint16_t*)p; p += al(b_scode);
+    h->S.snext = (uint8_t*)p; p += al(b_snext);
+    h->S.scstep = (uint16_t*)p; p += al(b_scstep);
+    h->S.mt = (uint32_t*)p;
+    h->S.n = num_envs;
+    e = hipMemsetAsync(h->base, 0, h->bytes, h->stream);
+    if (e == hipSuccess) e = hipEventCreate(&h->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&h->ev1);
+    if (e != hipSuccess) { (void)hipFree(h->base); delete h; return hip_fail("init", e); }
+    // default streams: env e behaves like a process that called np.random.seed(e)
+    hipLaunchKernelGGL(k_seed, dim3((h->n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, h->stream, h->S,
+                       (const uint32_t*)nullptr, 0u);
+    e = hipGetLastError();
+    if (e != hipSuccess) { (void)hipFree(h->base); delete h; return hip_fail("k_seed", e); }
+    *out = h;
+    return 0;
+}
+
+int fjsp_destroy(fjsp_handle* h) {
+    if (!h) return 0;
+    DeviceGuard g(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    (void)hipEventDestroy(h->ev0);
+    (void)hipEventDestroy(h->ev1);
+    (void)hipFree(h->base);
+    delete h;
+    return 0;
+}
+
+int fjsp_set_stream(fjsp_handle* h, void* s) {
+    if (!h) return fail("null handle");
+    h->stream = (hipStream_t)s;
+    return 0;
+}
+int fjsp_num_envs(const fjsp_handle* h) { return h ? h->n : -1; }
+int64_t fjsp_state_bytes(const fjsp_handle* h) { return h ? (int64_t)(h->bytes / h->n) : -1; }
+
+static const fjsp_out kNoOut = {};
+
+int fjsp_reset(fjsp_handle* h, const uint32_t* seeds, const uint8_t* env_mask, int32_t num_orders, const fjsp_out* out) {
+    if (!h) return fail("null handle");
+    if (num_orders < 0 || num_orders > MAX_ORDERS) return fail("num_orders must be in 0..64");
+    DeviceGuard g(h->device);
+    dim3 grid((h->n + BLOCK - 1) / BLOCK);
+    hipLaunchKernelGGL(k_reset, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, seeds, env_mask, num_orders,
+                       out ? *out : kNoOut);
+    HIPCHK(hipGetLastError());
+    h->has_reset = 1;
+    return 0;
+}
+
+int fjsp_step(fjsp_handle* h, const uint8_t* actions, const uint8_t* agent_order, int32_t autoreset, const fjsp_out* out) {
+    if (!h) return fail("null handle");
+    if (!actions) return fail("null actions");
+    if (!h->has_reset) return fail("fjsp_step before fjsp_reset");
+    bool canon = true;
+    uint64_t packed = 0;
+    if (agent_order) {
+        unsigned seen = 0;
+        for (int i = 0; i < NA; i++) {
+            if (agent_order[i] >= NA || (seen >> agent_order[i]) & 1u) return fail("agent_order must be a permutation of 0..7");
+            seen |= 1u << agent_order[i];
+            canon = canon && agent_order[i] == i;
+            packed |= (uint64_t)agent_order[i] << (8 * i);
+        }
+    }
+    DeviceGuard g(h->device);
+    dim3 grid((h->n + BLOCK - 1) / BLOCK);
+    HIPCHK(hipEventRecord(h->ev0, h->stream));
+    if (canon)
+        hipLaunchKernelGGL(k_step<true>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, packed, autoreset,
+                           out ? *out : kNoOut);
+    else
+        hipLaunchKernelGGL(k_step<false>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, packed, autoreset,
+                           out ? *out : kNoOut);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(h->ev1, h->stream));
+    h->timed = 1;
+    return 0;
+}
+
+int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env_gid0, uint32_t step0,
+                   int32_t action_mode, int32_t autoreset, const fjsp_out* traj) {
+    if (!h) return fail("null handle");
+    if (K < 0) return fail("K must be >= 0");
+    if (action_mode != FJSP_ACTIONS_UNMASKED && action_mode != FJSP_ACTIONS_MASKED) return fail("bad action_mode");
+    if (!h->has_reset) return fail("fjsp_step_many before fjsp_reset");
+    if (K == 0) return 0;
+    DeviceGuard g(h->device);
+    dim3 grid((h->n + BLOCK - 1) / BLOCK);
+    HIPCHK(hipEventRecord(h->ev0, h->stream));
+    hipLaunchKernelGGL(k_step_many, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0, step0,
+                       action_mode, autoreset, traj ? *traj : kNoOut);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(h->ev1, h->stream));
+    h->timed = 1;
+    return 0;
+}
+
+int fjsp_gae(const double* rewards, const float* values, const uint8_t* done, const double* boot, int32_t T, int32_t N,
+             int32_t M, double gamma, double lamb, double* ret, double* adv, void* stream) {
+    if (T <= 0 || N <= 0 || M <= 0 || M % N) return fail("bad GAE shape (T > 0, N > 0, M multiple of N)");
+    if (!rewards || !values || !done || !boot || !ret || !adv) return fail("null GAE buffer");
+    dim3 grid((M + 255) / 256);
+    hipLaunchKernelGGL(k_gae, grid, dim3(256), 0, (hipStream_t)stream, rewards, values, done, boot, T, N, M, gamma, lamb,
+                       ret, adv);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int fjsp_sync(fjsp_handle* h) {
+    if (!h) return fail("null handle");
+    DeviceGuard g(h->device);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int fjsp_last_kernel_ms(fjsp_handle* h, float* ms) {
+    if (!h || !ms) return fail("null argument");
+    if (!h->timed) return fail("no timed launch yet");
+    DeviceGuard g(h->device);
+    HIPCHK(hipEventSynchronize(h->ev1));
+    HIPCHK(hipEventElapsedTime(ms, h->ev0, h->ev1));
+    return 0;
+}
+
+// MT19937 state exchange in numpy's (key[624], pos) convention (np.random.get_state()[1:3]).
+int fjsp_mt_get(fjsp_handle* h, int32_t env, uint32_t* key, int32_t* pos) {
+    if (!h || !key || !pos) return fail("null argument");
+    if (env < 0 || env >= h->n) return fail("env index out of range");
+    DeviceGuard g(h->device);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    uint32_t st = 0;
+    HIPCHK(hipMemcpy(&st, h->S.words + (size_t)3 * h->n + env, 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy2D(key, 4, h->S.mt + env, (size_t)h->n * 4, 4, MT_N, hipMemcpyDeviceToHost));
+    int mti = (int)(st & 0x3FF), gg = (int)((st >> 16) & 0x3FF);
+    if (gg == 0) { *pos = MT_N; return 0; }
+    for (int i = gg; i < MT_N; i++) {   // finish the in-place twist of the current block
+        const int i1 = (i + 1 == MT_N) ? 0 : i + 1;
+        const int im = (i + 397 >= MT_N) ? i + 397 - MT_N : i + 397;
+        const uint32_t y = (key[i] & 0x80000000u) | (key[i1] & 0x7fffffffu);
+        key[i] = key[im] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    *pos = mti;
+    return 0;
+}
+
+int fjsp_mt_set(fjsp_handle* h, int32_t env, const uint32_t* key, int32_t pos) {
+    if (!h || !key) return fail("null argument");
+    if (env < 0 || env >= h->n) return fail("env index out of range");
+    if (pos < 0 || pos > MT_N) return fail("pos must be in 0..624");
+    DeviceGuard g(h->device);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    const uint32_t st = pos >= MT_N ? 0u : ((uint32_t)pos | ((uint32_t)MT_N << 16));
+    HIPCHK(hipMemcpy2D(h->S.mt + env, (size_t)h->n * 4, key, 4, 4, MT_N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->S.words + (size_t)3 * h->n + env, &st, 4, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int fjsp_read_env(fjsp_handle* h, int32_t env, fjsp_env_view* v) {
+    if (!h || !v) return fail("null argument");
+    if (env < 0 || env >= h->n) return fail("env index out of range");
+    DeviceGuard g(h->device);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    uint32_t w[NWORDS];
+    uint32_t orders[MAX_ORDERS];
+    for (int i = 0; i < NWORDS; i++)
+        HIPCHK(hipMemcpy(&w[i], h->S.words + (size_t)i * h->n + env, 4, hipMemcpyDeviceToHost));
+    for (int i = 0; i < MAX_ORDERS; i++)
+        HIPCHK(hipMemcpy(&orders[i], h->S.orders + (size_t)i * h->n + env, 4, hipMemcpyDeviceToHost));
+    memset(v, 0, sizeof(*v));
+    v->current_step = (int32_t)(w[0] & 0xFFFF);
+    v->num_orders = (int32_t)((w[0] >> 16) & 0xFF);
+    v->next_order = (int32_t)(w[0] >> 24);
+    v->orders_completed = (int32_t)(w[1] & 0xFF);
+    v->total_packaged = (int32_t)(w[1] >> 8);
+    v->status = w[2];
+    const int loc = (int)(w[6] & 7), carry = (int)((w[6] >> 3) & 0xFF), code = (int)((w[6] >> 11) & 0x1FFF);
+    v->agv_row = loc == LOC_SMALL ? 2 : (loc >= LOC_STORAGE ? 3 : 0);
+    v->agv_col = (loc == LOC_PICKUP || loc == LOC_STORAGE) ? 0 : (loc == LOC_PACK ? 5 : 3);
+    v->agv_carrying = carry != NIL;
+    v->agv_tray_count = carry != NIL ? (code >> 10) & 7 : 0;
+    for (int i = 0; i < v->num_orders && i < MAX_ORDERS; i++) {
+        const uint32_t o = orders[i];
+        const uint32_t n = (o >> 20) & 15, full = (1u << n) - 1u;
+        const uint32_t pc = (uint32_t)__builtin_popcount(o & full), kc = (uint32_t)__builtin_popcount((o >> 9) & full);
+        v->orders[i] = n | (((o >> 24) & 3) << 4) | (((o >> 26) & 3) << 6) | (pc << 8) | (kc << 12) | (((o >> 18) & 1) << 16);
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,200 @@
+"""FJSPVecEnv — N reference environments stepped in lockstep on one MI355X.
+
+Device-resident tensors in, device-resident tensors out (zero copy through the C-ABI).
+All layouts are field-major SoA with the env index fastest ([F, N]), the layout the
+kernels write coalesced; ``.t()`` gives the [N, F] view a network consumes.
+"""
+import ctypes
+
+import torch
+
+from . import _native as nat
+from .spec import AGENTS
+
+NI32, NI8, NF32, NMASK, NA = 20, 12, 6, 29, 8
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Buffers:
+    """Output tensors for T steps of N envs (T = 1 for step/reset)."""
+
+    def __init__(self, T, N, device, infos=True, next_obs=False):
+        z = lambda *s, dt: torch.zeros(*s, dtype=dt, device=device)  # noqa: E731
+        self.obs_i32 = z(T, NI32, N, dt=torch.int32)
+        self.obs_i8 = z(T, NI8, N, dt=torch.int8)
+        self.obs_f32 = z(T, NF32, N, dt=torch.float32)
+        self.masks = z(T, NMASK, N, dt=torch.int8)
+        self.rewards = z(T, NA, N, dt=torch.float64)
+        self.term = z(T, N, dt=torch.uint8)
+        self.trunc = z(T, N, dt=torch.uint8)
+        self.status = z(T, N, dt=torch.int32)
+        if infos:
+            self.results = z(T, NA, N, dt=torch.int32)
+            self.orders_completed = z(T, N, dt=torch.int32)
+            self.packaged = z(T, N, dt=torch.int32)
+            self.sim_time = z(T, N, dt=torch.float64)
+        else:
+            self.results = self.orders_completed = self.packaged = self.sim_time = None
+        if next_obs:
+            self.next_i32 = z(T, NI32, N, dt=torch.int32)
+            self.next_i8 = z(T, NI8, N, dt=torch.int8)
+            self.next_f32 = z(T, NF32, N, dt=torch.float32)
+            self.next_masks = z(T, NMASK, N, dt=torch.int8)
+        else:
+            self.next_i32 = self.next_i8 = self.next_f32 = self.next_masks = None
+
+    def struct(self):
+        o = nat.fjsp_out()
+        for k in nat.OUT_FIELDS:
+            t = getattr(self, k, None)
+            setattr(o, k, t.data_ptr() if t is not None else None)
+        return o
+
+
+class FJSPVecEnv:
+    """N independent FJSP environments (reference semantics per env) on one GPU.
+
+    Env ``e`` has global id ``env_id_base + e``; its default MT19937 stream is
+    ``np.random.seed(global id)`` and synthetic actions are keyed by the global id, so
+    results do not depend on how envs are sharded over GPUs.
+    """
+
+    def __init__(self, num_envs, device=None, config=None, env_id_base=0, **cfg_over):
+        if not torch.cuda.is_available():
+            raise nat.FjspNativeError("FJSPVecEnv needs a GPU (HIP); no CPU fallback exists")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.num_envs = int(num_envs)
+        self.env_id_base = int(env_id_base)
+        c = config if config is not None else nat.default_config(**cfg_over)
+        self.config = c
+        L = nat.lib()
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            nat.check(L.fjsp_create(ctypes.byref(c), self.num_envs, self.device.index or 0,
+                                    ctypes.c_void_p(stream), ctypes.byref(h)))
+        self._h = h
+        self._step_buf = None
+        self._num_orders = 30
+        if self.env_id_base:
+            self.seed(torch.arange(self.env_id_base, self.env_id_base + self.num_envs, dtype=torch.int64))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                nat.lib().fjsp_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # ------------------------------------------------------------------ helpers
+    def _sync_stream(self):
+        nat.check(nat.lib().fjsp_set_stream(self._h, ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+
+    @property
+    def handle(self):
+        return self._h
+
+    def state_bytes_per_env(self):
+        return int(nat.lib().fjsp_state_bytes(self._h))
+
+    def seed(self, seeds):
+        """np.random.seed(seeds[e]) for every env (applied at the next reset)."""
+        self._pending_seeds = torch.as_tensor(seeds, device=self.device).to(torch.int64).bitwise_and(0xFFFFFFFF).to(torch.int32)
+
+    # ------------------------------------------------------------------ API
+    def reset(self, seeds=None, env_mask=None, num_orders=30, buffers=None):
+        """FJSPSimulation.reset for the selected envs (FJSPSimulation.py:286-323)."""
+        self._sync_stream()
+        self._num_orders = int(num_orders)
+        if seeds is None and getattr(self, "_pending_seeds", None) is not None:
+            seeds = self._pending_seeds
+        self._pending_seeds = None
+        s = None
+        if seeds is not None:
+            s = torch.as_tensor(seeds, device=self.device)
+            s = s.to(torch.int64).bitwise_and(0xFFFFFFFF).to(torch.int32).contiguous()
+        m = None
+        if env_mask is not None:
+            m = torch.as_tensor(env_mask, device=self.device).to(torch.uint8).contiguous()
+        b = buffers or Buffers(1, self.num_envs, self.device, infos=False)
+        out = b.struct()
+        nat.check(nat.lib().fjsp_reset(self._h, _ptr(s), _ptr(m), self._num_orders, ctypes.byref(out)))
+        return b
+
+    def step(self, actions, agent_order=None, autoreset=True, buffers=None):
+        """One FJSPSimulation.step per env (FJSPSimulation.py:144-242).
+
+        actions: uint8 tensor [8, N] (agent-major) on the env's device."""
+        self._sync_stream()
+        a = actions
+        if a.dtype != torch.uint8 or not a.is_contiguous() or a.device != self.device:
+            a = a.to(device=self.device, dtype=torch.uint8).contiguous()
+        if tuple(a.shape) != (NA, self.num_envs):
+            raise ValueError(f"actions must be [8, {self.num_envs}], got {tuple(a.shape)}")
+        if buffers is None:
+            if self._step_buf is None:
+                self._step_buf = Buffers(1, self.num_envs, self.device, infos=True, next_obs=True)
+            buffers = self._step_buf
+        order = None
+        if agent_order is not None:
+            order = (ctypes.c_uint8 * 8)(*[int(x) for x in agent_order])
+        out = buffers.struct()
+        nat.check(nat.lib().fjsp_step(self._h, _ptr(a), order, int(bool(autoreset)), ctypes.byref(out)))
+        return buffers
+
+    def rollout(self, K, action_seed=0, step0=0, masked=False, autoreset=True, buffers=None, infos=False):
+        """K fused steps with on-device synthetic actions; returns [K, F, N] trajectories."""
+        self._sync_stream()
+        b = buffers or Buffers(K, self.num_envs, self.device, infos=infos)
+        out = b.struct()
+        nat.check(nat.lib().fjsp_step_many(self._h, int(K), int(action_seed) & (2**64 - 1), self.env_id_base,
+                                           int(step0), 1 if masked else 0, int(bool(autoreset)), ctypes.byref(out)))
+        return b
+
+    def last_kernel_ms(self):
+        ms = ctypes.c_float()
+        nat.check(nat.lib().fjsp_last_kernel_ms(self._h, ctypes.byref(ms)))
+        return ms.value
+
+    def read_env(self, e):
+        v = nat.fjsp_env_view()
+        nat.check(nat.lib().fjsp_read_env(self._h, int(e), ctypes.byref(v)))
+        return v
+
+    def mt_get(self, e):
+        import numpy as np
+        key = np.zeros(624, np.uint32)
+        pos = ctypes.c_int32()
+        nat.check(nat.lib().fjsp_mt_get(self._h, int(e), ctypes.c_void_p(key.ctypes.data), ctypes.byref(pos)))
+        return key, pos.value
+
+    def mt_set(self, e, key, pos):
+        import numpy as np
+        k = np.ascontiguousarray(key, dtype=np.uint32)
+        nat.check(nat.lib().fjsp_mt_set(self._h, int(e), ctypes.c_void_p(k.ctypes.data), int(pos)))
+
+    def sync(self):
+        nat.check(nat.lib().fjsp_sync(self._h))
+
+
+def gae(rewards, values, done, boot, gamma, lamb, out_ret=None, out_adv=None):
+    """Returns + GAE (transition_memory.py:83-105) on device tensors.
+
+    rewards f64 [T, M], values f32 [T, M], done u8 [T, N], boot f64 [M]; columns m = a*N + e."""
+    T, M = rewards.shape
+    N = done.shape[1]
+    ret = out_ret if out_ret is not None else torch.empty_like(rewards)
+    adv = out_adv if out_adv is not None else torch.empty_like(rewards)
+    r = rewards.contiguous(); v = values.contiguous(); d = done.to(torch.uint8).contiguous(); b = boot.contiguous()
+    stream = torch.cuda.current_stream(rewards.device).cuda_stream
+    nat.check(nat.lib().fjsp_gae(_ptr(r), _ptr(v), _ptr(d), _ptr(b), T, N, M, float(gamma), float(lamb),
+                                 _ptr(ret), _ptr(adv), ctypes.c_void_p(stream)))
+    return ret, adv
+
+
+__all__ = ["FJSPVecEnv", "Buffers", "gae", "AGENTS"]

@@ -367,8 +367,10 @@ def gen_gae(tm_mod):
                                                    (37, [37], 0.9, 0.5)]):
         rewards = np.round(rng.normal(0, 3, size=(T, 8)) * 8) / 8  # like env rewards
         values = rng.normal(0, 5, size=(T, 8)).astype(np.float32)
+        # a2c semantics: episode ends bootstrap with 0.0 (a2c.py:357-358), the batch end with
+        # the critic's V(s) (a2c.py:324-332)
         boots = rng.normal(0, 5, size=(len(segs), 8)).astype(np.float32)
-        boots[-1] = 0.0
+        boots[:-1] = 0.0
         mem = tm_mod.MultiAgentTransitionMemory(AGENTS, gamma, lamb, True)
         start = 0
         for si, end in enumerate(segs):

@@ -1,0 +1,42 @@
+"""The C-ABI library loads on CPU and exports every symbol include/fjsp.h declares
+(no compute calls: there is no GPU in the build container)."""
+import ctypes
+import os
+import re
+
+from tests import gpu_util as G
+
+
+def _declared():
+    hdr = open(os.path.join(G.REPO, "include", "fjsp.h")).read()
+    return sorted(set(re.findall(r"^\w[\w\s\*]*?\b(fjsp_\w+)\s*\(", hdr, re.M)))
+
+
+def test_header_matches_binding_list():
+    assert _declared() == sorted(G.native.EXPORTS)
+
+
+def test_library_exports_every_symbol():
+    L = G.native.lib()
+    for name in _declared():
+        assert hasattr(L, name), name
+    assert L.fjsp_abi_version() == 1
+
+
+def test_config_validation_without_gpu():
+    nat = G.native
+    c = nat.default_config()
+    assert (c.num_trays, c.tray_capacity, c.step_size, c.max_episode_steps, c.pt_small, c.pt_big,
+            c.pt_packaging, c.packaging_capacity) == (1000, 5, 10, 200, 60, 120, 30, 20)
+    assert nat.lib().fjsp_check_config(ctypes.byref(c)) == 0
+    bad = nat.default_config(pt_small=65)
+    assert nat.lib().fjsp_check_config(ctypes.byref(bad)) != 0
+    assert b"multiple of step_size" in nat.lib().fjsp_last_error()
+    bad = nat.default_config(step_size=8)
+    assert nat.lib().fjsp_check_config(ctypes.byref(bad)) != 0
+
+
+def test_kernels_compiled_for_gfx950():
+    data = open(G.native.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+    assert b"k_step_many" in data or b"_Z" in data

@@ -1,0 +1,238 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the reference's golden fixtures and
+the CPU oracle.  Bit-exact for every integer field and for the fp64 rewards / GAE."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from oracle import oracle as O  # noqa: E402
+from tests import parity_util as P  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def G():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    from tests import gpu_util
+    return gpu_util
+
+
+def _groups(traces):
+    groups = {}
+    for tr in traces:
+        key = (tuple(sorted(tr.cfg.items())), tr.num_orders)
+        groups.setdefault(key, []).append(tr)
+    return groups
+
+
+def _replay_group(G, trs):
+    cfg = dict(trs[0].cfg)
+    n = len(trs)
+    env = G.make_env(n, **cfg)
+    seeds = torch.tensor([tr.seed for tr in trs], dtype=torch.int64)
+    b = env.reset(seeds=seeds, num_orders=trs[0].num_orders)
+    r = G.to_np(b)
+    for i, tr in enumerate(trs):
+        assert P.bits_equal(r["obs_i32"][0, i], tr.init_i32), tr.name
+        assert P.bits_equal(r["masks"][0, i], tr.init_masks), tr.name
+    T = min(tr.steps for tr in trs)
+    acts = np.stack([tr.actions[:T] for tr in trs], axis=2)   # [T, 8, n]
+    acts_d = torch.from_numpy(np.ascontiguousarray(acts)).cuda()
+    for t in range(T):
+        b = env.step(acts_d[t], autoreset=True)
+        r = G.to_np(b)
+        for i, tr in enumerate(trs):
+            for k in ("obs_i32", "obs_i8", "obs_f32", "masks", "rewards", "results"):
+                assert P.bits_equal(r[k][0, i], getattr(tr, k)[t]), (tr.name, t, k, r[k][0, i], getattr(tr, k)[t])
+            assert r["term"][0, i] == tr.term[t] and r["trunc"][0, i] == tr.trunc[t], (tr.name, t)
+            assert r["orders_completed"][0, i] == tr.orders_completed[t], (tr.name, t)
+            assert r["packaged"][0, i] == tr.packaged[t], (tr.name, t)
+            assert r["sim_time"][0, i] == tr.sim_time[t], (tr.name, t)
+            assert P.bits_equal(r["next_i32"][0, i], tr.reset_i32[t]), (tr.name, t, "reset obs")
+            assert P.bits_equal(r["next_masks"][0, i], tr.reset_masks[t]), (tr.name, t, "reset masks")
+            assert r["status"][0, i] & 1 == 0
+
+
+def test_golden_traces(G):
+    for key, trs in _groups(P.load_traces()).items():
+        _replay_group(G, trs)
+
+
+def test_golden_scenarios(G):
+    for key, trs in _groups(P.load_scenarios()).items():
+        _replay_group(G, trs)
+
+
+def test_digests_fused_rollout(G):
+    """256 envs x 1000 steps of the fused kernel with on-device actions vs the reference's digests."""
+    dg = P.load_digests()
+    n, steps, chunk = dg["n_envs"], dg["steps"], dg["chunk"]
+    env = G.make_env(n)
+    env.reset(seeds=torch.arange(n), num_orders=dg["num_orders"])
+    b = env.rollout(steps, action_seed=dg["action_seed"], step0=0, masked=False)
+    r = G.to_np(b)
+    for e in range(n):
+        row = P.chunk_digests(lambda t: (r["obs_i32"][t, e], r["obs_i8"][t, e], r["obs_f32"][t, e],
+                                         r["masks"][t, e], r["rewards"][t, e], r["term"][t, e],
+                                         r["trunc"][t, e]), steps, chunk)
+        assert row == dg["digests"][e], e
+
+
+@pytest.mark.parametrize("masked", [False, True])
+def test_fused_vs_oracle(G, masked):
+    """1024 envs x 400 steps, every field bit-exact against the oracle's event-heap restatement."""
+    n, steps, seed = 1024, 400, 12345
+    env = G.make_env(n)
+    env.reset(seeds=torch.arange(n) + 1000, num_orders=30)
+    b = env.rollout(steps, action_seed=seed, masked=masked, infos=True)
+    r = G.to_np(b)
+    rec, _, _ = O.rollout(n, steps, seeds=np.arange(n) + 1000, gid0=0, num_orders=30, action_seed=seed,
+                          policy=1 if masked else 0)
+    for k in ("obs_i32", "obs_i8", "obs_f32", "masks", "rewards", "results"):
+        assert P.bits_equal(r[k], rec[k]), k
+    for k in ("term", "trunc", "orders_completed", "packaged"):
+        assert np.array_equal(r[k], rec[k]), k
+
+
+def test_step_vs_fused(G):
+    """k_step with host-supplied actions == k_step_many with on-device actions."""
+    n, steps = 512, 120
+    a = G.make_env(n)
+    bb = G.make_env(n)
+    a.reset(seeds=torch.arange(n), num_orders=30)
+    bb.reset(seeds=torch.arange(n), num_orders=30)
+    tr = G.to_np(bb.rollout(steps, action_seed=7, masked=True))
+    acts = np.zeros((steps, 8, n), np.uint8)
+    masks = a.reset(seeds=torch.arange(n), num_orders=30).masks[0].t().cpu().numpy()
+    for t in range(steps):
+        for e in range(n):
+            acts[t, :, e] = O.actions(7, e, t, masks[e])
+        r = G.to_np(a.step(torch.from_numpy(acts[t]).cuda()))
+        assert P.bits_equal(r["obs_i32"][0], tr["obs_i32"][t]), t
+        assert P.bits_equal(r["rewards"][0], tr["rewards"][t]), t
+        masks = r["next_masks"][0]
+
+
+def test_agent_order_and_absent_agents(G):
+    """Non-canonical dict order and missing agents against the oracle (FJSPSimulation.py:172-205)."""
+    n, steps = 64, 200
+    rng = np.random.default_rng(3)
+    env = G.make_env(n)
+    env.reset(seeds=torch.arange(n), num_orders=30)
+    oracles = [O.OracleEnv() for _ in range(n)]
+    for e, o in enumerate(oracles):
+        o.reset(seed=e, num_orders=30)
+    for t in range(steps):
+        order = rng.permutation(8).astype(np.uint8)
+        acts = np.stack([O.actions(99, e, t) for e in range(n)], 1).astype(np.uint8)   # [8, n]
+        absent = rng.random((8, n)) < 0.1
+        acts[absent] = 255
+        weird = rng.random((8, n)) < 0.03
+        acts[weird] = rng.integers(3, 255, size=weird.sum())
+        r = G.to_np(env.step(torch.from_numpy(acts).cuda(), agent_order=order.tolist()))
+        for e in range(n):
+            ro = oracles[e].step(acts[:, e], order=order)
+            for k in ("obs_i32", "obs_i8", "obs_f32", "masks", "rewards", "results"):
+                assert P.bits_equal(r[k][0, e], ro[k]), (t, e, k, r[k][0, e], ro[k])
+            if ro["term"] or ro["trunc"]:
+                oracles[e].reset(num_orders=30)
+
+
+def test_gae_golden(G):
+    d = np.load(f"{P.GOLDEN}/gae.npz")
+    for c in range(3):
+        g, l = d[f"c{c}_gamma_lamb"]
+        rw, v, boots, se = d[f"c{c}_rewards"], d[f"c{c}_values"], d[f"c{c}_boots"], d[f"c{c}_seg_end"]
+        T = rw.shape[0]
+        # segments end at episode ends (next value 0) and at the batch end (bootstrap)
+        done = se.copy()
+        done[-1] = 0
+        ret, adv = G.vec_env.gae(torch.from_numpy(rw).cuda(), torch.from_numpy(v).cuda(),
+                                 torch.from_numpy(done.reshape(T, 1)).cuda(),
+                                 torch.from_numpy(boots[-1].astype(np.float64)).cuda(), g, l)
+        assert P.bits_equal(ret.cpu().numpy(), d[f"c{c}_returns"]), c
+        assert P.bits_equal(adv.cpu().numpy(), d[f"c{c}_adv"]), c
+
+
+def test_gae_vs_oracle_large(G):
+    """T=256, 4096 envs x 8 agents with episode boundaries: bit-exact vs the oracle scan."""
+    T, N = 256, 4096
+    M = 8 * N
+    rng = np.random.default_rng(11)
+    rw = np.round(rng.normal(0, 3, size=(T, M)) * 8) / 8
+    v = rng.normal(0, 5, size=(T, M)).astype(np.float32)
+    done = (rng.random((T, N)) < 0.01).astype(np.uint8)
+    boot = rng.normal(0, 5, size=M)
+    ret, adv = G.vec_env.gae(torch.from_numpy(rw).cuda(), torch.from_numpy(v).cuda(), torch.from_numpy(done).cuda(),
+                             torch.from_numpy(boot).cuda(), 0.99, 0.95)
+    ret, adv = ret.cpu().numpy(), adv.cpu().numpy()
+    cols = rng.choice(M, 64, replace=False)
+    for m in cols:
+        e = m % N
+        se = done[:, e].copy()
+        se[-1] = 1
+        nseg = int(se.sum())
+        boots = np.zeros(nseg)
+        if not done[-1, e]:
+            boots[-1] = boot[m]
+        rr, aa = O.gae(rw[:, m:m + 1], v[:, m:m + 1], boots.reshape(-1, 1), se, 0.99, 0.95)
+        assert P.bits_equal(ret[:, m], rr[:, 0]), m
+        assert P.bits_equal(adv[:, m], aa[:, 0]), m
+
+
+def test_reset_tables_and_read_env(G):
+    d = np.load(f"{P.GOLDEN}/reset_tables.npz")
+    n = 256
+    env = G.make_env(n)
+    env.reset(seeds=torch.arange(n), num_orders=30)
+    for s in range(0, n, 17):
+        v = env.read_env(s)
+        o = np.array(v.orders[:30], np.uint32)
+        got = np.stack([o & 15, (o >> 4) & 3, (o >> 6) & 3], 1).astype(np.uint8)
+        assert np.array_equal(got, d["seeded"][s]), s
+        assert v.num_orders == 30 and v.current_step == 0
+
+
+def test_mt_exchange_matches_numpy(G):
+    """fjsp_mt_set/get + reset consume numpy's global stream exactly (FJSPSimulation.py:107-112)."""
+    env = G.make_env(3)
+    for s in (0, 5, 2**31 + 7):
+        rs = np.random.RandomState(s)
+        rs.randint(0, 100, size=int(s % 700))   # arbitrary position inside a block
+        st = rs.get_state()
+        env.mt_set(1, st[1], st[2])
+        env.reset(seeds=None, env_mask=torch.tensor([0, 1, 0], dtype=torch.uint8), num_orders=25)
+        exp = [(rs.randint(1, 10), rs.randint(0, 3) + 1, rs.randint(0, 3) + 1) for _ in range(25)]
+        v = env.read_env(1)
+        o = np.array(v.orders[:25], np.uint32)
+        got = list(zip((o & 15).tolist(), ((o >> 4) & 3).tolist(), ((o >> 6) & 3).tolist()))
+        assert got == exp
+        key, pos = env.mt_get(1)
+        st2 = rs.get_state()
+        assert pos == st2[2] and np.array_equal(key, st2[1])
+
+
+def test_full_size_properties(G):
+    """4096 envs x 1000 steps (the benchmark workload): size-independent invariants plus exact
+    parity of a sampled subset of envs against the oracle."""
+    n, steps = 4096, 1000
+    env = G.make_env(n)
+    env.reset(seeds=torch.arange(n), num_orders=30)
+    b = env.rollout(steps, action_seed=2024, masked=False)
+    torch.cuda.synchronize()
+    masks = b.masks
+    assert bool((masks[:, [0, 3, 11, 14, 17, 20, 23, 26], :] == 1).all())
+    trunc = b.trunc.cpu().numpy()
+    # all envs started together and never terminate under random actions -> truncation every 201 steps
+    assert np.array_equal(np.nonzero(trunc[:, 0])[0], np.array([200, 401, 602, 803]))
+    assert bool((b.trunc[:, 0:1] == b.trunc).all())
+    assert int(b.status.bitwise_and(1).sum()) == 0
+    # sampled exact parity
+    for e in np.arange(0, n, 97)[:8]:
+        r1, _, _ = O.rollout(1, steps, seeds=[e], gid0=int(e), num_orders=30, action_seed=2024, policy=0)
+        got = b.rewards[:, :, e].cpu().numpy()
+        assert P.bits_equal(got, r1["rewards"][:, 0]), e
+        got = b.obs_i32[:, :, e].cpu().numpy()
+        assert P.bits_equal(got, r1["obs_i32"][:, 0]), e
