@@ -69,6 +69,28 @@ typedef struct fjsp_config {
     int32_t packaging_capacity; /* simpy.Resource(capacity=20) (PackagingAgent.py:46) */
 } fjsp_config;
 
+/* RewardModel weights (utils/RewardModel.py:12-32; a dataclass of tunable fp64 fields).
+ * Rewards: g = ORDER*orders_done + THROUGHPUT*packaged + TIME*step_size (calculate_global_reward),
+ * r_a = g / 8 + local_a (combine_rewards), local sums in calculate_local_reward's order. */
+typedef struct fjsp_reward_weights {
+    double order_complete_reward;     /* 100.0 */
+    double throughput_bonus;          /* 10.0 */
+    double time_penalty;              /* -0.1 */
+    double pickup_load_reward;        /* 1.0 */
+    double pickup_tray_complete;      /* 5.0 */
+    double pickup_idle_penalty;       /* -1.0 */
+    double agv_delivery_reward;       /* 2.0 */
+    double agv_move_penalty;          /* -0.1 */
+    double agv_packaging_delivery;    /* 10.0 */
+    double agv_invalid_action;        /* -5.0 */
+    double machine_complete_reward;   /* 5.0 */
+    double machine_start_reward;      /* 1.0 */
+    double machine_idle_penalty;      /* -2.0 */
+    double packaging_complete_reward; /* 20.0 */
+    double packaging_start_reward;    /* 2.0 */
+    double packaging_idle_penalty;    /* -1.0 */
+} fjsp_reward_weights;
+
 /* Output buffers (device pointers).  Each array is [T][F][N] (field-major SoA, N fastest);
  * T = 1 for fjsp_reset / fjsp_step, K for fjsp_step_many.  Any pointer may be NULL (skip). */
 typedef struct fjsp_out {
@@ -111,6 +133,9 @@ typedef struct fjsp_handle fjsp_handle;
 int fjsp_abi_version(void);
 const char* fjsp_last_error(void);
 int fjsp_default_config(fjsp_config* cfg);
+int fjsp_default_reward_weights(fjsp_reward_weights* w);
+/* Replace the handle's reward weights (takes effect at the next launch). */
+int fjsp_set_reward_weights(fjsp_handle* h, const fjsp_reward_weights* w);
 /* Validate a config (0 = usable by the closed-form kernels). */
 int fjsp_check_config(const fjsp_config* cfg);
 
@@ -118,6 +143,9 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
                 fjsp_handle** out);
 int fjsp_destroy(fjsp_handle* h);
 int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
+/* Tuning knobs: "fused_lds" (0/1; default 1 when num_envs <= 16384: stage the per-env tables
+ * of k_step_many in LDS, one 64-env workgroup per CU). */
+int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value);
 int fjsp_num_envs(const fjsp_handle* h);
 /* Bytes of device state per env (HBM footprint of the SoA state). */
 int64_t fjsp_state_bytes(const fjsp_handle* h);

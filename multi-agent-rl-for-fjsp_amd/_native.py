@@ -28,6 +28,17 @@ class fjsp_config(ctypes.Structure):
         "max_episode_steps", "agv_speed", "pt_small", "pt_big", "pt_packaging", "packaging_capacity")]
 
 
+REWARD_FIELDS = ["order_complete_reward", "throughput_bonus", "time_penalty", "pickup_load_reward",
+                 "pickup_tray_complete", "pickup_idle_penalty", "agv_delivery_reward", "agv_move_penalty",
+                 "agv_packaging_delivery", "agv_invalid_action", "machine_complete_reward", "machine_start_reward",
+                 "machine_idle_penalty", "packaging_complete_reward", "packaging_start_reward",
+                 "packaging_idle_penalty"]
+
+
+class fjsp_reward_weights(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_double) for k in REWARD_FIELDS]
+
+
 OUT_FIELDS = ["obs_i32", "obs_i8", "obs_f32", "masks", "rewards", "term", "trunc", "results",
               "orders_completed", "packaged", "sim_time", "status",
               "next_i32", "next_i8", "next_f32", "next_masks"]
@@ -46,7 +57,8 @@ class fjsp_env_view(ctypes.Structure):
 
 # every symbol include/fjsp.h declares (checked by tests/test_abi.py)
 EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_check_config",
-           "fjsp_create", "fjsp_destroy", "fjsp_set_stream", "fjsp_num_envs", "fjsp_state_bytes",
+           "fjsp_default_reward_weights", "fjsp_set_reward_weights",
+           "fjsp_create", "fjsp_destroy", "fjsp_set_stream", "fjsp_set_option", "fjsp_num_envs", "fjsp_state_bytes",
            "fjsp_reset", "fjsp_step", "fjsp_step_many", "fjsp_gae", "fjsp_mt_get", "fjsp_mt_set",
            "fjsp_read_env", "fjsp_sync", "fjsp_last_kernel_ms"]
 
@@ -89,9 +101,12 @@ def lib():
         "fjsp_last_error": (ctypes.c_char_p, []),
         "fjsp_default_config": (I, [ctypes.POINTER(fjsp_config)]),
         "fjsp_check_config": (I, [ctypes.POINTER(fjsp_config)]),
+        "fjsp_default_reward_weights": (I, [ctypes.POINTER(fjsp_reward_weights)]),
+        "fjsp_set_reward_weights": (I, [P, ctypes.POINTER(fjsp_reward_weights)]),
         "fjsp_create": (I, [ctypes.POINTER(fjsp_config), I, I, P, ctypes.POINTER(P)]),
         "fjsp_destroy": (I, [P]),
         "fjsp_set_stream": (I, [P, P]),
+        "fjsp_set_option": (I, [P, ctypes.c_char_p, ctypes.c_int64]),
         "fjsp_num_envs": (I, [P]),
         "fjsp_state_bytes": (ctypes.c_int64, [P]),
         "fjsp_reset": (I, [P, P, P, I, ctypes.POINTER(fjsp_out)]),

@@ -61,9 +61,15 @@ FJSP_DEV int tc_count(int c) { return (c >> 10) & 7; }
 FJSP_DEV int tc_make(int o, int s, int n) { return o | (s << 6) | (n << 10); }
 FJSP_DEV uint32_t tc_range(int c) { return ((1u << tc_count(c)) - 1u) << tc_start(c); }
 
+// RewardModel weights (utils/RewardModel.py:12-32), in fjsp_reward_weights field order.
+enum : int { W_ORDER = 0, W_THROUGHPUT, W_TIME, W_PICK_LOAD, W_PICK_TRAY, W_PICK_IDLE, W_AGV_DELIVERY, W_AGV_MOVE,
+             W_AGV_PACKAGING, W_AGV_INVALID, W_M_COMPLETE, W_M_START, W_M_IDLE, W_P_COMPLETE, W_P_START, W_P_IDLE,
+             NW };
+
 struct Cfg {
     int step_size, max_steps, tray_cap, mask_tray_cap, storage_cap, pool0, pkg_cap;
     int ptk_small, ptk_big, ptk_pack;   // processing times in steps
+    double w[NW];
 };
 
 // status bits (include/fjsp.h)
@@ -537,33 +543,33 @@ FJSP_DEV void env_step(Env& E, const Tables& T, const Cfg& C, const int* act, co
     pack_run<3>(E, T, C, p_started[3], &orders_done);
     E.ncompleted += orders_done;
     // 3-4. rewards (RewardModel.calculate_global_reward / calculate_local_reward / combine)
-    double g = 100.0 * (double)orders_done;
-    g += 10.0 * (double)(E.total_packaged - products_before);
-    g += -0.1 * (double)C.step_size;
-    const double g8 = g / 8.0;
+    double g = C.w[W_ORDER] * (double)orders_done;
+    g += C.w[W_THROUGHPUT] * (double)(E.total_packaged - products_before);
+    g += C.w[W_TIME] * (double)C.step_size;
+    const double g8 = g / 8.0;   // combine_rewards: global / len(self.agents)
 #pragma unroll
     for (int a = 0; a < NA; a++) {
         const uint32_t r = res[a];
         const int a0 = act[a] == 0;   // actions.get(agent_id, 0) == 0 (absent agents: r == 0)
         double loc = 0.0;
         if (a == 0) {
-            if (r & 2u) loc += 1.0;
-            if (r & 4u) loc += 5.0;
-            if (a0 && (r & 8u)) loc += -1.0;
+            if (r & 2u) loc += C.w[W_PICK_LOAD];
+            if (r & 4u) loc += C.w[W_PICK_TRAY];
+            if (a0 && (r & 8u)) loc += C.w[W_PICK_IDLE];
         } else if (a == 1) {
-            if (r & 8u) loc += 2.0;
-            if (r & 16u) loc += 2.0;
-            if (r & 32u) loc += 10.0;
-            if (r & 4u) loc += -0.1;
-            if (r & 2u) loc += -5.0;
+            if (r & 8u) loc += C.w[W_AGV_DELIVERY];
+            if (r & 16u) loc += C.w[W_AGV_DELIVERY];
+            if (r & 32u) loc += C.w[W_AGV_PACKAGING];
+            if (r & 4u) loc += C.w[W_AGV_MOVE];
+            if (r & 2u) loc += C.w[W_AGV_INVALID];
         } else if (a <= 3) {
-            if (r & 2u) loc += 1.0;
-            if (r & 4u) loc += 5.0;
-            if (a0 && (r & 8u)) loc += -2.0;
+            if (r & 2u) loc += C.w[W_M_START];
+            if (r & 4u) loc += C.w[W_M_COMPLETE];
+            if (a0 && (r & 8u)) loc += C.w[W_M_IDLE];
         } else {
-            if (r & 2u) loc += 2.0;
-            if (r & 4u) loc += 20.0;
-            if (a0 && (r & 8u)) loc += -1.0;
+            if (r & 2u) loc += C.w[W_P_START];
+            if (r & 4u) loc += C.w[W_P_COMPLETE];
+            if (a0 && (r & 8u)) loc += C.w[W_P_IDLE];
         }
         rew[a] = g8 + loc;
     }

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <string>
 
@@ -179,23 +180,29 @@ __device__ __forceinline__ Tables tables_of(const DevState& S, int e) {
     return T;
 }
 
-__device__ __forceinline__ void write_obs(const Obs& o, int32_t* i32, int8_t* i8, float* f32, int8_t* mk, size_t base_t,
-                                          int n, int e) {
+// Output byte offsets are 32-bit (the host checks every output slab is < 4 GiB), so the
+// stores use the SGPR-base + 32-bit VGPR-offset form instead of 64-bit per-lane addresses.
+template <class V>
+__device__ __forceinline__ void st32(V* base, uint32_t elem, V v) {
+    *reinterpret_cast<V*>(reinterpret_cast<char*>(base) + elem * (uint32_t)sizeof(V)) = v;
+}
+__device__ __forceinline__ void write_obs(const Obs& o, int32_t* i32, int8_t* i8, float* f32, int8_t* mk, uint32_t t,
+                                          uint32_t n, uint32_t e) {
     if (i32) {
 #pragma unroll
-        for (int f = 0; f < NI32; f++) i32[(base_t * NI32 + f) * n + e] = o.i32[f];
+        for (uint32_t f = 0; f < NI32; f++) st32(i32, (t * NI32 + f) * n + e, o.i32[f]);
     }
     if (i8) {
 #pragma unroll
-        for (int f = 0; f < NI8; f++) i8[(base_t * NI8 + f) * n + e] = o.i8[f];
+        for (uint32_t f = 0; f < NI8; f++) st32(i8, (t * NI8 + f) * n + e, o.i8[f]);
     }
     if (f32) {
 #pragma unroll
-        for (int f = 0; f < NF32; f++) f32[(base_t * NF32 + f) * n + e] = o.f32[f];
+        for (uint32_t f = 0; f < NF32; f++) st32(f32, (t * NF32 + f) * n + e, o.f32[f]);
     }
     if (mk) {
 #pragma unroll
-        for (int f = 0; f < NMASK; f++) mk[(base_t * NMASK + f) * n + e] = o.mask[f];
+        for (uint32_t f = 0; f < NMASK; f++) st32(mk, (t * NMASK + f) * n + e, o.mask[f]);
     }
 }
 
@@ -220,7 +227,7 @@ __global__ void __launch_bounds__(BLOCK) k_reset(DevState S, Cfg C, const uint32
     env_store(E, S.words, S.n, e);
     Obs o;
     observe(E, C, o);
-    write_obs(o, out.obs_i32, out.obs_i8, out.obs_f32, out.masks, 0, S.n, e);
+    write_obs(o, out.obs_i32, out.obs_i8, out.obs_f32, out.masks, 0u, (uint32_t)S.n, (uint32_t)e);
     if (out.status) out.status[e] = E.status;
 }
 
@@ -263,8 +270,8 @@ __device__ __forceinline__ void synth_actions(uint64_t seed, uint32_t gid, uint3
 template <bool CANON>
 __device__ __forceinline__ void step_and_emit(Env& E, const Tables& T, const Cfg& C, const DevState& S, int e,
                                               const int* act, const uint8_t* order, int autoreset, const fjsp_out& out,
-                                              size_t t) {
-    const int n = S.n;
+                                              uint32_t t) {
+    const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
     uint32_t res[NA];
     double rew[NA];
     env_step<CANON>(E, T, C, act, order, res, rew);
@@ -272,27 +279,27 @@ __device__ __forceinline__ void step_and_emit(Env& E, const Tables& T, const Cfg
     observe(E, C, o);
     const int all_done = E.ncompleted == E.norders && E.norders > 0 && E.next_order == E.norders;
     const int truncated = E.step >= C.max_steps;
-    write_obs(o, out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, e);
+    write_obs(o, out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, ue);
     if (out.rewards) {
 #pragma unroll
-        for (int a = 0; a < NA; a++) out.rewards[(t * NA + a) * n + e] = rew[a];
+        for (int a = 0; a < NA; a++) st32(out.rewards, (t * NA + (uint32_t)a) * n + ue, rew[a]);
     }
     if (out.results) {
 #pragma unroll
-        for (int a = 0; a < NA; a++) out.results[(t * NA + a) * n + e] = res[a];
+        for (int a = 0; a < NA; a++) st32(out.results, (t * NA + (uint32_t)a) * n + ue, res[a]);
     }
-    if (out.term) out.term[t * n + e] = (uint8_t)all_done;
-    if (out.trunc) out.trunc[t * n + e] = (uint8_t)truncated;
-    if (out.orders_completed) out.orders_completed[t * n + e] = E.ncompleted;
-    if (out.packaged) out.packaged[t * n + e] = E.total_packaged;
-    if (out.sim_time) out.sim_time[t * n + e] = (double)(E.step + 1) * (double)C.step_size;
-    if (out.status) out.status[t * n + e] = E.status;
+    if (out.term) st32(out.term, t * n + ue, (uint8_t)all_done);
+    if (out.trunc) st32(out.trunc, t * n + ue, (uint8_t)truncated);
+    if (out.orders_completed) st32(out.orders_completed, t * n + ue, E.ncompleted);
+    if (out.packaged) st32(out.packaged, t * n + ue, E.total_packaged);
+    if (out.sim_time) st32(out.sim_time, t * n + ue, (double)(E.step + 1) * (double)C.step_size);
+    if (out.status) st32(out.status, t * n + ue, E.status);
     E.step += 1;
     if (autoreset && (all_done || truncated)) {
         env_reset(E, T, C, S, e, E.norders);   // reset(seed=None) continues the MT stream
         observe(E, C, o);
     }
-    write_obs(o, out.next_i32, out.next_i8, out.next_f32, out.next_masks, t, n, e);
+    write_obs(o, out.next_i32, out.next_i8, out.next_f32, out.next_masks, t, n, ue);
 }
 
 template <bool CANON>
@@ -313,17 +320,50 @@ __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t
     env_store(E, S.words, S.n, e);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0,
-                                                     int mode, int autoreset, fjsp_out out) {
-    const int e = blockIdx.x * BLOCK + threadIdx.x;
+// K fused steps.  LDS = true stages the env's order table and tray-slot arena in LDS for
+// the whole launch (one 64-lane workgroup = 64 envs, 97.5 KB of LDS), so the linked-list
+// walks and order-word read-modify-writes of the step are ds_* round trips (~100 cycles)
+// instead of L2/HBM round trips; only the used prefix is copied in and out.
+template <bool LDS>
+__global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0,
+                                                     uint32_t step0, int mode, int autoreset, fjsp_out out) {
+    __shared__ uint32_t s_orders[LDS ? MAX_ORDERS * BLOCK : 1];
+    __shared__ uint16_t s_code[LDS ? MAX_SLOTS * BLOCK : 1];
+    __shared__ uint8_t s_next[LDS ? MAX_SLOTS * BLOCK : 1];
+    __shared__ uint16_t s_cstep[LDS ? MAX_SLOTS * BLOCK : 1];
+    const int lane = threadIdx.x;
+    const int e = blockIdx.x * BLOCK + lane;
     if (e >= S.n) return;
-    Tables T = tables_of(S, e);
     Env E;
     env_load(E, S.words, S.n, e);
+    Tables T;
+    if constexpr (LDS) {
+        T.orders = s_orders + lane;
+        T.scode = s_code + lane;
+        T.snext = s_next + lane;
+        T.scstep = s_cstep + lane;
+        T.stride = BLOCK;
+        for (int o = 0; o < E.norders; o++) T.orders[o * BLOCK] = S.orders[(size_t)o * S.n + e];
+        for (int s = 0; s < E.slot_next; s++) {
+            T.scode[s * BLOCK] = S.scode[(size_t)s * S.n + e];
+            T.snext[s * BLOCK] = S.snext[(size_t)s * S.n + e];
+            T.scstep[s * BLOCK] = S.scstep[(size_t)s * S.n + e];
+        }
+    } else {
+        T = tables_of(S, e);
+    }
     for (int k = 0; k < K; k++) {
         int act[NA];
         synth_actions(seed, gid0 + (uint32_t)e, step0 + (uint32_t)k, mode, E, C, act);
-        step_and_emit<true>(E, T, C, S, e, act, nullptr, autoreset, out, (size_t)k);
+        step_and_emit<true>(E, T, C, S, e, act, nullptr, autoreset, out, (uint32_t)k);
+    }
+    if constexpr (LDS) {
+        for (int o = 0; o < E.norders; o++) S.orders[(size_t)o * S.n + e] = T.orders[o * BLOCK];
+        for (int s = 0; s < E.slot_next; s++) {
+            S.scode[(size_t)s * S.n + e] = T.scode[s * BLOCK];
+            S.snext[(size_t)s * S.n + e] = T.snext[s * BLOCK];
+            S.scstep[(size_t)s * S.n + e] = T.scstep[s * BLOCK];
+        }
     }
     env_store(E, S.words, S.n, e);
 }
@@ -371,6 +411,7 @@ struct fjsp_handle {
     int has_reset;
     hipEvent_t ev0, ev1;
     int timed;
+    int use_lds;   // fused kernel variant (FJSP_FUSED_LDS env var / fjsp_set_option)
 };
 
 static thread_local std::string g_err;
@@ -424,6 +465,20 @@ int fjsp_default_config(fjsp_config* c) {
     return 0;
 }
 
+int fjsp_default_reward_weights(fjsp_reward_weights* w) {
+    if (!w) return fail("null weights");
+    const double d[NW] = {100.0, 10.0, -0.1, 1.0, 5.0, -1.0, 2.0, -0.1, 10.0, -5.0, 5.0, 1.0, -2.0, 20.0, 2.0, -1.0};
+    static_assert(sizeof(fjsp_reward_weights) == sizeof(double) * NW, "reward weight layout");
+    memcpy(w, d, sizeof(d));
+    return 0;
+}
+
+int fjsp_set_reward_weights(fjsp_handle* h, const fjsp_reward_weights* w) {
+    if (!h || !w) return fail("null argument");
+    memcpy(h->dcfg.w, w, sizeof(h->dcfg.w));
+    return 0;
+}
+
 int fjsp_check_config(const fjsp_config* c) {
     if (!c) return fail("null config");
     if (c->step_size <= 0) return fail("step_size must be > 0");
@@ -453,6 +508,12 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     h->n = num_envs;
     h->device = device;
     h->stream = (hipStream_t)hip_stream;
+    {
+        // the LDS variant holds 97.5 KB per 64-env workgroup (one workgroup per CU): use it
+        // only while every workgroup gets a CU of its own (256 CUs x 64 envs)
+        const char* v = getenv("FJSP_FUSED_LDS");
+        h->use_lds = v ? atoi(v) : (num_envs <= 256 * BLOCK);
+    }
     h->dcfg.step_size = c.step_size;
     h->dcfg.max_steps = c.max_episode_steps;
     h->dcfg.tray_cap = c.tray_capacity;
@@ -463,6 +524,11 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     h->dcfg.ptk_small = c.pt_small / c.step_size;
     h->dcfg.ptk_big = c.pt_big / c.step_size;
     h->dcfg.ptk_pack = c.pt_packaging / c.step_size;
+    {
+        fjsp_reward_weights w;
+        fjsp_default_reward_weights(&w);
+        memcpy(h->dcfg.w, &w, sizeof(h->dcfg.w));
+    }
     const size_t n = (size_t)num_envs;
     const size_t b_words = (size_t)NWORDS * n * 4, b_orders = (size_t)MAX_ORDERS * n * 4;
     const size_t b_scode = (size_t)MAX_SLOTS * n * 2, b_snext = (size_t)MAX_SLOTS * n, b_scstep = (size_t)MAX_SLOTS * n * 2;
@@ -501,6 +567,12 @@ int fjsp_destroy(fjsp_handle* h) {
     (void)hipFree(h->base);
     delete h;
     return 0;
+}
+
+int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
+    if (!h || !name) return fail("null argument");
+    if (!strcmp(name, "fused_lds")) { h->use_lds = value != 0; return 0; }
+    return fail("unknown option");
 }
 
 int fjsp_set_stream(fjsp_handle* h, void* s) {
@@ -562,11 +634,16 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
     if (action_mode != FJSP_ACTIONS_UNMASKED && action_mode != FJSP_ACTIONS_MASKED) return fail("bad action_mode");
     if (!h->has_reset) return fail("fjsp_step_many before fjsp_reset");
     if (K == 0) return 0;
+    if ((uint64_t)K * (uint64_t)h->n * 64ull >= (1ull << 32)) return fail("K * num_envs too large for one launch (< 2^26)");
     DeviceGuard g(h->device);
     dim3 grid((h->n + BLOCK - 1) / BLOCK);
     HIPCHK(hipEventRecord(h->ev0, h->stream));
-    hipLaunchKernelGGL(k_step_many, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0, step0,
-                       action_mode, autoreset, traj ? *traj : kNoOut);
+    if (h->use_lds)
+        hipLaunchKernelGGL(k_step_many<true>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0,
+                           step0, action_mode, autoreset, traj ? *traj : kNoOut);
+    else
+        hipLaunchKernelGGL(k_step_many<false>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0,
+                           step0, action_mode, autoreset, traj ? *traj : kNoOut);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(h->ev1, h->stream));
     h->timed = 1;

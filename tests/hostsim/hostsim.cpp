@@ -39,6 +39,8 @@ void* hs_create(const int32_t* c, int n) {
     h->C.step_size = c[4]; h->C.max_steps = c[5]; h->C.tray_cap = c[1]; h->C.mask_tray_cap = c[2];
     h->C.storage_cap = c[3]; h->C.pool0 = c[0] < 1000 ? c[0] : 1000; h->C.pkg_cap = c[10];
     h->C.ptk_small = c[7] / c[4]; h->C.ptk_big = c[8] / c[4]; h->C.ptk_pack = c[9] / c[4];
+    const double w[NW] = {100.0, 10.0, -0.1, 1.0, 5.0, -1.0, 2.0, -0.1, 10.0, -5.0, 5.0, 1.0, -2.0, 20.0, 2.0, -1.0};
+    for (int i = 0; i < NW; i++) h->C.w[i] = w[i];
     h->E = (Env*)calloc(n, sizeof(Env));
     h->orders = (uint32_t*)calloc((size_t)MAX_ORDERS * n, 4);
     h->scode = (uint16_t*)calloc((size_t)MAX_SLOTS * n, 2);

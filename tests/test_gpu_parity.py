@@ -236,3 +236,19 @@ def test_full_size_properties(G):
         assert P.bits_equal(got, r1["rewards"][:, 0]), e
         got = b.obs_i32[:, :, e].cpu().numpy()
         assert P.bits_equal(got, r1["obs_i32"][:, 0]), e
+
+
+def test_fused_lds_matches_global_tables(G):
+    """The LDS-staged fused kernel and the global-table variant produce identical bytes."""
+    n, steps = 2048, 450
+    outs = []
+    for lds in (0, 1):
+        env = G.make_env(n)
+        G.native.check(G.native.lib().fjsp_set_option(env.handle, b"fused_lds", lds))
+        env.reset(seeds=torch.arange(n) * 7, num_orders=12)
+        r1 = G.to_np(env.rollout(steps // 2, action_seed=3, masked=True, infos=True))
+        r2 = G.to_np(env.rollout(steps - steps // 2, action_seed=3, step0=steps // 2, masked=True, infos=True))
+        outs.append((r1, r2))
+    for k in outs[0][0]:
+        assert P.bits_equal(outs[0][0][k], outs[1][0][k]), k
+        assert P.bits_equal(outs[0][1][k], outs[1][1][k]), k
