@@ -186,6 +186,11 @@ int fjsp_gae(const double* rewards, const float* values, const uint8_t* done, co
 int fjsp_mt_get(fjsp_handle* h, int32_t env, uint32_t* key, int32_t* pos);
 int fjsp_mt_set(fjsp_handle* h, int32_t env, const uint32_t* key, int32_t pos);
 
+/* Same scan with fp64 values (transition_memory accepts arbitrary Python floats). */
+int fjsp_gae_f64(const double* rewards, const double* values, const uint8_t* done, const double* boot,
+                 int32_t T, int32_t N, int32_t M, double gamma, double lamb, double* ret, double* adv,
+                 void* hip_stream);
+
 /* Synchronous host copy of one env's state summary (debug / facade use). */
 int fjsp_read_env(fjsp_handle* h, int32_t env, fjsp_env_view* out);
 /* Wait for all work queued on the handle's stream. */

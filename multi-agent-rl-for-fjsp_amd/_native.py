@@ -59,7 +59,7 @@ class fjsp_env_view(ctypes.Structure):
 EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_check_config",
            "fjsp_default_reward_weights", "fjsp_set_reward_weights",
            "fjsp_create", "fjsp_destroy", "fjsp_set_stream", "fjsp_set_option", "fjsp_num_envs", "fjsp_state_bytes",
-           "fjsp_reset", "fjsp_step", "fjsp_step_many", "fjsp_gae", "fjsp_mt_get", "fjsp_mt_set",
+           "fjsp_reset", "fjsp_step", "fjsp_step_many", "fjsp_gae", "fjsp_gae_f64", "fjsp_mt_get", "fjsp_mt_set",
            "fjsp_read_env", "fjsp_sync", "fjsp_last_kernel_ms"]
 
 _lib = None
@@ -113,6 +113,7 @@ def lib():
         "fjsp_step": (I, [P, P, P, I, ctypes.POINTER(fjsp_out)]),
         "fjsp_step_many": (I, [P, I, U64, U32, U32, I, I, ctypes.POINTER(fjsp_out)]),
         "fjsp_gae": (I, [P, P, P, P, I, I, I, D, D, P, P, P]),
+        "fjsp_gae_f64": (I, [P, P, P, P, I, I, I, D, D, P, P, P]),
         "fjsp_mt_get": (I, [P, I, P, ctypes.POINTER(I)]),
         "fjsp_mt_set": (I, [P, I, P, I]),
         "fjsp_read_env": (I, [P, I, ctypes.POINTER(fjsp_env_view)]),

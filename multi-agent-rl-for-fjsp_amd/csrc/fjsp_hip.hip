@@ -369,7 +369,8 @@ __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, u
 }
 
 // transition_memory.py:83-105 over a [T][M] rollout buffer; column m = a*N + e
-__global__ void __launch_bounds__(256) k_gae(const double* __restrict__ r, const float* __restrict__ v,
+template <class VT>
+__global__ void __launch_bounds__(256) k_gae(const double* __restrict__ r, const VT* __restrict__ v,
                                              const uint8_t* __restrict__ done, const double* __restrict__ boot, int T,
                                              int N, int M, double gamma, double lamb, double* __restrict__ ret,
                                              double* __restrict__ adv) {
@@ -655,8 +656,19 @@ int fjsp_gae(const double* rewards, const float* values, const uint8_t* done, co
     if (T <= 0 || N <= 0 || M <= 0 || M % N) return fail("bad GAE shape (T > 0, N > 0, M multiple of N)");
     if (!rewards || !values || !done || !boot || !ret || !adv) return fail("null GAE buffer");
     dim3 grid((M + 255) / 256);
-    hipLaunchKernelGGL(k_gae, grid, dim3(256), 0, (hipStream_t)stream, rewards, values, done, boot, T, N, M, gamma, lamb,
-                       ret, adv);
+    hipLaunchKernelGGL(k_gae<float>, grid, dim3(256), 0, (hipStream_t)stream, rewards, values, done, boot, T, N, M, gamma,
+                       lamb, ret, adv);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int fjsp_gae_f64(const double* rewards, const double* values, const uint8_t* done, const double* boot, int32_t T,
+                 int32_t N, int32_t M, double gamma, double lamb, double* ret, double* adv, void* stream) {
+    if (T <= 0 || N <= 0 || M <= 0 || M % N) return fail("bad GAE shape (T > 0, N > 0, M multiple of N)");
+    if (!rewards || !values || !done || !boot || !ret || !adv) return fail("null GAE buffer");
+    dim3 grid((M + 255) / 256);
+    hipLaunchKernelGGL(k_gae<double>, grid, dim3(256), 0, (hipStream_t)stream, rewards, values, done, boot, T, N, M, gamma,
+                       lamb, ret, adv);
     HIPCHK(hipGetLastError());
     return 0;
 }

@@ -185,15 +185,18 @@ class FJSPVecEnv:
 def gae(rewards, values, done, boot, gamma, lamb, out_ret=None, out_adv=None):
     """Returns + GAE (transition_memory.py:83-105) on device tensors.
 
-    rewards f64 [T, M], values f32 [T, M], done u8 [T, N], boot f64 [M]; columns m = a*N + e."""
+    rewards f64 [T, M], values f32 or f64 [T, M], done u8 [T, N], boot f64 [M]; columns m = a*N + e."""
     T, M = rewards.shape
     N = done.shape[1]
     ret = out_ret if out_ret is not None else torch.empty_like(rewards)
     adv = out_adv if out_adv is not None else torch.empty_like(rewards)
     r = rewards.contiguous(); v = values.contiguous(); d = done.to(torch.uint8).contiguous(); b = boot.contiguous()
     stream = torch.cuda.current_stream(rewards.device).cuda_stream
-    nat.check(nat.lib().fjsp_gae(_ptr(r), _ptr(v), _ptr(d), _ptr(b), T, N, M, float(gamma), float(lamb),
-                                 _ptr(ret), _ptr(adv), ctypes.c_void_p(stream)))
+    fn = nat.lib().fjsp_gae_f64 if v.dtype == torch.float64 else nat.lib().fjsp_gae
+    if v.dtype not in (torch.float32, torch.float64):
+        raise TypeError("values must be float32 or float64")
+    nat.check(fn(_ptr(r), _ptr(v), _ptr(d), _ptr(b), T, N, M, float(gamma), float(lamb),
+                 _ptr(ret), _ptr(adv), ctypes.c_void_p(stream)))
     return ret, adv
 
 
