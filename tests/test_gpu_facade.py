@@ -221,7 +221,8 @@ def test_state_render_spaces(M):
     env = M["W"].FJSPParallelEnv(render_mode="rgb_array")
     env.reset(seed=0)
     st = env.state()
-    assert st.dtype == np.float32 and st.shape == (38 + 29 + 4,)
+    # np.concatenate promotes int32 + float32 to float64, as in the reference (wrapper :119-136)
+    assert st.dtype == np.float64 and st.shape == (38 + 29 + 4,)
     grid = env.render()
     assert grid.shape == (4, 6, 3) and tuple(grid[0, 0]) == (0, 0, 0)
     assert env.action_space("agv").n == 8 and env.action_space("packaging_red").n == 3
