@@ -10,7 +10,8 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libfjsp.so")
+# FJSP_LIB selects a diagnostic build (e.g. libfjsp_stamps.so); default: the product library
+LIB_PATH = os.environ.get("FJSP_LIB") or os.path.join(HERE, "libfjsp.so")
 SRC = os.path.join(HERE, "csrc", "fjsp_hip.hip")
 HEADERS = [os.path.join(HERE, "csrc", "fjsp_env.h"), os.path.join(REPO, "include", "fjsp.h")]
 

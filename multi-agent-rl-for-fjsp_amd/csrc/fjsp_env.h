@@ -24,6 +24,9 @@
 
 namespace fjsp {
 
+FJSP_DEV float __uint_as_float_fjsp(uint32_t u) { float f; __builtin_memcpy(&f, &u, 4); return f; }
+FJSP_DEV uint32_t __float_as_uint_fjsp(float f) { uint32_t u; __builtin_memcpy(&u, &f, 4); return u; }
+
 constexpr int NA = 8;
 constexpr int NI32 = 20, NI8 = 12, NF32 = 6, NMASK = 29;
 constexpr int MAX_ORDERS = 64;
@@ -66,36 +69,183 @@ enum : int { W_ORDER = 0, W_THROUGHPUT, W_TIME, W_PICK_LOAD, W_PICK_TRAY, W_PICK
              W_AGV_PACKAGING, W_AGV_INVALID, W_M_COMPLETE, W_M_START, W_M_IDLE, W_P_COMPLETE, W_P_START, W_P_IDLE,
              NW };
 
+// Reward lookup table (device memory): the local reward of every (agent kind, result bits,
+// action == 0) combination, each summed from 0.0 in calculate_local_reward's order on the host,
+// plus the global-reward weights.  Layout: [0,16) pickup, [16,48) AGV, [48,64) machine,
+// [64,80) packaging, [80] ORDER, [81] THROUGHPUT, [82] TIME * step_size.
+constexpr int RLUT_SIZE = 96;
+
 struct Cfg {
     int step_size, max_steps, tray_cap, mask_tray_cap, storage_cap, pool0, pkg_cap;
     int ptk_small, ptk_big, ptk_pack;   // processing times in steps
-    double w[NW];
+    const double* lut;                  // RLUT_SIZE doubles
 };
+
+// Host side: fill the reward table from RewardModel weights (w in fjsp_reward_weights order).
+inline void build_reward_lut(const double* w, int step_size, double* lut) {
+    for (int i = 0; i < RLUT_SIZE; i++) lut[i] = 0.0;
+    for (int idx = 0; idx < 16; idx++) {   // bit0 start/loaded, bit1 completed, bit2 idle flag, bit3 action == 0
+        const bool b0 = idx & 1, b1 = idx & 2, idle = (idx & 4) && (idx & 8);
+        double p = 0.0, m = 0.0, k = 0.0;
+        if (b0) p += w[W_PICK_LOAD];
+        if (b1) p += w[W_PICK_TRAY];
+        if (idle) p += w[W_PICK_IDLE];
+        if (b0) m += w[W_M_START];
+        if (b1) m += w[W_M_COMPLETE];
+        if (idle) m += w[W_M_IDLE];
+        if (b0) k += w[W_P_START];
+        if (b1) k += w[W_P_COMPLETE];
+        if (idle) k += w[W_P_IDLE];
+        lut[idx] = p; lut[48 + idx] = m; lut[64 + idx] = k;
+    }
+    for (int idx = 0; idx < 32; idx++) {   // bit0 invalid, bit1 moved, bit2 pickup, bit3 drop, bit4 to packaging
+        double a = 0.0;
+        if (idx & 4) a += w[W_AGV_DELIVERY];
+        if (idx & 8) a += w[W_AGV_DELIVERY];
+        if (idx & 16) a += w[W_AGV_PACKAGING];
+        if (idx & 2) a += w[W_AGV_MOVE];
+        if (idx & 1) a += w[W_AGV_INVALID];
+        lut[16 + idx] = a;
+    }
+    lut[80] = w[W_ORDER];
+    lut[81] = w[W_THROUGHPUT];
+    lut[82] = w[W_TIME] * (double)step_size;   // TIME_PENALTY * time_elapsed (time_elapsed = step_size)
+}
 
 // status bits (include/fjsp.h)
 constexpr uint32_t ST_DIVERGED = 0x1u, ST_OBS_OVERFLOW = 0x2u, ST_PKG_WAIT = 0x4u, ST_TRAY_LOST = 0x8u,
                    ST_PROD_LOST = 0x10u, ST_OVERWRITE = 0x20u, ST_SLOT_OVERFLOW = 0x40u;
 
 // Number of packed u32 words of Env in the SoA state buffer.
-constexpr int NWORDS = 40;
+constexpr int NWORDS = 40;   // rows of the HBM state buffer (30 used)
 
-// Per-env register state.  Field names follow the reference objects.
+// Diagnostic build only (-DFJSP_STAMPS): per-wave s_memtime deltas per step phase.
+#ifdef FJSP_STAMPS
+#define FJSP_STAMP(E, i)                                   \
+    do {                                                   \
+        uint64_t _t = __builtin_amdgcn_s_memtime();        \
+        (E).st_acc[i] += _t - (E).st_t0;                   \
+        (E).st_t0 = _t;                                    \
+    } while (0)
+#else
+#define FJSP_STAMP(E, i) ((void)0)
+#endif
+
+// Per-env register state: 30 packed u32 words, bit-identical to the HBM `words` rows, so
+// loading / storing an env is a plain copy and the live state costs 30 VGPRs instead of ~95.
+// Field names follow the reference objects; every word index below is a compile-time
+// constant at each use (list / machine / station indices come from templates or unrolled
+// loops), so the words stay in registers.
+//   W0  step[0,16) norders[16,24) next_order[24,32)     W1  ncompleted[0,8) total_packaged[8,32)
+//   W2  status                                          W3  MT19937 cursor (mti | g << 16)
+//   W4  pickup: cur_order[0,8) (0xFF none) cur_idx[8,12) cur_n[12,16) cur_type[16,18)
+//       cur_color[18,20) tray_valid[20] tray_count[21,24) tray_start[24,28)
+//   W5  tray_order[0,8) pool[8,24) slot_next[24,32)
+//   W6  AGV: loc[0,3) carry[3,11) carry_code[11,24) carry_type[24,26) carry_color[26,28) np[28] nk[29]
+//   W7+l   list l: head[0,8) tail[8,16) len[16,32)
+//   W17+m  machine m: busy[0] cur[1,9) code[9,22) prog[22] k[23,27)     W19 next[0]|next[1] << 16
+//   W20+s  packaging s: busy[0] hascur[1] qfirst[2,10) inflight[10,18) queued[18,32)
+//   W24/25 completed[0..3] (16 bits each)                               W26+s progress (f32 bits)
+constexpr int NSTATE = 30;
+
 struct Env {
-    int step, norders, next_order, ncompleted, total_packaged, mti;
-    uint32_t status;
+    uint32_t w[NSTATE];
+#ifdef FJSP_STAMPS
+    uint64_t st_acc[8], st_t0;
+#endif
+    FJSP_DEV uint32_t bf(int i, int o, int b) const { return (w[i] >> o) & ((1u << b) - 1u); }
+    FJSP_DEV void sbf(int i, int o, int b, uint32_t v) {
+        const uint32_t m = ((1u << b) - 1u) << o;
+        w[i] = (w[i] & ~m) | ((v << o) & m);
+    }
+    // episode
+    FJSP_DEV int step() const { return bf(0, 0, 16); }
+    FJSP_DEV void set_step(int v) { sbf(0, 0, 16, v); }
+    FJSP_DEV int norders() const { return bf(0, 16, 8); }
+    FJSP_DEV void set_norders(int v) { sbf(0, 16, 8, v); }
+    FJSP_DEV int next_order() const { return w[0] >> 24; }
+    FJSP_DEV void set_next_order(int v) { sbf(0, 24, 8, v); }
+    FJSP_DEV int ncompleted() const { return bf(1, 0, 8); }
+    FJSP_DEV void set_ncompleted(int v) { sbf(1, 0, 8, v); }
+    FJSP_DEV int total_packaged() const { return w[1] >> 8; }
+    FJSP_DEV void set_total_packaged(int v) { sbf(1, 8, 24, v); }
+    FJSP_DEV uint32_t status() const { return w[2]; }
+    FJSP_DEV void flag(uint32_t b) { w[2] |= b; }
+    FJSP_DEV int mti() const { return (int)w[3]; }
+    FJSP_DEV void set_mti(int v) { w[3] = (uint32_t)v; }
     // pickup station (PickupStationAgent.py:88-94)
-    int cur_order, cur_idx, cur_n, cur_type, cur_color;
-    int tray_valid, tray_order, tray_start, tray_count, pool, slot_next;
-    // AGV (AGVAgent.py:41-45): location, carried tray slot (NIL = none) and cached tray facts
-    int loc, carry, carry_code, carry_type, carry_color, carry_np, carry_nk;
+    FJSP_DEV int cur_order() const { const int v = bf(4, 0, 8); return v == 0xFF ? -1 : v; }
+    FJSP_DEV void set_cur_order(int v) { sbf(4, 0, 8, v < 0 ? 0xFFu : (uint32_t)v); }
+    FJSP_DEV int cur_idx() const { return bf(4, 8, 4); }
+    FJSP_DEV void set_cur_idx(int v) { sbf(4, 8, 4, v); }
+    FJSP_DEV int cur_n() const { return bf(4, 12, 4); }
+    FJSP_DEV int cur_type() const { return bf(4, 16, 2); }
+    FJSP_DEV int cur_color() const { return bf(4, 18, 2); }
+    FJSP_DEV void set_cur_info(uint32_t ow) {   // n, type, colour of an order word at once
+        sbf(4, 12, 8, ((ow >> 20) & 15u) | (((ow >> 24) & 15u) << 4));
+    }
+    FJSP_DEV int tray_valid() const { return bf(4, 20, 1); }
+    FJSP_DEV void set_tray_valid(int v) { sbf(4, 20, 1, v); }
+    FJSP_DEV int tray_count() const { return bf(4, 21, 3); }
+    FJSP_DEV void set_tray_count(int v) { sbf(4, 21, 3, v); }
+    FJSP_DEV int tray_start() const { return bf(4, 24, 4); }
+    FJSP_DEV void set_tray_start(int v) { sbf(4, 24, 4, v); }
+    FJSP_DEV int tray_order() const { return bf(5, 0, 8); }
+    FJSP_DEV void set_tray_order(int v) { sbf(5, 0, 8, v); }
+    FJSP_DEV int pool() const { return bf(5, 8, 16); }
+    FJSP_DEV void set_pool(int v) { sbf(5, 8, 16, v); }
+    FJSP_DEV int slot_next() const { return w[5] >> 24; }
+    FJSP_DEV void set_slot_next(int v) { sbf(5, 24, 8, v); }
+    // AGV (AGVAgent.py:41-45): location, carried tray slot (NIL = none), cached tray facts
+    FJSP_DEV int loc() const { return bf(6, 0, 3); }
+    FJSP_DEV void set_loc(int v) { sbf(6, 0, 3, v); }
+    FJSP_DEV int carry() const { return bf(6, 3, 8); }
+    FJSP_DEV void set_carry(int v) { sbf(6, 3, 8, v); }
+    FJSP_DEV int carry_code() const { return bf(6, 11, 13); }
+    FJSP_DEV int carry_type() const { return bf(6, 24, 2); }
+    FJSP_DEV int carry_color() const { return bf(6, 26, 2); }
+    FJSP_DEV int carry_np() const { return bf(6, 28, 1); }
+    FJSP_DEV int carry_nk() const { return bf(6, 29, 1); }
+    FJSP_DEV void set_carried(int slot, int code, int type, int color, int np, int nk) {
+        w[6] = (w[6] & 7u) | ((uint32_t)slot << 3) | ((uint32_t)code << 11) | ((uint32_t)type << 24) |
+               ((uint32_t)color << 26) | ((uint32_t)np << 28) | ((uint32_t)nk << 29);
+    }
     // FIFO lists in the slot arena
-    int lh[NLIST], lt[NLIST], ll[NLIST];
-    // machines (MachineAgent.py:40-47): current tray slot/code, busy, progress(0/1),
-    // products processed so far, step of the next product completion
-    int m_busy[2], m_cur[2], m_code[2], m_prog[2], m_k[2], m_next[2];
+    FJSP_DEV int lh(int l) const { return bf(7 + l, 0, 8); }
+    FJSP_DEV int lt(int l) const { return bf(7 + l, 8, 8); }
+    FJSP_DEV int ll(int l) const { return w[7 + l] >> 16; }
+    FJSP_DEV void set_list(int l, int h, int t, int n) {
+        w[7 + l] = (uint32_t)h | ((uint32_t)t << 8) | ((uint32_t)n << 16);
+    }
+    // machines (MachineAgent.py:40-47)
+    FJSP_DEV int m_busy(int m) const { return bf(17 + m, 0, 1); }
+    FJSP_DEV void set_m_busy(int m, int v) { sbf(17 + m, 0, 1, v); }
+    FJSP_DEV int m_cur(int m) const { return bf(17 + m, 1, 8); }
+    FJSP_DEV void set_m_cur(int m, int v) { sbf(17 + m, 1, 8, v); }
+    FJSP_DEV int m_code(int m) const { return bf(17 + m, 9, 13); }
+    FJSP_DEV int m_prog(int m) const { return bf(17 + m, 22, 1); }
+    FJSP_DEV void set_m_prog(int m, int v) { sbf(17 + m, 22, 1, v); }
+    FJSP_DEV int m_k(int m) const { return bf(17 + m, 23, 4); }
+    FJSP_DEV void set_m_k(int m, int v) { sbf(17 + m, 23, 4, v); }
+    FJSP_DEV int m_next(int m) const { return bf(19, 16 * m, 16); }
+    FJSP_DEV void set_m_next(int m, int v) { sbf(19, 16 * m, 16, v); }
+    FJSP_DEV void set_m_grant(int m, int slot, int code, int busy) {   // k = 0, progress unchanged
+        w[17 + m] = (w[17 + m] & (1u << 22)) | (uint32_t)busy | ((uint32_t)slot << 1) | ((uint32_t)code << 9);
+    }
     // packaging (PackagingAgent.py:250-256): qfirst = first queued (not yet granted) run
-    int p_busy[4], p_hascur[4], p_completed[4], p_qfirst[4], p_inflight[4], p_queued[4];
-    float p_prog[4];
+    FJSP_DEV int p_busy(int s) const { return bf(20 + s, 0, 1); }
+    FJSP_DEV void set_p_busy(int s, int v) { sbf(20 + s, 0, 1, v); }
+    FJSP_DEV int p_hascur(int s) const { return bf(20 + s, 1, 1); }
+    FJSP_DEV int p_qfirst(int s) const { return bf(20 + s, 2, 8); }
+    FJSP_DEV void set_p_qfirst(int s, int v) { sbf(20 + s, 2, 8, v); }
+    FJSP_DEV int p_inflight(int s) const { return bf(20 + s, 10, 8); }
+    FJSP_DEV void set_p_inflight(int s, int v) { sbf(20 + s, 10, 8, v); }
+    FJSP_DEV int p_queued(int s) const { return w[20 + s] >> 18; }
+    FJSP_DEV void set_p_queued(int s, int v) { sbf(20 + s, 18, 14, v); }
+    FJSP_DEV int p_completed(int s) const { return bf(24 + (s >> 1), 16 * (s & 1), 16); }
+    FJSP_DEV void set_p_completed(int s, int v) { sbf(24 + (s >> 1), 16 * (s & 1), 16, v); }
+    FJSP_DEV float p_prog(int s) const { return __uint_as_float_fjsp(w[26 + s]); }
+    FJSP_DEV void set_p_prog(int s, float v) { w[26 + s] = __float_as_uint_fjsp(v); }
 };
 
 // ---- table accessors: element i of a per-env table = base[i * stride]
@@ -107,24 +257,25 @@ struct Tables {
     int stride;
 };
 
-FJSP_DEV void list_push(Env& E, const Tables& T, int L, int s) {
+template <int L>
+FJSP_DEV void list_push(Env& E, const Tables& T, int s) {
+    const int n = E.ll(L);
     T.snext[s * T.stride] = (uint8_t)NIL;
-    if (E.ll[L] == 0) E.lh[L] = s;
-    else T.snext[E.lt[L] * T.stride] = (uint8_t)s;
-    E.lt[L] = s;
-    E.ll[L] += 1;
+    if (n != 0) T.snext[E.lt(L) * T.stride] = (uint8_t)s;
+    E.set_list(L, n == 0 ? s : E.lh(L), s, n + 1);
 }
-FJSP_DEV int list_pop(Env& E, const Tables& T, int L) {
-    int s = E.lh[L];
-    E.lh[L] = T.snext[s * T.stride];
-    E.ll[L] -= 1;
-    if (E.ll[L] == 0) { E.lh[L] = NIL; E.lt[L] = NIL; }
+template <int L>
+FJSP_DEV int list_pop(Env& E, const Tables& T) {
+    const int s = E.lh(L), n = E.ll(L) - 1;
+    const int next = T.snext[s * T.stride];
+    E.set_list(L, n == 0 ? NIL : next, n == 0 ? NIL : E.lt(L), n);
     return s;
 }
 // new tray slot holding `code` (bump allocator, reset per episode)
 FJSP_DEV int slot_new(Env& E, const Tables& T, int code) {
-    if (E.slot_next >= MAX_SLOTS) { E.status |= ST_SLOT_OVERFLOW | ST_DIVERGED; return -1; }
-    int s = E.slot_next++;
+    const int s = E.slot_next();
+    if (s >= MAX_SLOTS) { E.flag(ST_SLOT_OVERFLOW | ST_DIVERGED); return -1; }
+    E.set_slot_next(s + 1);
     T.scode[s * T.stride] = (uint16_t)code;
     return s;
 }
@@ -136,46 +287,50 @@ constexpr uint32_t R_EXEC = 0x80u;
 FJSP_DEV uint32_t pickup_execute(Env& E, const Tables& T, const Cfg& C, int action) {
     uint32_t r = R_EXEC;   // 1 success, 2 product_loaded, 4 tray_completed, 8 idle_with_orders
     auto push_tray = [&]() {
-        int s = slot_new(E, T, tc_make(E.tray_order, E.tray_start, E.tray_count));
-        if (s >= 0) list_push(E, T, L_PREADY, s);
-        E.tray_valid = 0;
+        const int s = slot_new(E, T, tc_make(E.tray_order(), E.tray_start(), E.tray_count()));
+        if (s >= 0) list_push<L_PREADY>(E, T, s);
+        E.set_tray_valid(0);
     };
     if (action == 0) {
-        if (E.next_order < E.norders || E.cur_order >= 0) r |= 8u;
+        if (E.next_order() < E.norders() || E.cur_order() >= 0) r |= 8u;
         r |= 1u;
     } else if (action == 1) {
-        if (E.cur_order < 0) {
-            if (E.next_order < E.norders) {
-                E.cur_order = E.next_order++;
-                E.cur_idx = 0;
-                uint32_t w = T.orders[E.cur_order * T.stride];
-                E.cur_n = ow_n(w); E.cur_type = ow_type(w); E.cur_color = ow_color(w);
+        if (E.cur_order() < 0) {
+            const int no = E.next_order();
+            if (no < E.norders()) {
+                E.set_next_order(no + 1);
+                E.set_cur_order(no);
+                E.set_cur_idx(0);
+                E.set_cur_info(T.orders[no * T.stride]);
             } else {
                 return r;
             }
         }
-        if (!E.tray_valid) {
-            if (E.pool > 0) {
-                E.pool -= 1;
-                E.tray_valid = 1; E.tray_order = E.cur_order; E.tray_start = E.cur_idx; E.tray_count = 0;
+        if (!E.tray_valid()) {
+            const int pool = E.pool();
+            if (pool > 0) {
+                E.set_pool(pool - 1);
+                E.set_tray_valid(1); E.set_tray_order(E.cur_order()); E.set_tray_start(E.cur_idx()); E.set_tray_count(0);
             } else {
                 return r;
             }
         }
-        if (E.tray_count < C.tray_cap) {
-            if (E.cur_order != E.tray_order) {   // :231-235 (unreachable with the reference's flow)
+        const int cnt = E.tray_count();
+        if (cnt < C.tray_cap) {
+            if (E.cur_order() != E.tray_order()) {   // :231-235 (unreachable with the reference's flow)
                 push_tray();
                 return r | 4u;
             }
-            E.tray_count += 1;
-            E.cur_idx += 1;
+            E.set_tray_count(cnt + 1);
+            const int idx = E.cur_idx() + 1;
+            E.set_cur_idx(idx);
             r |= 2u | 1u;
-            if (E.cur_idx >= E.cur_n) {
-                E.cur_order = -1; E.cur_idx = 0;
+            if (idx >= E.cur_n()) {
                 push_tray();
+                E.set_cur_order(-1); E.set_cur_idx(0);
                 return r | 4u;
             }
-            if (E.tray_count >= C.tray_cap) {
+            if (cnt + 1 >= C.tray_cap) {
                 push_tray();
                 return r | 4u;
             }
@@ -184,7 +339,7 @@ FJSP_DEV uint32_t pickup_execute(Env& E, const Tables& T, const Cfg& C, int acti
             return r | 4u;
         }
     } else if (action == 2) {
-        if (E.tray_valid && E.tray_count > 0) {
+        if (E.tray_valid() && E.tray_count() > 0) {
             push_tray();
             r |= 1u;
         }
@@ -194,93 +349,89 @@ FJSP_DEV uint32_t pickup_execute(Env& E, const Tables& T, const Cfg& C, int acti
 
 // FJSPSimulation.add_tray_to_packaging (FJSPSimulation.py:402-430): first station (dict order
 // blue_1, blue_2, red, green) whose colour matches and whose Resource has capacity.
+template <int S>
+FJSP_DEV void pkg_enqueue(Env& E, const Tables& T, int s, int n) {
+    list_push<L_PKG + S>(E, T, s);
+    if (E.p_qfirst(S) == NIL) E.set_p_qfirst(S, s);
+    E.set_p_queued(S, E.p_queued(S) + n);
+}
 FJSP_DEV void add_tray_to_packaging(Env& E, const Tables& T, const Cfg& C, int s, int code) {
-    const int color = E.carry_color;
+    const int color = E.carry_color();
     // PackagingColor RED=1 BLUE=2 GREEN=3; stations 0,1 blue, 2 red, 3 green
-    int st = -1;
-    if (color == 2) {
-        if (E.p_inflight[0] < C.pkg_cap) st = 0;
-        else if (E.p_inflight[1] < C.pkg_cap) st = 1;
-    } else if (color == 1) {
-        if (E.p_inflight[2] < C.pkg_cap) st = 2;
-    } else if (color == 3) {
-        if (E.p_inflight[3] < C.pkg_cap) st = 3;
-    }
-    int n = tc_count(code);
-    switch (st) {   // constant list indices keep the list registers out of scratch
-    case 0: list_push(E, T, L_PKG + 0, s); if (E.p_qfirst[0] == NIL) E.p_qfirst[0] = s; E.p_queued[0] += n; break;
-    case 1: list_push(E, T, L_PKG + 1, s); if (E.p_qfirst[1] == NIL) E.p_qfirst[1] = s; E.p_queued[1] += n; break;
-    case 2: list_push(E, T, L_PKG + 2, s); if (E.p_qfirst[2] == NIL) E.p_qfirst[2] = s; E.p_queued[2] += n; break;
-    case 3: list_push(E, T, L_PKG + 3, s); if (E.p_qfirst[3] == NIL) E.p_qfirst[3] = s; E.p_queued[3] += n; break;
-    default: E.status |= ST_PROD_LOST; break;
-    }
+    const int n = tc_count(code);
+    if (color == 2 && E.p_inflight(0) < C.pkg_cap) pkg_enqueue<0>(E, T, s, n);
+    else if (color == 2 && E.p_inflight(1) < C.pkg_cap) pkg_enqueue<1>(E, T, s, n);
+    else if (color == 1 && E.p_inflight(2) < C.pkg_cap) pkg_enqueue<2>(E, T, s, n);
+    else if (color == 3 && E.p_inflight(3) < C.pkg_cap) pkg_enqueue<3>(E, T, s, n);
+    else E.flag(ST_PROD_LOST);
+}
+
+template <int L>
+FJSP_DEV int pop_if_any(Env& E, const Tables& T) {
+    return E.ll(L) ? list_pop<L>(E, T) : -1;
 }
 
 // AGVAgent.execute_action / _execute_pickup / _execute_drop (AGVAgent.py:180-368).
 // Returns the result word; *move_to receives the target location of a spawned move.
 FJSP_DEV uint32_t agv_execute(Env& E, const Tables& T, const Cfg& C, int action, int* move_to) {
     uint32_t r = R_EXEC;   // 1 success, 2 invalid, 4 moved, 8 pickup, 16 drop, 32 to packaging; 16.. distance
+    const int loc = E.loc();
     if (action == 0) return r | 1u;
     if (action >= 1 && action <= 5) {
-        int l = move_loc(action);
-        int d = manhattan(E.loc, l);
+        const int l = move_loc(action);
+        const int d = manhattan(loc, l);
         if (d == 0) return r | 1u;
         *move_to = l;
         return r | 1u | 4u | ((uint32_t)d << 16);
     }
     if (action == 6) {
-        if (E.carry != NIL) return r | 2u;
-        int s = -1;
-        switch (E.loc) {
-        case LOC_PICKUP: if (E.ll[L_PREADY]) s = list_pop(E, T, L_PREADY); break;
-        case LOC_SMALL: if (E.ll[L_M0R]) s = list_pop(E, T, L_M0R); break;
-        case LOC_BIG: if (E.ll[L_M1R]) s = list_pop(E, T, L_M1R); break;
-        case LOC_STORAGE: if (E.ll[L_STORAGE]) s = list_pop(E, T, L_STORAGE); break;
-        default: return r | 2u;   // PACKAGING
+        if (E.carry() != NIL || loc == LOC_PACK) return r | 2u;
+        int s;
+        switch (loc) {
+        case LOC_PICKUP: s = pop_if_any<L_PREADY>(E, T); break;
+        case LOC_SMALL: s = pop_if_any<L_M0R>(E, T); break;
+        case LOC_BIG: s = pop_if_any<L_M1R>(E, T); break;
+        default: s = pop_if_any<L_STORAGE>(E, T); break;
         }
         if (s < 0) return r | 2u;
-        int code = T.scode[s * T.stride];
-        E.carry = s; E.carry_code = code;
-        int n = tc_count(code);
-        if (n > 0) {
-            uint32_t w = T.orders[tc_order(code) * T.stride];
-            uint32_t rg = tc_range(code);
-            E.carry_type = ow_type(w);
-            E.carry_color = ow_color(w);
-            E.carry_np = (w & rg) != rg;
-            E.carry_nk = ((w >> 9) & rg) != rg;
+        const int code = T.scode[s * T.stride];
+        if (tc_count(code) > 0) {
+            const uint32_t w = T.orders[tc_order(code) * T.stride];
+            const uint32_t rg = tc_range(code);
+            E.set_carried(s, code, ow_type(w), ow_color(w), (w & rg) != rg, ((w >> 9) & rg) != rg);
         } else {
-            E.carry_type = 0; E.carry_color = 0; E.carry_np = 0; E.carry_nk = 0;
+            E.set_carried(s, code, 0, 0, 0, 0);
         }
         return r | 1u | 8u;
     }
     if (action == 7) {
-        if (E.carry == NIL) return r | 2u;
-        int s = E.carry, code = E.carry_code, ty = E.carry_type;
-        switch (E.loc) {
+        const int s = E.carry();
+        if (s == NIL) return r | 2u;
+        const int code = E.carry_code(), ty = E.carry_type(), np = E.carry_np();
+        switch (loc) {
         case LOC_PICKUP:
             if (tc_count(code) != 0) return r | 2u;
-            E.pool += 1;    // add_empty_tray
+            E.set_pool(E.pool() + 1);    // add_empty_tray
             break;
         case LOC_SMALL:
-            if (!(E.carry_np && (ty == 1 || ty == 2))) return r | 2u;
-            list_push(E, T, L_M0Q, s);
+            if (!(np && (ty == 1 || ty == 2))) return r | 2u;
+            list_push<L_M0Q>(E, T, s);
             break;
         case LOC_BIG:
-            if (!(E.carry_np && (ty == 3 || ty == 2))) return r | 2u;
-            list_push(E, T, L_M1Q, s);
+            if (!(np && (ty == 3 || ty == 2))) return r | 2u;
+            list_push<L_M1Q>(E, T, s);
             break;
         case LOC_STORAGE:
-            if (E.ll[L_STORAGE] < C.storage_cap) list_push(E, T, L_STORAGE, s);
-            else E.status |= ST_TRAY_LOST;
+            if (E.ll(L_STORAGE) < C.storage_cap) list_push<L_STORAGE>(E, T, s);
+            else E.flag(ST_TRAY_LOST);
             break;
         default:   // PACKAGING
-            if (!(E.carry_nk && !E.carry_np)) return r | 2u;
+            if (!(E.carry_nk() && !np)) return r | 2u;
             add_tray_to_packaging(E, T, C, s, code);
             r |= 32u;
             break;
         }
-        E.carry = NIL;
+        E.set_carry(NIL);
         return r | 1u | 16u;
     }
     return r | 2u;
@@ -292,18 +443,19 @@ FJSP_DEV uint32_t machine_execute(Env& E, const Tables& T, int action, int* star
     constexpr int LQ = M == 0 ? L_M0Q : L_M1Q;
     constexpr int LR = M == 0 ? L_M0R : L_M1R;
     uint32_t r = R_EXEC;   // 1 success, 2 started, 4 completed, 8 idle_with_queue
+    const int idle_q = E.ll(LQ) > 0 && !E.m_busy(M);
     if (action == 0) {
-        if (E.ll[LQ] > 0 && !E.m_busy[M]) r |= 8u;
-        r |= 1u;
+        r |= 1u | (idle_q ? 8u : 0u);
     } else if (action == 1) {
-        if (E.ll[LQ] > 0 && !E.m_busy[M]) {
-            *start_slot = list_pop(E, T, LQ);
+        if (idle_q) {
+            *start_slot = list_pop<LQ>(E, T);
             r |= 2u | 1u;
         }
     } else if (action == 2) {
-        if (!E.m_busy[M] && E.m_cur[M] != NIL) {
-            list_push(E, T, LR, E.m_cur[M]);
-            E.m_cur[M] = NIL;
+        const int cur = E.m_cur(M);
+        if (!E.m_busy(M) && cur != NIL) {
+            list_push<LR>(E, T, cur);
+            E.set_m_cur(M, NIL);
             r |= 4u | 1u;
         }
     }
@@ -314,19 +466,18 @@ FJSP_DEV uint32_t machine_execute(Env& E, const Tables& T, int action, int* star
 template <int S>
 FJSP_DEV uint32_t pack_execute(Env& E, int action, int* started) {
     uint32_t r = R_EXEC;   // 1 success, 2 started, 4 completed, 8 idle_with_queue; 16.. completed count
+    const int n = E.p_queued(S);
     if (action == 0) {
-        if (E.p_queued[S] > 0 && !E.p_busy[S]) r |= 8u;
-        r |= 1u;
+        r |= 1u | ((n > 0 && !E.p_busy(S)) ? 8u : 0u);
     } else if (action == 1) {
-        int n = E.p_queued[S];
         if (n > 0) {
             *started = 1;
             // self.processing_progress = (i / len(self.product_queue)) * 100 with i == 1
-            E.p_prog[S] = (float)((1.0 / (double)n) * 100.0);
+            E.set_p_prog(S, (float)((1.0 / (double)n) * 100.0));
             r |= 2u | 1u;
         }
     } else if (action == 2) {
-        if (!E.p_busy[S] && E.p_hascur[S]) r |= 4u | ((uint32_t)(E.p_completed[S] & 0xFFFF) << 16);
+        if (!E.p_busy(S) && E.p_hascur(S)) r |= 4u | ((uint32_t)E.p_completed(S) << 16);
     }
     return r;
 }
@@ -336,21 +487,22 @@ FJSP_DEV uint32_t pack_execute(Env& E, int action, int* started) {
 template <int M>
 FJSP_DEV void machine_run(Env& E, const Tables& T, const Cfg& C, int start_slot) {
     const int ptk = M == 0 ? C.ptk_small : C.ptk_big;
-    if (E.m_busy[M] && E.m_next[M] == E.step) {
-        int code = E.m_code[M];
-        int o = tc_order(code);
-        uint32_t bit = 1u << (tc_start(code) + E.m_k[M]);
-        T.orders[o * T.stride] |= bit;          // product.is_processed = True
-        E.m_k[M] += 1;
-        if (E.m_k[M] >= tc_count(code)) { E.m_busy[M] = 0; E.m_prog[M] = 1; }
-        else E.m_next[M] = E.step + ptk;
+    const int step = E.step();
+    if (E.m_busy(M) && E.m_next(M) == step) {
+        const int code = E.m_code(M);
+        const int k = E.m_k(M);
+        T.orders[tc_order(code) * T.stride] |= 1u << (tc_start(code) + k);   // product.is_processed = True
+        E.set_m_k(M, k + 1);
+        if (k + 1 >= tc_count(code)) { E.set_m_busy(M, 0); E.set_m_prog(M, 1); }
+        else E.set_m_next(M, step + ptk);
     }
     if (start_slot >= 0) {   // grant at T: is_busy, current_tray := tray (MachineAgent.py:159-160)
-        if (E.m_cur[M] != NIL) E.status |= ST_OVERWRITE;
-        int code = T.scode[start_slot * T.stride];
-        E.m_cur[M] = start_slot; E.m_code[M] = code; E.m_k[M] = 0;
-        if (tc_count(code) > 0) { E.m_busy[M] = 1; E.m_next[M] = E.step + ptk; }
-        else { E.m_busy[M] = 0; E.m_prog[M] = 1; }   // empty tray: loop body never runs
+        if (E.m_cur(M) != NIL) E.flag(ST_OVERWRITE);
+        const int code = T.scode[start_slot * T.stride];
+        const int busy = tc_count(code) > 0;   // an empty tray's loop body never runs
+        E.set_m_grant(M, start_slot, code, busy);
+        if (busy) E.set_m_next(M, step + ptk);
+        else E.set_m_prog(M, 1);
     }
 }
 
@@ -358,16 +510,18 @@ FJSP_DEV void machine_run(Env& E, const Tables& T, const Cfg& C, int start_slot)
 template <int S>
 FJSP_DEV void pack_run(Env& E, const Tables& T, const Cfg& C, int started, int* orders_done) {
     constexpr int L = L_PKG + S;
-    if (started && E.p_inflight[S] + E.p_queued[S] > C.pkg_cap)
-        E.status |= ST_PKG_WAIT | ST_DIVERGED;   // Request would wait (users == capacity)
+    const int step = E.step();
+    const int qfirst = E.p_qfirst(S);
+    if (started && E.p_inflight(S) + E.p_queued(S) > C.pkg_cap)
+        E.flag(ST_PKG_WAIT | ST_DIVERGED);   // Request would wait (users == capacity)
     // completions (PackagingAgent.py:143-147)
     int done = 0;
-    while (E.ll[L] > 0 && E.lh[L] != E.p_qfirst[S] && T.scstep[E.lh[L] * T.stride] == (uint16_t)E.step) {
-        int s = list_pop(E, T, L);
-        int code = T.scode[s * T.stride];
-        int o = tc_order(code);
+    while (E.ll(L) > 0 && E.lh(L) != qfirst && T.scstep[E.lh(L) * T.stride] == (uint16_t)step) {
+        const int s = list_pop<L>(E, T);
+        const int code = T.scode[s * T.stride];
+        const int o = tc_order(code);
         uint32_t w = T.orders[o * T.stride] | (tc_range(code) << 9);
-        uint32_t full = (1u << ow_n(w)) - 1u;
+        const uint32_t full = (1u << ow_n(w)) - 1u;
         if (!(w & (1u << 18)) && ((w >> 9) & full) == full) {   // _check_order_completions
             w |= 1u << 18;
             *orders_done += 1;
@@ -376,142 +530,180 @@ FJSP_DEV void pack_run(Env& E, const Tables& T, const Cfg& C, int started, int* 
         done += tc_count(code);
     }
     if (done) {
-        E.p_completed[S] += done; E.total_packaged += done; E.p_inflight[S] -= done; E.p_busy[S] = 0;
+        E.set_p_completed(S, E.p_completed(S) + done);
+        E.set_total_packaged(E.total_packaged() + done);
+        E.set_p_inflight(S, E.p_inflight(S) - done);
+        E.set_p_busy(S, 0);
     }
     // grants: every queued product, in queue order (PackagingAgent.py:136-141)
     if (started) {
-        uint16_t cs = (uint16_t)(E.step + C.ptk_pack);
-        for (int s = E.p_qfirst[S]; s != NIL; s = T.snext[s * T.stride]) T.scstep[s * T.stride] = cs;
-        E.p_qfirst[S] = NIL;
-        E.p_inflight[S] += E.p_queued[S];
-        E.p_queued[S] = 0;
-        E.p_busy[S] = 1;
-        E.p_hascur[S] = 1;
+        const uint16_t cs = (uint16_t)(step + C.ptk_pack);
+        for (int s = qfirst; s != NIL; s = T.snext[s * T.stride]) T.scstep[s * T.stride] = cs;
+        const int inflight = E.p_inflight(S) + E.p_queued(S);
+        // busy = 1, hascur = 1, qfirst = NIL, inflight += queued, queued = 0
+        E.w[20 + S] = 3u | ((uint32_t)NIL << 2) | ((uint32_t)(inflight & 0xFF) << 10);
     }
 }
 
 // ---------------------------------------------------------------- observations
+// Observations and masks are emitted field by field into a Sink (store-as-you-go keeps the
+// 67 output values out of the register file).  Sink API:
+//   i32(f, v)  f in [0,20)   i8(f, v)  f in [0,12)   f32(f, v)  f in [0,6)   mask(f, v)  f in [0,29)
 struct Obs {
     int32_t i32[NI32];
     int8_t i8[NI8];
     float f32[NF32];
     int8_t mask[NMASK];
 };
-
-FJSP_DEV void compute_masks(const Env& E, const Cfg& C, int8_t* m) {
-    // pickup (PickupStationAgent.py:144-186)
-    int has_order = E.cur_order >= 0 || E.next_order < E.norders;
-    int has_tray = E.tray_valid || E.pool > 0;
-    int not_full = E.tray_valid ? (E.tray_count < C.mask_tray_cap) : 1;
-    int prem = E.cur_order >= 0 ? (E.cur_idx < E.cur_n) : (E.next_order < E.norders);
-    m[0] = 1;
-    m[1] = (int8_t)(has_order && has_tray && not_full && prem);
-    m[2] = (int8_t)(E.tray_valid && E.tray_count > 0);
-    // AGV (AGVAgent.py:79-178); the AGV is never mid-move at a step boundary
-    m[3] = 1;
-    m[4] = E.loc != LOC_PICKUP;
-    m[5] = E.loc != LOC_SMALL;
-    m[6] = E.loc != LOC_BIG;
-    m[7] = E.loc != LOC_STORAGE;
-    m[8] = E.loc != LOC_PACK;
-    int pick = 0, drop = 0;
-    if (E.carry == NIL) {
-        pick = (E.loc == LOC_PICKUP && E.ll[L_PREADY] > 0) || (E.loc == LOC_SMALL && E.ll[L_M0R] > 0) ||
-               (E.loc == LOC_BIG && E.ll[L_M1R] > 0) || (E.loc == LOC_STORAGE && E.ll[L_STORAGE] > 0);
-    } else {
-        int ty = E.carry_type;
-        drop = (E.loc == LOC_PICKUP && tc_count(E.carry_code) == 0) ||
-               (E.loc == LOC_SMALL && E.carry_np && (ty == 1 || ty == 2)) ||
-               (E.loc == LOC_BIG && E.carry_np && (ty == 3 || ty == 2)) ||
-               (E.loc == LOC_PACK && E.carry_nk && !E.carry_np) || (E.loc == LOC_STORAGE);
+struct ObsSink {   // materialises an Obs (host harness, tests)
+    Obs& o;
+    FJSP_DEV void i32(int f, int v) { o.i32[f] = v; }
+    FJSP_DEV void i8(int f, int v) { o.i8[f] = (int8_t)v; }
+    FJSP_DEV void f32(int f, float v) { o.f32[f] = v; }
+    FJSP_DEV void mask(int f, int v) { o.mask[f] = (int8_t)v; }
+};
+struct MaskBits {  // mask bits per agent (bit i = action i valid), for masked synthetic actions
+    uint32_t bits[NA] = {0, 0, 0, 0, 0, 0, 0, 0};
+    FJSP_DEV void i32(int, int) {}
+    FJSP_DEV void i8(int, int) {}
+    FJSP_DEV void f32(int, float) {}
+    FJSP_DEV void mask(int f, int v) {
+        const int a = f < 3 ? 0 : f < 11 ? 1 : 2 + (f - 11) / 3;
+        const int off = f < 3 ? 0 : f < 11 ? 3 : 11 + 3 * (a - 2);
+        bits[a] |= (uint32_t)(v != 0) << (f - off);
     }
-    m[9] = (int8_t)pick;
-    m[10] = (int8_t)drop;
+};
+
+template <class Sink>
+FJSP_DEV void compute_masks(const Env& E, const Cfg& C, Sink& m) {
+    // pickup (PickupStationAgent.py:144-186)
+    const int co = E.cur_order(), more_orders = E.next_order() < E.norders();
+    const int tv = E.tray_valid(), tcnt = E.tray_count();
+    const int has_order = co >= 0 || more_orders;
+    const int has_tray = tv || E.pool() > 0;
+    const int not_full = tv ? (tcnt < C.mask_tray_cap) : 1;
+    const int prem = co >= 0 ? (E.cur_idx() < E.cur_n()) : more_orders;
+    m.mask(0, 1);
+    m.mask(1, has_order && has_tray && not_full && prem);
+    m.mask(2, tv && tcnt > 0);
+    // AGV (AGVAgent.py:79-178); the AGV is never mid-move at a step boundary
+    const int loc = E.loc();
+    m.mask(3, 1);
+    m.mask(4, loc != LOC_PICKUP);
+    m.mask(5, loc != LOC_SMALL);
+    m.mask(6, loc != LOC_BIG);
+    m.mask(7, loc != LOC_STORAGE);
+    m.mask(8, loc != LOC_PACK);
+    int pick = 0, drop = 0;
+    if (E.carry() == NIL) {
+        pick = (loc == LOC_PICKUP && E.ll(L_PREADY) > 0) || (loc == LOC_SMALL && E.ll(L_M0R) > 0) ||
+               (loc == LOC_BIG && E.ll(L_M1R) > 0) || (loc == LOC_STORAGE && E.ll(L_STORAGE) > 0);
+    } else {
+        const int ty = E.carry_type(), np = E.carry_np();
+        drop = (loc == LOC_PICKUP && tc_count(E.carry_code()) == 0) ||
+               (loc == LOC_SMALL && np && (ty == 1 || ty == 2)) || (loc == LOC_BIG && np && (ty == 3 || ty == 2)) ||
+               (loc == LOC_PACK && E.carry_nk() && !np) || (loc == LOC_STORAGE);
+    }
+    m.mask(9, pick);
+    m.mask(10, drop);
     // machines (MachineAgent.py:72-97)
-    m[11] = 1; m[12] = E.ll[L_M0Q] > 0 && !E.m_busy[0]; m[13] = !E.m_busy[0] && E.m_cur[0] != NIL;
-    m[14] = 1; m[15] = E.ll[L_M1Q] > 0 && !E.m_busy[1]; m[16] = !E.m_busy[1] && E.m_cur[1] != NIL;
+    m.mask(11, 1); m.mask(12, E.ll(L_M0Q) > 0 && !E.m_busy(0)); m.mask(13, !E.m_busy(0) && E.m_cur(0) != NIL);
+    m.mask(14, 1); m.mask(15, E.ll(L_M1Q) > 0 && !E.m_busy(1)); m.mask(16, !E.m_busy(1) && E.m_cur(1) != NIL);
     // packaging (PackagingAgent.py:64-89)
 #pragma unroll
     for (int s = 0; s < 4; s++) {
-        m[17 + 3 * s] = 1;
-        m[18 + 3 * s] = E.p_queued[s] > 0 && !E.p_busy[s] && E.p_inflight[s] < C.pkg_cap;
-        m[19 + 3 * s] = !E.p_busy[s] && E.p_hascur[s];
+        const int busy = E.p_busy(s);
+        m.mask(17 + 3 * s, 1);
+        m.mask(18 + 3 * s, E.p_queued(s) > 0 && !busy && E.p_inflight(s) < C.pkg_cap);
+        m.mask(19 + 3 * s, !busy && E.p_hascur(s));
     }
 }
 
-FJSP_DEV int8_t to_i8(Env& E, int v) {
-    if (v > 127) E.status |= ST_OBS_OVERFLOW | ST_DIVERGED;
-    return (int8_t)v;
+FJSP_DEV int obs_i8_checked(Env& E, int v) {
+    if (v > 127) E.flag(ST_OBS_OVERFLOW | ST_DIVERGED);
+    return (int)(int8_t)v;
 }
 
-FJSP_DEV void observe(Env& E, const Cfg& C, Obs& o) {
+template <class Sink>
+FJSP_DEV void observe(Env& E, const Cfg& C, Sink& o) {
     // pickup (PickupStationAgent.py:102-142)
     int osz = 0, rem = 0, npt = 0, npc = 0;
-    if (E.cur_order >= 0) {
-        osz = E.cur_n; rem = E.cur_n - E.cur_idx;
-        if (rem > 0) { npt = E.cur_type; npc = E.cur_color; }
+    const int co = E.cur_order();
+    if (co >= 0) {
+        osz = E.cur_n(); rem = osz - E.cur_idx();
+        if (rem > 0) { npt = E.cur_type(); npc = E.cur_color(); }
     }
     int tt = 0, tcol = 0, tcnt = 0;
-    if (E.tray_valid) {
-        tcnt = E.tray_count;
-        if (tcnt > 0 && E.tray_order == E.cur_order) {   // a loaded tray always belongs to the current order
-            tt = E.cur_type; tcol = E.cur_color;
+    if (E.tray_valid()) {
+        tcnt = E.tray_count();
+        if (tcnt > 0 && E.tray_order() == co) {   // a loaded tray always belongs to the current order
+            tt = E.cur_type(); tcol = E.cur_color();
         }
     }
-    o.i32[0] = osz; o.i32[1] = rem; o.i32[2] = npt; o.i32[3] = npc;
-    o.i32[4] = tt; o.i32[5] = tcol; o.i32[6] = tcnt;
+    o.i32(0, osz); o.i32(1, rem); o.i32(2, npt); o.i32(3, npc);
+    o.i32(4, tt); o.i32(5, tcol); o.i32(6, tcnt);
     // AGV (AGVAgent.py:53-76)
-    int c = E.carry != NIL;
-    o.i32[7] = loc_row(E.loc); o.i32[8] = loc_col(E.loc);
-    o.i32[9] = c;
-    o.i32[10] = c ? tc_count(E.carry_code) : 0;
-    o.i32[11] = c ? E.carry_type : 0;
-    o.i32[12] = c ? E.carry_np : 0;
-    o.i32[13] = c ? E.carry_nk : 0;
-    o.i32[14] = E.ll[L_PREADY];
-    o.i32[15] = E.m_busy[0]; o.i32[16] = E.m_busy[1];
-    o.i32[17] = E.ll[L_M0R]; o.i32[18] = E.ll[L_M1R];
-    o.i32[19] = E.ll[L_STORAGE];
+    const int c = E.carry() != NIL, loc = E.loc();
+    o.i32(7, loc_row(loc)); o.i32(8, loc_col(loc));
+    o.i32(9, c);
+    o.i32(10, c ? tc_count(E.carry_code()) : 0);
+    o.i32(11, c ? E.carry_type() : 0);
+    o.i32(12, c ? E.carry_np() : 0);
+    o.i32(13, c ? E.carry_nk() : 0);
+    o.i32(14, E.ll(L_PREADY));
+    o.i32(15, E.m_busy(0)); o.i32(16, E.m_busy(1));
+    o.i32(17, E.ll(L_M0R)); o.i32(18, E.ll(L_M1R));
+    o.i32(19, E.ll(L_STORAGE));
     // machines (MachineAgent.py:62-70) and packaging (PackagingAgent.py:54-62)
-    o.i8[0] = (int8_t)E.m_busy[0]; o.i8[1] = to_i8(E, E.ll[L_M0Q]);
-    o.i8[2] = (int8_t)E.m_busy[1]; o.i8[3] = to_i8(E, E.ll[L_M1Q]);
-    o.f32[0] = E.m_prog[0] ? 1.0f : 0.0f;
-    o.f32[1] = E.m_prog[1] ? 1.0f : 0.0f;
+    o.i8(0, E.m_busy(0)); o.i8(1, obs_i8_checked(E, E.ll(L_M0Q)));
+    o.i8(2, E.m_busy(1)); o.i8(3, obs_i8_checked(E, E.ll(L_M1Q)));
+    o.f32(0, E.m_prog(0) ? 1.0f : 0.0f);
+    o.f32(1, E.m_prog(1) ? 1.0f : 0.0f);
 #pragma unroll
     for (int s = 0; s < 4; s++) {
-        o.i8[4 + 2 * s] = (int8_t)E.p_busy[s];
-        o.i8[5 + 2 * s] = to_i8(E, E.p_queued[s]);
-        o.f32[2 + s] = E.p_prog[s];
+        o.i8(4 + 2 * s, E.p_busy(s));
+        o.i8(5 + 2 * s, obs_i8_checked(E, E.p_queued(s)));
+        o.f32(2 + s, E.p_prog(s));
     }
-    compute_masks(E, C, o.mask);
+    compute_masks(E, C, o);
 }
 
 // ---------------------------------------------------------------- reset
+// Fresh episode state (FJSPSimulation.reset: new agents, storage, tray pool); the MT cursor
+// (W3) is kept.
 FJSP_DEV void env_clear(Env& E, const Cfg& C) {
-    E.step = 0; E.next_order = 0; E.ncompleted = 0; E.total_packaged = 0; E.status = 0;
-    E.cur_order = -1; E.cur_idx = 0; E.cur_n = 0; E.cur_type = 0; E.cur_color = 0;
-    E.tray_valid = 0; E.tray_order = 0; E.tray_start = 0; E.tray_count = 0;
-    E.pool = C.pool0; E.slot_next = 0;
-    E.loc = LOC_PICKUP; E.carry = NIL; E.carry_code = 0; E.carry_type = 0; E.carry_color = 0; E.carry_np = 0; E.carry_nk = 0;
+    const uint32_t mt = E.w[3];
 #pragma unroll
-    for (int l = 0; l < NLIST; l++) { E.lh[l] = NIL; E.lt[l] = NIL; E.ll[l] = 0; }
+    for (int i = 0; i < NSTATE; i++) E.w[i] = 0;
+    E.w[3] = mt;
+    E.w[4] = 0xFFu;                                            // cur_order = none
+    E.w[5] = (uint32_t)C.pool0 << 8;                           // tray pool, slot_next = 0
+    E.w[6] = (uint32_t)LOC_PICKUP | ((uint32_t)NIL << 3);      // AGV at pickup, carrying nothing
 #pragma unroll
-    for (int m = 0; m < 2; m++) { E.m_busy[m] = 0; E.m_cur[m] = NIL; E.m_code[m] = 0; E.m_prog[m] = 0; E.m_k[m] = 0; E.m_next[m] = 0; }
+    for (int l = 0; l < NLIST; l++) E.w[7 + l] = (uint32_t)NIL | ((uint32_t)NIL << 8);
 #pragma unroll
-    for (int s = 0; s < 4; s++) {
-        E.p_busy[s] = 0; E.p_hascur[s] = 0; E.p_completed[s] = 0; E.p_qfirst[s] = NIL;
-        E.p_inflight[s] = 0; E.p_queued[s] = 0; E.p_prog[s] = 0.0f;
-    }
+    for (int m = 0; m < 2; m++) E.w[17 + m] = (uint32_t)NIL << 1;
+#pragma unroll
+    for (int s = 0; s < 4; s++) E.w[20 + s] = (uint32_t)NIL << 2;
 }
 
 // ---------------------------------------------------------------- one step
-// actions[a] for agent a in canonical order; order = execution order (CANON -> 0..7).
-// Returns the number of orders completed this step; fills res[8] and rewards[8].
+// calculate_local_reward (utils/RewardModel.py:46-97) as one table lookup (build_reward_lut).
+FJSP_DEV double local_reward(const Cfg& C, int a, uint32_t r, int act) {
+    const uint32_t a0 = act == 0;   // actions.get(agent_id, 0) == 0 (absent agents have r == 0)
+    const uint32_t f = (r >> 1) & 7u;
+    const uint32_t idx = a == 0 ? (f | (a0 << 3)) : a == 1 ? 16u + ((r >> 1) & 31u)
+                                                           : (a <= 3 ? 48u : 64u) + (f | (a0 << 3));
+    return C.lut[idx];
+}
+
+// Actions in dict order, then env.run in closed form.  actions[a] for agent a (canonical order);
+// order = execution order (CANON -> 0..7).  Fills res[8]; returns the shared global reward / 8.
 template <bool CANON>
-FJSP_DEV void env_step(Env& E, const Tables& T, const Cfg& C, const int* act, const uint8_t* order,
-                       uint32_t* res, double* rew) {
+FJSP_DEV double env_advance(Env& E, const Tables& T, const Cfg& C, const int* act, const uint8_t* order,
+                            uint32_t* res) {
     int move_to = 0, m_start[2] = {-1, -1}, p_started[4] = {0, 0, 0, 0};
-    const int products_before = E.total_packaged;
+    const int products_before = E.total_packaged();
     // 1. actions in dict order (FJSPSimulation.py:172-174)
 #pragma unroll
     for (int i = 0; i < NA; i++) {
@@ -532,8 +724,9 @@ FJSP_DEV void env_step(Env& E, const Tables& T, const Cfg& C, const int* act, co
         }
         res[a] = r;
     }
+    FJSP_STAMP(E, 1);
     // 2. env.run(until=now+step_size) in closed form
-    if (move_to) E.loc = move_to;
+    if (move_to) E.set_loc(move_to);
     machine_run<0>(E, T, C, m_start[0]);
     machine_run<1>(E, T, C, m_start[1]);
     int orders_done = 0;
@@ -541,38 +734,22 @@ FJSP_DEV void env_step(Env& E, const Tables& T, const Cfg& C, const int* act, co
     pack_run<1>(E, T, C, p_started[1], &orders_done);
     pack_run<2>(E, T, C, p_started[2], &orders_done);
     pack_run<3>(E, T, C, p_started[3], &orders_done);
-    E.ncompleted += orders_done;
-    // 3-4. rewards (RewardModel.calculate_global_reward / calculate_local_reward / combine)
-    double g = C.w[W_ORDER] * (double)orders_done;
-    g += C.w[W_THROUGHPUT] * (double)(E.total_packaged - products_before);
-    g += C.w[W_TIME] * (double)C.step_size;
-    const double g8 = g / 8.0;   // combine_rewards: global / len(self.agents)
+    E.set_ncompleted(E.ncompleted() + orders_done);
+    FJSP_STAMP(E, 2);
+    // 3. calculate_global_reward; combine_rewards divides it by len(self.agents)
+    double g = C.lut[80] * (double)orders_done;
+    g += C.lut[81] * (double)(E.total_packaged() - products_before);
+    g += C.lut[82];
+    return g / 8.0;
+}
+
+// One step with rewards (host harness / tests): r_a = g / 8 + local_a (combine_rewards).
+template <bool CANON>
+FJSP_DEV void env_step(Env& E, const Tables& T, const Cfg& C, const int* act, const uint8_t* order, uint32_t* res,
+                       double* rew) {
+    const double g8 = env_advance<CANON>(E, T, C, act, order, res);
 #pragma unroll
-    for (int a = 0; a < NA; a++) {
-        const uint32_t r = res[a];
-        const int a0 = act[a] == 0;   // actions.get(agent_id, 0) == 0 (absent agents: r == 0)
-        double loc = 0.0;
-        if (a == 0) {
-            if (r & 2u) loc += C.w[W_PICK_LOAD];
-            if (r & 4u) loc += C.w[W_PICK_TRAY];
-            if (a0 && (r & 8u)) loc += C.w[W_PICK_IDLE];
-        } else if (a == 1) {
-            if (r & 8u) loc += C.w[W_AGV_DELIVERY];
-            if (r & 16u) loc += C.w[W_AGV_DELIVERY];
-            if (r & 32u) loc += C.w[W_AGV_PACKAGING];
-            if (r & 4u) loc += C.w[W_AGV_MOVE];
-            if (r & 2u) loc += C.w[W_AGV_INVALID];
-        } else if (a <= 3) {
-            if (r & 2u) loc += C.w[W_M_START];
-            if (r & 4u) loc += C.w[W_M_COMPLETE];
-            if (a0 && (r & 8u)) loc += C.w[W_M_IDLE];
-        } else {
-            if (r & 2u) loc += C.w[W_P_START];
-            if (r & 4u) loc += C.w[W_P_COMPLETE];
-            if (a0 && (r & 8u)) loc += C.w[W_P_IDLE];
-        }
-        rew[a] = g8 + loc;
-    }
+    for (int a = 0; a < NA; a++) rew[a] = g8 + local_reward(C, a, res[a], act[a]);
 }
 
 }  // namespace fjsp

@@ -29,6 +29,9 @@ namespace {
 
 constexpr int BLOCK = 64;
 constexpr int MT_N = 624;
+#ifdef FJSP_STAMPS
+__device__ unsigned long long g_stamps[8];
+#endif
 
 struct DevState {
     uint32_t* words;
@@ -40,74 +43,17 @@ struct DevState {
     int n;
 };
 
-// ---------------------------------------------------------------- pack / unpack of Env
+// ---------------------------------------------------------------- load / store of Env
+// The register state is the HBM row layout itself (fjsp_env.h, struct Env): 30 coalesced words.
 __device__ __forceinline__ void env_load(Env& E, const uint32_t* __restrict__ w, int n, int e) {
-    auto W = [&](int i) { return w[i * n + e]; };
-    uint32_t x;
-    x = W(0); E.step = x & 0xFFFF; E.norders = (x >> 16) & 0xFF; E.next_order = x >> 24;
-    x = W(1); E.ncompleted = x & 0xFF; E.total_packaged = x >> 8;
-    E.status = W(2);
-    E.mti = W(3);
-    x = W(4);
-    E.cur_order = (x & 0xFF) == 0xFF ? -1 : (int)(x & 0xFF);
-    E.cur_idx = (x >> 8) & 15; E.cur_n = (x >> 12) & 15; E.cur_type = (x >> 16) & 3; E.cur_color = (x >> 18) & 3;
-    E.tray_valid = (x >> 20) & 1; E.tray_count = (x >> 21) & 7; E.tray_start = (x >> 24) & 15;
-    x = W(5); E.tray_order = x & 0xFF; E.pool = (x >> 8) & 0xFFFF; E.slot_next = x >> 24;
-    x = W(6);
-    E.loc = x & 7; E.carry = (x >> 3) & 0xFF; E.carry_code = (x >> 11) & 0x1FFF; E.carry_type = (x >> 24) & 3;
-    E.carry_color = (x >> 26) & 3; E.carry_np = (x >> 28) & 1; E.carry_nk = (x >> 29) & 1;
 #pragma unroll
-    for (int l = 0; l < NLIST; l++) {
-        x = W(7 + l); E.lh[l] = x & 0xFF; E.lt[l] = (x >> 8) & 0xFF; E.ll[l] = x >> 16;
-    }
-#pragma unroll
-    for (int m = 0; m < 2; m++) {
-        x = W(17 + m);
-        E.m_busy[m] = x & 1; E.m_cur[m] = (x >> 1) & 0xFF; E.m_code[m] = (x >> 9) & 0x1FFF;
-        E.m_prog[m] = (x >> 22) & 1; E.m_k[m] = (x >> 23) & 15;
-    }
-    x = W(19); E.m_next[0] = x & 0xFFFF; E.m_next[1] = x >> 16;
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-        x = W(20 + s);
-        E.p_busy[s] = x & 1; E.p_hascur[s] = (x >> 1) & 1; E.p_qfirst[s] = (x >> 2) & 0xFF;
-        E.p_inflight[s] = (x >> 10) & 0xFF; E.p_queued[s] = (x >> 18) & 0x3FFF;
-    }
-    x = W(24); E.p_completed[0] = x & 0xFFFF; E.p_completed[1] = x >> 16;
-    x = W(25); E.p_completed[2] = x & 0xFFFF; E.p_completed[3] = x >> 16;
-#pragma unroll
-    for (int s = 0; s < 4; s++) E.p_prog[s] = __uint_as_float(W(26 + s));
+    for (int i = 0; i < NSTATE; i++) E.w[i] = w[i * n + e];
 }
-
 __device__ __forceinline__ void env_store(const Env& E, uint32_t* __restrict__ w, int n, int e) {
-    auto W = [&](int i, uint32_t v) { w[i * n + e] = v; };
-    W(0, (uint32_t)E.step | ((uint32_t)E.norders << 16) | ((uint32_t)E.next_order << 24));
-    W(1, (uint32_t)E.ncompleted | ((uint32_t)E.total_packaged << 8));
-    W(2, E.status);
-    W(3, (uint32_t)E.mti);
-    W(4, (uint32_t)(E.cur_order < 0 ? 0xFF : E.cur_order) | ((uint32_t)E.cur_idx << 8) | ((uint32_t)E.cur_n << 12) |
-             ((uint32_t)E.cur_type << 16) | ((uint32_t)E.cur_color << 18) | ((uint32_t)E.tray_valid << 20) |
-             ((uint32_t)E.tray_count << 21) | ((uint32_t)E.tray_start << 24));
-    W(5, (uint32_t)E.tray_order | ((uint32_t)E.pool << 8) | ((uint32_t)E.slot_next << 24));
-    W(6, (uint32_t)E.loc | ((uint32_t)E.carry << 3) | ((uint32_t)E.carry_code << 11) | ((uint32_t)E.carry_type << 24) |
-             ((uint32_t)E.carry_color << 26) | ((uint32_t)E.carry_np << 28) | ((uint32_t)E.carry_nk << 29));
 #pragma unroll
-    for (int l = 0; l < NLIST; l++) W(7 + l, (uint32_t)E.lh[l] | ((uint32_t)E.lt[l] << 8) | ((uint32_t)E.ll[l] << 16));
-#pragma unroll
-    for (int m = 0; m < 2; m++)
-        W(17 + m, (uint32_t)E.m_busy[m] | ((uint32_t)E.m_cur[m] << 1) | ((uint32_t)E.m_code[m] << 9) |
-                      ((uint32_t)E.m_prog[m] << 22) | ((uint32_t)E.m_k[m] << 23));
-    W(19, (uint32_t)E.m_next[0] | ((uint32_t)E.m_next[1] << 16));
-#pragma unroll
-    for (int s = 0; s < 4; s++)
-        W(20 + s, (uint32_t)E.p_busy[s] | ((uint32_t)E.p_hascur[s] << 1) | ((uint32_t)E.p_qfirst[s] << 2) |
-                      ((uint32_t)(E.p_inflight[s] & 0xFF) << 10) | ((uint32_t)(E.p_queued[s] & 0x3FFF) << 18));
-    W(24, (uint32_t)(E.p_completed[0] & 0xFFFF) | ((uint32_t)E.p_completed[1] << 16));
-    W(25, (uint32_t)(E.p_completed[2] & 0xFFFF) | ((uint32_t)E.p_completed[3] << 16));
-#pragma unroll
-    for (int s = 0; s < 4; s++) W(26 + s, __float_as_uint(E.p_prog[s]));
+    for (int i = 0; i < NSTATE; i++) w[i * n + e] = E.w[i];
 }
-static_assert(NWORDS >= 30, "packed state needs 30 words");
+static_assert(NWORDS >= NSTATE, "state buffer rows");
 
 // ---------------------------------------------------------------- MT19937, lazily twisted
 // State word: mti (bits 0..9) | g (bits 16..25).  Words [0, g) of the array already hold the
@@ -156,18 +102,105 @@ __device__ void mt_seed(uint32_t* __restrict__ mt, int n, int e, uint32_t seed) 
     }
 }
 
-// FJSPSimulation.reset body after the optional reseed (FJSPSimulation.py:301-320)
-__device__ void env_reset(Env& E, const Tables& T, const Cfg& C, const DevState& S, int e, int num_orders) {
-    env_clear(E, C);
-    E.norders = num_orders;
-    int mti = E.mti;
-    for (int o = 0; o < num_orders; o++) {     // generate_order (FJSPSimulation.py:101-131)
-        const int n = 1 + mt_bounded(S.mt, S.n, e, mti, 8u, 15u);    // randint(1, 10)
-        const int ty = 1 + mt_bounded(S.mt, S.n, e, mti, 2u, 3u);    // choice(list(ProductType))
-        const int co = 1 + mt_bounded(S.mt, S.n, e, mti, 2u, 3u);    // choice(list(PackagingColor))
-        T.orders[o * T.stride] = ow_make(n, ty, co);
+// Batched reader of the lazily twisted MT19937 stream for resets.  A refill issues every load
+// of up to MTB words at once (mt[i..i+MTB] and mt[i+397..]) and waits once, instead of one
+// dependent round trip per draw: inside the step kernels every wait also drains the lane's
+// outstanding output stores.  Regenerated words are stored back (same in-place recurrence as
+// mt_draw); tempered outputs are staged in a per-lane LDS buffer `buf` (stride BLOCK).
+// Consumption (the rejection loops, divergent across lanes) only reads LDS; refills happen at
+// one wave-uniform point, so the lanes of a wave share each memory round trip.
+constexpr int MTB = 32;
+struct MtReader {
+    uint32_t* mt;
+    uint32_t* buf;   // LDS, element j at buf[j * BLOCK]
+    int n, e;
+    int pos, g;      // next word to consume, regenerated prefix of the current block
+    int bi, bcnt;    // consumption index / size of the staged batch
+
+    // Branch-free: every load is issued unconditionally (indices wrapped into the block) so
+    // the 2*MTB + 1 loads leave back to back and the lane waits once; stores are predicated.
+    __device__ __forceinline__ void fill() {
+        const int cnt = (MT_N - pos) < MTB ? (MT_N - pos) : MTB;
+        uint32_t a[MTB + 1], c[MTB];
+#pragma unroll
+        for (int j = 0; j <= MTB; j++) {
+            int idx = pos + j;
+            idx = idx >= MT_N ? idx - MT_N : idx;   // j == cnt at the block end reads mt[0] (new word 0)
+            a[j] = mt[idx * n + e];
+        }
+#pragma unroll
+        for (int j = 0; j < MTB; j++) {
+            int im = pos + j + 397;
+            im = im >= MT_N ? im - MT_N : im;
+            c[j] = mt[im * n + e];
+        }
+#pragma unroll
+        for (int j = 0; j < MTB; j++) {
+            const int idx = pos + j;
+            const uint32_t y = (a[j] & 0x80000000u) | (a[j + 1] & 0x7fffffffu);
+            const uint32_t regen = c[j] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+            const bool fresh = idx >= g;
+            uint32_t v = fresh ? regen : a[j];
+            if (fresh && j < cnt) mt[idx * n + e] = v;
+            v ^= v >> 11;
+            v ^= (v << 7) & 0x9d2c5680u;
+            v ^= (v << 15) & 0xefc60000u;
+            v ^= v >> 18;
+            buf[j * BLOCK] = v;
+        }
+        if (pos + cnt > g) g = pos + cnt;
+        bi = 0;
+        bcnt = cnt;
     }
-    E.mti = mti;
+    __device__ __forceinline__ uint32_t next() {   // caller guarantees bi < bcnt
+        const uint32_t v = buf[bi * BLOCK];
+        bi += 1;
+        pos += 1;
+        if (pos == MT_N) { pos = 0; g = 0; }
+        return v;
+    }
+};
+
+// FJSPSimulation.reset body after the optional reseed (FJSPSimulation.py:301-320).
+// generate_order draws randint(1, 10) then choice(ProductType) then choice(PackagingColor)
+// per order (FJSPSimulation.py:107,111-112): field f = 3 * order + k with numpy's masked
+// rejection (rng 8 / mask 15 for k = 0, rng 2 / mask 3 otherwise).
+// mtbuf: this lane's LDS staging buffer for the MT reader (MTB words, stride BLOCK).
+__device__ __forceinline__ void env_reset(Env& E, const Tables& T, const Cfg& C, const DevState& S, int e, int num_orders,
+                                          uint32_t* mtbuf) {
+    env_clear(E, C);
+    E.set_norders(num_orders);
+    MtReader R{S.mt, mtbuf, S.n, e, E.mti() & 0x3FF, (E.mti() >> 16) & 0x3FF, 0, 0};
+    const int nf = 3 * num_orders;
+    int f = 0, k = 0, np = 0, ty = 0;
+    for (;;) {
+        while (f < nf && R.bi < R.bcnt) {   // LDS-only consumption
+            const uint32_t x = R.next() & (k == 0 ? 15u : 3u);
+            if (x > (k == 0 ? 8u : 2u)) continue;   // rejected draw
+            if (k == 0) { np = 1 + (int)x; k = 1; }
+            else if (k == 1) { ty = 1 + (int)x; k = 2; }
+            else { T.orders[(f / 3) * T.stride] = ow_make(np, ty, 1 + (int)x); k = 0; }
+            f += 1;
+        }
+        const bool need = f < nf;
+        if (!__any(need)) break;   // wave-uniform refill point
+        if (need) R.fill();
+    }
+    E.set_mti(R.pos | (R.g << 16));
+}
+
+// Auto-reset inside the step kernels is a cold path (once per ~200 steps): a non-inlined call
+// keeps the MT reader's registers out of the hot loop's allocation.  Everything is passed and
+// returned by value so the env state never has its address taken (it stays in VGPRs).
+#ifdef FJSP_RESET_INLINE
+__device__ __forceinline__
+#else
+__device__ __attribute__((noinline))
+#endif
+Env env_reset_cold(Env E, Tables T, Cfg C, DevState S, int e, int num_orders,
+                                                        uint32_t* mtbuf) {
+    env_reset(E, T, C, S, e, num_orders, mtbuf);
+    return E;
 }
 
 __device__ __forceinline__ Tables tables_of(const DevState& S, int e) {
@@ -186,25 +219,16 @@ template <class V>
 __device__ __forceinline__ void st32(V* base, uint32_t elem, V v) {
     *reinterpret_cast<V*>(reinterpret_cast<char*>(base) + elem * (uint32_t)sizeof(V)) = v;
 }
-__device__ __forceinline__ void write_obs(const Obs& o, int32_t* i32, int8_t* i8, float* f32, int8_t* mk, uint32_t t,
-                                          uint32_t n, uint32_t e) {
-    if (i32) {
-#pragma unroll
-        for (uint32_t f = 0; f < NI32; f++) st32(i32, (t * NI32 + f) * n + e, o.i32[f]);
-    }
-    if (i8) {
-#pragma unroll
-        for (uint32_t f = 0; f < NI8; f++) st32(i8, (t * NI8 + f) * n + e, o.i8[f]);
-    }
-    if (f32) {
-#pragma unroll
-        for (uint32_t f = 0; f < NF32; f++) st32(f32, (t * NF32 + f) * n + e, o.f32[f]);
-    }
-    if (mk) {
-#pragma unroll
-        for (uint32_t f = 0; f < NMASK; f++) st32(mk, (t * NMASK + f) * n + e, o.mask[f]);
-    }
-}
+// Sink that stores each observation field as soon as it is computed (fjsp_env.h observe()).
+struct StoreSink {
+    int32_t* pi32; int8_t* pi8; float* pf32; int8_t* pmk;
+    uint32_t t, n, e;
+    __device__ __forceinline__ void i32(int f, int v) { if (pi32) st32(pi32, (t * NI32 + (uint32_t)f) * n + e, (int32_t)v); }
+    __device__ __forceinline__ void i8(int f, int v) { if (pi8) st32(pi8, (t * NI8 + (uint32_t)f) * n + e, (int8_t)v); }
+    __device__ __forceinline__ void f32(int f, float v) { if (pf32) st32(pf32, (t * NF32 + (uint32_t)f) * n + e, v); }
+    __device__ __forceinline__ void mask(int f, int v) { if (pmk) st32(pmk, (t * NMASK + (uint32_t)f) * n + e, (int8_t)v); }
+};
+
 
 __global__ void __launch_bounds__(BLOCK) k_seed(DevState S, const uint32_t* __restrict__ seeds, uint32_t seed_base) {
     const int e = blockIdx.x * BLOCK + threadIdx.x;
@@ -215,6 +239,7 @@ __global__ void __launch_bounds__(BLOCK) k_seed(DevState S, const uint32_t* __re
 
 __global__ void __launch_bounds__(BLOCK) k_reset(DevState S, Cfg C, const uint32_t* __restrict__ seeds,
                                                  const uint8_t* __restrict__ env_mask, int num_orders, fjsp_out out) {
+    __shared__ uint32_t s_mtbuf[MTB * BLOCK];
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     if (e >= S.n) return;
     if (env_mask && !env_mask[e]) return;
@@ -222,13 +247,12 @@ __global__ void __launch_bounds__(BLOCK) k_reset(DevState S, Cfg C, const uint32
     Env E;
     int mti = (int)S.words[3 * S.n + e];
     if (seeds) { mt_seed(S.mt, S.n, e, seeds[e]); mti = 0; }
-    E.mti = mti;
-    env_reset(E, T, C, S, e, num_orders);
+    E.set_mti(mti);
+    env_reset(E, T, C, S, e, num_orders, s_mtbuf + threadIdx.x);
+    StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, 0u, (uint32_t)S.n, (uint32_t)e};
+    observe(E, C, sink);
     env_store(E, S.words, S.n, e);
-    Obs o;
-    observe(E, C, o);
-    write_obs(o, out.obs_i32, out.obs_i8, out.obs_f32, out.masks, 0u, (uint32_t)S.n, (uint32_t)e);
-    if (out.status) out.status[e] = E.status;
+    if (out.status) out.status[e] = E.status();
 }
 
 // fmix64 counter RNG for synthetic actions (oracle_actions spec)
@@ -248,15 +272,11 @@ __device__ __forceinline__ void synth_actions(uint64_t seed, uint32_t gid, uint3
         for (int a = 0; a < NA; a++) act[a] = (int)((((uint32_t)(h >> (8 * a)) & 0xFFu) * (uint32_t)nact[a]) >> 8);
         return;
     }
-    int8_t m[NMASK];
-    compute_masks(E, C, m);
-    const int moff[NA] = {0, 3, 11, 14, 17, 20, 23, 26};
+    MaskBits mb;
+    compute_masks(E, C, mb);
 #pragma unroll
     for (int a = 0; a < NA; a++) {
-        uint32_t bits = 0;
-#pragma unroll
-        for (int i = 0; i < 8; i++)
-            if (i < nact[a] && m[moff[a] + i]) bits |= 1u << i;
+        const uint32_t bits = mb.bits[a];
         const int cnt = __popc(bits);
         int j = (int)((((uint32_t)(h >> (8 * a)) & 0xFFu) * (uint32_t)cnt) >> 8);
         // j-th set bit
@@ -267,44 +287,55 @@ __device__ __forceinline__ void synth_actions(uint64_t seed, uint32_t gid, uint3
 }
 
 // One full env step + outputs at trajectory index t; handles auto-reset.
-template <bool CANON>
+// FULL = false: only obs, masks, rewards, term, trunc and status are written (the other
+// fjsp_out pointers are never read, so they take no SGPRs in the hot loop).
+template <bool CANON, bool FULL = true>
 __device__ __forceinline__ void step_and_emit(Env& E, const Tables& T, const Cfg& C, const DevState& S, int e,
                                               const int* act, const uint8_t* order, int autoreset, const fjsp_out& out,
-                                              uint32_t t) {
+                                              uint32_t t, uint32_t* mtbuf) {
     const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
     uint32_t res[NA];
-    double rew[NA];
-    env_step<CANON>(E, T, C, act, order, res, rew);
-    Obs o;
-    observe(E, C, o);
-    const int all_done = E.ncompleted == E.norders && E.norders > 0 && E.next_order == E.norders;
-    const int truncated = E.step >= C.max_steps;
-    write_obs(o, out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, ue);
+    const double g8 = env_advance<CANON>(E, T, C, act, order, res);
     if (out.rewards) {
 #pragma unroll
-        for (int a = 0; a < NA; a++) st32(out.rewards, (t * NA + (uint32_t)a) * n + ue, rew[a]);
+        for (int a = 0; a < NA; a++) st32(out.rewards, (t * NA + (uint32_t)a) * n + ue, g8 + local_reward(C, a, res[a], act[a]));
     }
-    if (out.results) {
+    if (FULL && out.results) {
 #pragma unroll
         for (int a = 0; a < NA; a++) st32(out.results, (t * NA + (uint32_t)a) * n + ue, res[a]);
     }
+    FJSP_STAMP(E, 3);
+    StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, ue};
+    observe(E, C, sink);
+    FJSP_STAMP(E, 4);
+    const int nord = E.norders();
+    const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
+    const int truncated = E.step() >= C.max_steps;
     if (out.term) st32(out.term, t * n + ue, (uint8_t)all_done);
     if (out.trunc) st32(out.trunc, t * n + ue, (uint8_t)truncated);
-    if (out.orders_completed) st32(out.orders_completed, t * n + ue, E.ncompleted);
-    if (out.packaged) st32(out.packaged, t * n + ue, E.total_packaged);
-    if (out.sim_time) st32(out.sim_time, t * n + ue, (double)(E.step + 1) * (double)C.step_size);
-    if (out.status) st32(out.status, t * n + ue, E.status);
-    E.step += 1;
-    if (autoreset && (all_done || truncated)) {
-        env_reset(E, T, C, S, e, E.norders);   // reset(seed=None) continues the MT stream
-        observe(E, C, o);
+    if (FULL && out.orders_completed) st32(out.orders_completed, t * n + ue, E.ncompleted());
+    if (FULL && out.packaged) st32(out.packaged, t * n + ue, E.total_packaged());
+    if (FULL && out.sim_time) st32(out.sim_time, t * n + ue, (double)(E.step() + 1) * (double)C.step_size);
+    if (out.status) st32(out.status, t * n + ue, E.status());
+    FJSP_STAMP(E, 5);
+    E.set_step(E.step() + 1);
+    if (autoreset && (all_done || truncated))
+        E = env_reset_cold(E, T, C, S, e, nord, mtbuf);   // reset(seed=None) continues the MT stream
+    if (FULL && (out.next_i32 || out.next_i8 || out.next_f32 || out.next_masks)) {
+        StoreSink nsink{out.next_i32, out.next_i8, out.next_f32, out.next_masks, t, n, ue};
+        observe(E, C, nsink);
     }
-    write_obs(o, out.next_i32, out.next_i8, out.next_f32, out.next_masks, t, n, ue);
+    FJSP_STAMP(E, 6);
 }
 
 template <bool CANON>
 __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t* __restrict__ actions, uint64_t order_packed,
                                                 int autoreset, fjsp_out out) {
+    __shared__ uint32_t s_mtbuf[MTB * BLOCK];
+    __shared__ double s_lut[RLUT_SIZE];
+    for (int i = threadIdx.x; i < RLUT_SIZE; i += BLOCK) s_lut[i] = C.lut[i];
+    __syncthreads();
+    C.lut = s_lut;
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     if (e >= S.n) return;
     Tables T = tables_of(S, e);
@@ -316,7 +347,7 @@ __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t
     uint8_t order[NA];
 #pragma unroll
     for (int i = 0; i < NA; i++) order[i] = (uint8_t)(order_packed >> (8 * i));
-    step_and_emit<CANON>(E, T, C, S, e, act, order, autoreset, out, 0);
+    step_and_emit<CANON>(E, T, C, S, e, act, order, autoreset, out, 0, s_mtbuf + threadIdx.x);
     env_store(E, S.words, S.n, e);
 }
 
@@ -324,14 +355,19 @@ __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t
 // the whole launch (one 64-lane workgroup = 64 envs, 97.5 KB of LDS), so the linked-list
 // walks and order-word read-modify-writes of the step are ds_* round trips (~100 cycles)
 // instead of L2/HBM round trips; only the used prefix is copied in and out.
-template <bool LDS>
+template <bool LDS, bool FULL>
 __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0,
                                                      uint32_t step0, int mode, int autoreset, fjsp_out out) {
     __shared__ uint32_t s_orders[LDS ? MAX_ORDERS * BLOCK : 1];
     __shared__ uint16_t s_code[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint8_t s_next[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint16_t s_cstep[LDS ? MAX_SLOTS * BLOCK : 1];
+    __shared__ uint32_t s_mtbuf[MTB * BLOCK];
+    __shared__ double s_lut[RLUT_SIZE];
     const int lane = threadIdx.x;
+    for (int i = lane; i < RLUT_SIZE; i += BLOCK) s_lut[i] = C.lut[i];
+    __syncthreads();
+    C.lut = s_lut;
     const int e = blockIdx.x * BLOCK + lane;
     if (e >= S.n) return;
     Env E;
@@ -343,8 +379,8 @@ __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, u
         T.snext = s_next + lane;
         T.scstep = s_cstep + lane;
         T.stride = BLOCK;
-        for (int o = 0; o < E.norders; o++) T.orders[o * BLOCK] = S.orders[(size_t)o * S.n + e];
-        for (int s = 0; s < E.slot_next; s++) {
+        for (int o = 0; o < E.norders(); o++) T.orders[o * BLOCK] = S.orders[(size_t)o * S.n + e];
+        for (int s = 0; s < E.slot_next(); s++) {
             T.scode[s * BLOCK] = S.scode[(size_t)s * S.n + e];
             T.snext[s * BLOCK] = S.snext[(size_t)s * S.n + e];
             T.scstep[s * BLOCK] = S.scstep[(size_t)s * S.n + e];
@@ -352,20 +388,29 @@ __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, u
     } else {
         T = tables_of(S, e);
     }
+#ifdef FJSP_STAMPS
+    for (int i = 0; i < 8; i++) E.st_acc[i] = 0;
+    E.st_t0 = __builtin_amdgcn_s_memtime();
+#endif
     for (int k = 0; k < K; k++) {
         int act[NA];
         synth_actions(seed, gid0 + (uint32_t)e, step0 + (uint32_t)k, mode, E, C, act);
-        step_and_emit<true>(E, T, C, S, e, act, nullptr, autoreset, out, (uint32_t)k);
+        FJSP_STAMP(E, 0);
+        step_and_emit<true, FULL>(E, T, C, S, e, act, nullptr, autoreset, out, (uint32_t)k, s_mtbuf + lane);
     }
     if constexpr (LDS) {
-        for (int o = 0; o < E.norders; o++) S.orders[(size_t)o * S.n + e] = T.orders[o * BLOCK];
-        for (int s = 0; s < E.slot_next; s++) {
+        for (int o = 0; o < E.norders(); o++) S.orders[(size_t)o * S.n + e] = T.orders[o * BLOCK];
+        for (int s = 0; s < E.slot_next(); s++) {
             S.scode[(size_t)s * S.n + e] = T.scode[s * BLOCK];
             S.snext[(size_t)s * S.n + e] = T.snext[s * BLOCK];
             S.scstep[(size_t)s * S.n + e] = T.scstep[s * BLOCK];
         }
     }
     env_store(E, S.words, S.n, e);
+#ifdef FJSP_STAMPS
+    if (lane == 0)
+        for (int i = 0; i < 8; i++) atomicAdd((unsigned long long*)&g_stamps[i], (unsigned long long)E.st_acc[i]);
+#endif
 }
 
 // transition_memory.py:83-105 over a [T][M] rollout buffer; column m = a*N + e
@@ -412,6 +457,8 @@ struct fjsp_handle {
     int has_reset;
     hipEvent_t ev0, ev1;
     int timed;
+    double* lut_dev;
+    double lut_host[RLUT_SIZE];
     int use_lds;   // fused kernel variant (FJSP_FUSED_LDS env var / fjsp_set_option)
 };
 
@@ -476,7 +523,11 @@ int fjsp_default_reward_weights(fjsp_reward_weights* w) {
 
 int fjsp_set_reward_weights(fjsp_handle* h, const fjsp_reward_weights* w) {
     if (!h || !w) return fail("null argument");
-    memcpy(h->dcfg.w, w, sizeof(h->dcfg.w));
+    DeviceGuard g(h->device);
+    build_reward_lut(reinterpret_cast<const double*>(w), h->cfg.step_size, h->lut_host);
+    // stream-ordered: launches queued before this call keep the old table contents
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipMemcpy(h->lut_dev, h->lut_host, sizeof(double) * RLUT_SIZE, hipMemcpyHostToDevice));
     return 0;
 }
 
@@ -510,10 +561,10 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     h->device = device;
     h->stream = (hipStream_t)hip_stream;
     {
-        // the LDS variant holds 97.5 KB per 64-env workgroup (one workgroup per CU): use it
-        // only while every workgroup gets a CU of its own (256 CUs x 64 envs)
+        // the LDS variant (97.5 KB per 64-env workgroup) measured no faster than the
+        // global-table variant once resets stopped draining the store queue; opt-in only
         const char* v = getenv("FJSP_FUSED_LDS");
-        h->use_lds = v ? atoi(v) : (num_envs <= 256 * BLOCK);
+        h->use_lds = v ? atoi(v) : 0;
     }
     h->dcfg.step_size = c.step_size;
     h->dcfg.max_steps = c.max_episode_steps;
@@ -525,11 +576,7 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     h->dcfg.ptk_small = c.pt_small / c.step_size;
     h->dcfg.ptk_big = c.pt_big / c.step_size;
     h->dcfg.ptk_pack = c.pt_packaging / c.step_size;
-    {
-        fjsp_reward_weights w;
-        fjsp_default_reward_weights(&w);
-        memcpy(h->dcfg.w, &w, sizeof(h->dcfg.w));
-    }
+
     const size_t n = (size_t)num_envs;
     const size_t b_words = (size_t)NWORDS * n * 4, b_orders = (size_t)MAX_ORDERS * n * 4;
     const size_t b_scode = (size_t)MAX_SLOTS * n * 2, b_snext = (size_t)MAX_SLOTS * n, b_scstep = (size_t)MAX_SLOTS * n * 2;
@@ -550,6 +597,16 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     if (e == hipSuccess) e = hipEventCreate(&h->ev0);
     if (e == hipSuccess) e = hipEventCreate(&h->ev1);
     if (e != hipSuccess) { (void)hipFree(h->base); delete h; return hip_fail("init", e); }
+    e = hipMalloc(&h->lut_dev, sizeof(double) * RLUT_SIZE);
+    if (e != hipSuccess) { (void)hipFree(h->base); delete h; return hip_fail("hipMalloc(reward table)", e); }
+    h->dcfg.lut = h->lut_dev;
+    {
+        fjsp_reward_weights w;
+        fjsp_default_reward_weights(&w);
+        build_reward_lut(reinterpret_cast<const double*>(&w), c.step_size, h->lut_host);
+        e = hipMemcpy(h->lut_dev, h->lut_host, sizeof(double) * RLUT_SIZE, hipMemcpyHostToDevice);
+        if (e != hipSuccess) { (void)hipFree(h->lut_dev); (void)hipFree(h->base); delete h; return hip_fail("reward table", e); }
+    }
     // default streams: env e behaves like a process that called np.random.seed(e)
     hipLaunchKernelGGL(k_seed, dim3((h->n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, h->stream, h->S,
                        (const uint32_t*)nullptr, 0u);
@@ -565,6 +622,7 @@ int fjsp_destroy(fjsp_handle* h) {
     (void)hipStreamSynchronize(h->stream);
     (void)hipEventDestroy(h->ev0);
     (void)hipEventDestroy(h->ev1);
+    (void)hipFree(h->lut_dev);
     (void)hipFree(h->base);
     delete h;
     return 0;
@@ -639,12 +697,18 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
     DeviceGuard g(h->device);
     dim3 grid((h->n + BLOCK - 1) / BLOCK);
     HIPCHK(hipEventRecord(h->ev0, h->stream));
-    if (h->use_lds)
-        hipLaunchKernelGGL(k_step_many<true>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0,
-                           step0, action_mode, autoreset, traj ? *traj : kNoOut);
-    else
-        hipLaunchKernelGGL(k_step_many<false>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0,
-                           step0, action_mode, autoreset, traj ? *traj : kNoOut);
+    const fjsp_out o = traj ? *traj : kNoOut;
+    const bool full = o.results || o.orders_completed || o.packaged || o.sim_time || o.next_i32 || o.next_i8 ||
+                      o.next_f32 || o.next_masks;
+    auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0, step0,
+                           action_mode, autoreset, o);
+    };
+    if (h->use_lds) {
+        if (full) launch(k_step_many<true, true>); else launch(k_step_many<true, false>);
+    } else {
+        if (full) launch(k_step_many<false, true>); else launch(k_step_many<false, false>);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(h->ev1, h->stream));
     h->timed = 1;
@@ -672,6 +736,17 @@ int fjsp_gae_f64(const double* rewards, const double* values, const uint8_t* don
     HIPCHK(hipGetLastError());
     return 0;
 }
+
+#ifdef FJSP_STAMPS
+// diagnostic build only: accumulated per-phase wave cycles of k_step_many (and reset them)
+extern "C" int fjsp_debug_stamps(unsigned long long* out) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8));
+    unsigned long long z[8] = {0};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)));
+    return 0;
+}
+#endif
 
 int fjsp_sync(fjsp_handle* h) {
     if (!h) return fail("null handle");

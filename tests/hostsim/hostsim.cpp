@@ -5,7 +5,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
-#define FJSP_DEV static inline
+#define FJSP_DEV inline
 #include "../../multi-agent-rl-for-fjsp_amd/csrc/fjsp_env.h"
 using namespace fjsp;
 
@@ -14,7 +14,7 @@ struct HS {
     Env* E; uint32_t* orders; uint16_t* scode; uint8_t* snext; uint16_t* scstep;
     uint32_t (*mt)[624]; int* mti;
 };
-static uint32_t mt_next(uint32_t* s, int& mti) {
+static uint32_t mt_next_(uint32_t* s, int& mti) {
     if (mti >= 624) {
         for (int i = 0; i < 624; i++) {
             uint32_t y = (s[i] & 0x80000000u) | (s[(i + 1) % 624] & 0x7fffffffu);
@@ -27,7 +27,7 @@ static uint32_t mt_next(uint32_t* s, int& mti) {
     return y;
 }
 static int bounded(uint32_t* s, int& mti, uint32_t rng, uint32_t mask) {
-    uint32_t v; do { v = mt_next(s, mti) & mask; } while (v > rng); return (int)v;
+    uint32_t v; do { v = mt_next_(s, mti) & mask; } while (v > rng); return (int)v;
 }
 static Tables tabs(HS* h, int e) { Tables T; T.orders = h->orders + e; T.scode = h->scode + e; T.snext = h->snext + e; T.scstep = h->scstep + e; T.stride = h->n; return T; }
 
@@ -40,7 +40,9 @@ void* hs_create(const int32_t* c, int n) {
     h->C.storage_cap = c[3]; h->C.pool0 = c[0] < 1000 ? c[0] : 1000; h->C.pkg_cap = c[10];
     h->C.ptk_small = c[7] / c[4]; h->C.ptk_big = c[8] / c[4]; h->C.ptk_pack = c[9] / c[4];
     const double w[NW] = {100.0, 10.0, -0.1, 1.0, 5.0, -1.0, 2.0, -0.1, 10.0, -5.0, 5.0, 1.0, -2.0, 20.0, 2.0, -1.0};
-    for (int i = 0; i < NW; i++) h->C.w[i] = w[i];
+    double* lut = (double*)calloc(RLUT_SIZE, sizeof(double));
+    build_reward_lut(w, c[4], lut);
+    h->C.lut = lut;
     h->E = (Env*)calloc(n, sizeof(Env));
     h->orders = (uint32_t*)calloc((size_t)MAX_ORDERS * n, 4);
     h->scode = (uint16_t*)calloc((size_t)MAX_SLOTS * n, 2);
@@ -56,7 +58,7 @@ void hs_destroy(void* p) {
 static void reset_one(HS* h, int e, int num_orders) {
     Env& E = h->E[e]; Tables T = tabs(h, e);
     env_clear(E, h->C);
-    E.norders = num_orders;
+    E.set_norders(num_orders);
     for (int o = 0; o < num_orders; o++) {
         int n = 1 + bounded(h->mt[e], h->mti[e], 8, 15);
         int ty = 1 + bounded(h->mt[e], h->mti[e], 2, 3);
@@ -66,7 +68,7 @@ static void reset_one(HS* h, int e, int num_orders) {
 }
 // out: obs_i32[20], i8[12], f32[6], masks[29] per env (AoS for the harness)
 static void obs_out(HS* h, int e, int32_t* i32, int8_t* i8, float* f32, int8_t* mk) {
-    Obs o; observe(h->E[e], h->C, o);
+    Obs o; ObsSink sk{o}; observe(h->E[e], h->C, sk);
     memcpy(i32 + 20 * e, o.i32, 80); memcpy(i8 + 12 * e, o.i8, 12); memcpy(f32 + 6 * e, o.f32, 24); memcpy(mk + 29 * e, o.mask, 29);
 }
 void hs_reset(void* p, const uint32_t* seeds, int num_orders, int32_t* i32, int8_t* i8, float* f32, int8_t* mk) {
@@ -91,11 +93,12 @@ void hs_step(void* p, const uint8_t* actions, int autoreset, int32_t* i32, int8_
         int act[8]; for (int a = 0; a < 8; a++) act[a] = actions[8 * e + a];
         env_step<true>(E, T, h->C, act, nullptr, res + 8 * e, rew + 8 * e);
         obs_out(h, e, i32, i8, f32, mk);
-        int all_done = E.ncompleted == E.norders && E.norders > 0 && E.next_order == E.norders;
-        int tr = E.step >= h->C.max_steps;
-        term[e] = (uint8_t)all_done; trunc[e] = (uint8_t)tr; status[e] = E.status;
-        E.step += 1;
-        if (autoreset && (all_done || tr)) reset_one(h, e, E.norders);
+        const int nord = E.norders();
+        int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
+        int tr = E.step() >= h->C.max_steps;
+        term[e] = (uint8_t)all_done; trunc[e] = (uint8_t)tr; status[e] = E.status();
+        E.set_step(E.step() + 1);
+        if (autoreset && (all_done || tr)) reset_one(h, e, nord);
         obs_out(h, e, ri32, ri8, rf32, rmk);
     }
 }
