@@ -120,15 +120,35 @@ constexpr uint32_t ST_DIVERGED = 0x1u, ST_OBS_OVERFLOW = 0x2u, ST_PKG_WAIT = 0x4
 constexpr int NWORDS = 40;   // rows of the HBM state buffer (30 used)
 
 // Diagnostic build only (-DFJSP_STAMPS): per-wave s_memtime deltas per step phase.
+// -DFJSP_STAMPS_FINE splits the action phase per agent: slots 0 synth, 1 pickup, 2 AGV,
+// 3 machines, 4 packaging, 5 run, 6 rewards + observe + stores, 7 auto-reset.
 #ifdef FJSP_STAMPS
-#define FJSP_STAMP(E, i)                                   \
+#define FJSP_STAMP_AT(E, i)                                \
     do {                                                   \
         uint64_t _t = __builtin_amdgcn_s_memtime();        \
         (E).st_acc[i] += _t - (E).st_t0;                   \
         (E).st_t0 = _t;                                    \
     } while (0)
+#ifdef FJSP_STAMPS_FINE
+#define FJSP_STAMP(E, i)                                                          \
+    do {                                                                          \
+        constexpr int _m[7] = {0, -1, 5, 6, 6, 6, 7};                             \
+        if (_m[i] >= 0) FJSP_STAMP_AT(E, _m[i]);                                  \
+    } while (0)
+#define FJSP_STAMP_AGENT(E, a)                                                    \
+    do {                                                                          \
+        if ((a) == 0) FJSP_STAMP_AT(E, 1);                                        \
+        if ((a) == 1) FJSP_STAMP_AT(E, 2);                                        \
+        if ((a) == 3) FJSP_STAMP_AT(E, 3);                                        \
+        if ((a) == 7) FJSP_STAMP_AT(E, 4);                                        \
+    } while (0)
+#else
+#define FJSP_STAMP(E, i) FJSP_STAMP_AT(E, i)
+#define FJSP_STAMP_AGENT(E, a) ((void)0)
+#endif
 #else
 #define FJSP_STAMP(E, i) ((void)0)
+#define FJSP_STAMP_AGENT(E, a) ((void)0)
 #endif
 
 // Per-env register state: 30 packed u32 words, bit-identical to the HBM `words` rows, so
@@ -723,6 +743,7 @@ FJSP_DEV double env_advance(Env& E, const Tables& T, const Cfg& C, const int* ac
             }
         }
         res[a] = r;
+        if (CANON) FJSP_STAMP_AGENT(E, i);
     }
     FJSP_STAMP(E, 1);
     // 2. env.run(until=now+step_size) in closed form

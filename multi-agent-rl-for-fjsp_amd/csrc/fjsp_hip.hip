@@ -19,6 +19,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <string>
+#include <type_traits>
 
 #include "fjsp_env.h"
 #include "../../include/fjsp.h"
@@ -287,6 +288,86 @@ __device__ __forceinline__ void synth_actions(uint64_t seed, uint32_t gid, uint3
 }
 
 // One full env step + outputs at trajectory index t; handles auto-reset.
+// Per-wave LDS staging tile of one step's lean outputs ([F][64] per field block).  The step
+// writes it with ds_write (StageSink), then the wave copies each block out as whole 16-byte
+// chunks: ~15 global_store_dwordx4 (every instruction 1 KiB contiguous) instead of ~85
+// scalar-per-lane stores.  Requires N % 64 == 0 and 16-byte aligned outputs (host-checked).
+struct alignas(16) StageTile {
+    int32_t i32[NI32 * BLOCK];
+    float f32[NF32 * BLOCK];
+    double rew[NA * BLOCK];
+    uint32_t status[BLOCK];
+    int8_t i8[NI8 * BLOCK];
+    int8_t mask[NMASK * BLOCK];
+    uint8_t term[BLOCK];
+    uint8_t trunc[BLOCK];
+};
+struct StageSink {
+    StageTile* tl;
+    int lane;
+    __device__ __forceinline__ void i32(int f, int v) { tl->i32[f * BLOCK + lane] = v; }
+    __device__ __forceinline__ void i8(int f, int v) { tl->i8[f * BLOCK + lane] = (int8_t)v; }
+    __device__ __forceinline__ void f32(int f, float v) { tl->f32[f * BLOCK + lane] = v; }
+    __device__ __forceinline__ void mask(int f, int v) { tl->mask[f * BLOCK + lane] = (int8_t)v; }
+};
+// Copy ROWS rows of ROWBYTES from the tile to global rows spaced `gstride` bytes apart.
+template <int ROWS, int ROWBYTES>
+__device__ __forceinline__ void copy_rows(const void* tile, void* gbase, size_t gstride, int lane) {
+    constexpr int CPR = ROWBYTES / 16;
+    constexpr int TOTAL = ROWS * CPR;
+    const uint8_t* src = (const uint8_t*)tile;
+    uint8_t* dst = (uint8_t*)gbase;
+#pragma unroll
+    for (int c0 = 0; c0 < TOTAL; c0 += BLOCK) {
+        const int c = c0 + lane;
+        if (c < TOTAL) {
+            const int r = c / CPR, off = (c - r * CPR) * 16;
+            const uint4 v = *(const uint4*)(src + r * ROWBYTES + off);
+            *(uint4*)(dst + (size_t)r * gstride + off) = v;
+        }
+    }
+}
+__device__ __forceinline__ void copy_out(const StageTile& tl, const fjsp_out& out, uint32_t t, size_t n, int blk,
+                                         int lane) {
+    const size_t col = (size_t)blk * BLOCK;
+    if (out.obs_i32) copy_rows<NI32, 4 * BLOCK>(tl.i32, out.obs_i32 + (size_t)t * NI32 * n + col, n * 4, lane);
+    if (out.obs_f32) copy_rows<NF32, 4 * BLOCK>(tl.f32, out.obs_f32 + (size_t)t * NF32 * n + col, n * 4, lane);
+    if (out.rewards) copy_rows<NA, 8 * BLOCK>(tl.rew, out.rewards + (size_t)t * NA * n + col, n * 8, lane);
+    if (out.status) copy_rows<1, 4 * BLOCK>(tl.status, out.status + (size_t)t * n + col, n * 4, lane);
+    if (out.obs_i8) copy_rows<NI8, BLOCK>(tl.i8, out.obs_i8 + (size_t)t * NI8 * n + col, n, lane);
+    if (out.masks) copy_rows<NMASK, BLOCK>(tl.mask, out.masks + (size_t)t * NMASK * n + col, n, lane);
+    if (out.term) copy_rows<1, BLOCK>(tl.term, out.term + (size_t)t * n + col, n, lane);
+    if (out.trunc) copy_rows<1, BLOCK>(tl.trunc, out.trunc + (size_t)t * n + col, n, lane);
+}
+
+// Lean + LDS-staged variant of step_and_emit (obs, masks, rewards, term, trunc, status).
+__device__ __forceinline__ void step_and_emit_staged(Env& E, const Tables& T, const Cfg& C, const DevState& S, int e,
+                                                     const int* act, int autoreset, const fjsp_out& out, uint32_t t,
+                                                     uint32_t* mtbuf, StageTile* tl, int lane) {
+    uint32_t res[NA];
+    const double g8 = env_advance<true>(E, T, C, act, nullptr, res);
+#pragma unroll
+    for (int a = 0; a < NA; a++) tl->rew[a * BLOCK + lane] = g8 + local_reward(C, a, res[a], act[a]);
+    FJSP_STAMP(E, 3);
+    StageSink sink{tl, lane};
+    observe(E, C, sink);
+    FJSP_STAMP(E, 4);
+    const int nord = E.norders();
+    const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
+    const int truncated = E.step() >= C.max_steps;
+    tl->term[lane] = (uint8_t)all_done;
+    tl->trunc[lane] = (uint8_t)truncated;
+    tl->status[lane] = E.status();
+    __syncthreads();
+    copy_out(*tl, out, t, (size_t)S.n, blockIdx.x, lane);
+    __syncthreads();
+    FJSP_STAMP(E, 5);
+    E.set_step(E.step() + 1);
+    if (autoreset && (all_done || truncated))
+        E = env_reset_cold(E, T, C, S, e, nord, mtbuf);   // reset(seed=None) continues the MT stream
+    FJSP_STAMP(E, 6);
+}
+
 // FULL = false: only obs, masks, rewards, term, trunc and status are written (the other
 // fjsp_out pointers are never read, so they take no SGPRs in the hot loop).
 template <bool CANON, bool FULL = true>
@@ -355,9 +436,11 @@ __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t
 // the whole launch (one 64-lane workgroup = 64 envs, 97.5 KB of LDS), so the linked-list
 // walks and order-word read-modify-writes of the step are ds_* round trips (~100 cycles)
 // instead of L2/HBM round trips; only the used prefix is copied in and out.
-template <bool LDS, bool FULL>
+template <bool LDS, bool FULL, bool STAGED = false>
 __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0,
                                                      uint32_t step0, int mode, int autoreset, fjsp_out out) {
+    struct NoTile { int unused; };
+    __shared__ typename std::conditional<STAGED, StageTile, NoTile>::type s_tile;
     __shared__ uint32_t s_orders[LDS ? MAX_ORDERS * BLOCK : 1];
     __shared__ uint16_t s_code[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint8_t s_next[LDS ? MAX_SLOTS * BLOCK : 1];
@@ -396,7 +479,10 @@ __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, u
         int act[NA];
         synth_actions(seed, gid0 + (uint32_t)e, step0 + (uint32_t)k, mode, E, C, act);
         FJSP_STAMP(E, 0);
-        step_and_emit<true, FULL>(E, T, C, S, e, act, nullptr, autoreset, out, (uint32_t)k, s_mtbuf + lane);
+        if constexpr (STAGED)
+            step_and_emit_staged(E, T, C, S, e, act, autoreset, out, (uint32_t)k, s_mtbuf + lane, &s_tile, lane);
+        else
+            step_and_emit<true, FULL>(E, T, C, S, e, act, nullptr, autoreset, out, (uint32_t)k, s_mtbuf + lane);
     }
     if constexpr (LDS) {
         for (int o = 0; o < E.norders(); o++) S.orders[(size_t)o * S.n + e] = T.orders[o * BLOCK];
@@ -459,7 +545,8 @@ struct fjsp_handle {
     int timed;
     double* lut_dev;
     double lut_host[RLUT_SIZE];
-    int use_lds;   // fused kernel variant (FJSP_FUSED_LDS env var / fjsp_set_option)
+    int use_lds;     // fused kernel variant (FJSP_FUSED_LDS env var / fjsp_set_option)
+    int use_staged;  // LDS-staged wide output stores (FJSP_STAGED env var / fjsp_set_option)
 };
 
 static thread_local std::string g_err;
@@ -565,6 +652,8 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
         // global-table variant once resets stopped draining the store queue; opt-in only
         const char* v = getenv("FJSP_FUSED_LDS");
         h->use_lds = v ? atoi(v) : 0;
+        const char* st = getenv("FJSP_STAGED");
+        h->use_staged = st ? atoi(st) : 0;   // measured: no faster than direct stores (opt-in)
     }
     h->dcfg.step_size = c.step_size;
     h->dcfg.max_steps = c.max_episode_steps;
@@ -631,6 +720,7 @@ int fjsp_destroy(fjsp_handle* h) {
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
     if (!h || !name) return fail("null argument");
     if (!strcmp(name, "fused_lds")) { h->use_lds = value != 0; return 0; }
+    if (!strcmp(name, "staged_stores")) { h->use_staged = value != 0; return 0; }
     return fail("unknown option");
 }
 
@@ -704,10 +794,19 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
         hipLaunchKernelGGL(kern, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0, step0,
                            action_mode, autoreset, o);
     };
+    // staged stores need whole 64-env blocks and 16-byte aligned output rows
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
+    const bool staged = h->use_staged && !full && h->n % BLOCK == 0 && al16(o.obs_i32) && al16(o.obs_i8) &&
+                        al16(o.obs_f32) && al16(o.masks) && al16(o.rewards) && al16(o.term) && al16(o.trunc) &&
+                        al16(o.status);
     if (h->use_lds) {
-        if (full) launch(k_step_many<true, true>); else launch(k_step_many<true, false>);
+        if (full) launch(k_step_many<true, true>);
+        else if (staged) launch(k_step_many<true, false, true>);
+        else launch(k_step_many<true, false>);
     } else {
-        if (full) launch(k_step_many<false, true>); else launch(k_step_many<false, false>);
+        if (full) launch(k_step_many<false, true>);
+        else if (staged) launch(k_step_many<false, false, true>);
+        else launch(k_step_many<false, false>);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(h->ev1, h->stream));

@@ -9,6 +9,8 @@ nat = importlib.import_module("multi-agent-rl-for-fjsp_amd._native")
 L = nat.lib()
 L.fjsp_debug_stamps.argtypes = [ctypes.c_void_p]
 names = ["synth_actions", "action_phase", "run_phase", "rewards", "observe", "stores", "autoreset+next_obs", "-"]
+if "fine" in (sys.argv[1] if len(sys.argv) > 1 else ""):
+    names = ["synth_actions", "pickup", "agv", "machines", "packaging", "run_phase", "rewards+observe+stores", "autoreset"]
 for N in (4096,):
     for lds in (1, 0):
         env = ve.FJSPVecEnv(N)
@@ -21,6 +23,6 @@ for N in (4096,):
         env.rollout(200, step0=200, buffers=b); torch.cuda.synchronize()
         L.fjsp_debug_stamps(buf)
         waves, steps = N // 64, 200
-        tot = sum(buf[:7])
+        tot = sum(buf[:8])
         print(json.dumps({"N": N, "lds": lds, "cycles_per_wave_step": tot / waves / steps,
-                          "phases": {names[i]: round(buf[i] / waves / steps, 1) for i in range(7)}}))
+                          "phases": {names[i]: round(buf[i] / waves / steps, 1) for i in range(8)}}))
