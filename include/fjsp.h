@@ -18,6 +18,8 @@
  *                       (agents/ execute_action, SimPy run, RewardModel, get_observations)
  *   fjsp_step_many   <- K x FJSPSimulation.step with random actions (train.py:268 sample())
  *   fjsp_gae         <- MultiAgentTransitionMemory.finish_trajectory transition_memory.py:45-105
+ *   fjsp_pack_a2c    <- MultiAgentA2C._get_global_state / _flatten_obs  a2c.py:118-166
+ *   FJSP_ACTIONS_HEURISTIC <- MultiAgentA2C._get_heuristic_actions     a2c.py:390-537
  *   fjsp_read_env    <- FJSPSimulation.get_order_progress   FJSPSimulation.py:260-284
  *                       + agv.position / agv.carrying_tray / current_step (a2c.py:298-376)
  *
@@ -32,13 +34,14 @@
 extern "C" {
 #endif
 
-#define FJSP_ABI_VERSION 1
+#define FJSP_ABI_VERSION 2
 
 #define FJSP_NUM_AGENTS 8      /* pickup, agv, small, big, pkg_blue_1, pkg_blue_2, pkg_red, pkg_green */
 #define FJSP_OBS_I32 20        /* pickup 7 + agv 13 (position = 2) int32 observation fields */
 #define FJSP_OBS_I8 12         /* 6 stations x {is_busy, queue_length} int8 fields */
 #define FJSP_OBS_F32 6         /* 6 stations x processing_progress float32 */
 #define FJSP_MASKS 29          /* action masks: 3 + 8 + 6 x 3 int8 */
+#define FJSP_A2C_FEATS 38      /* a2c global state: per agent sorted keys w/o action_mask (a2c.py:118-166) */
 #define FJSP_MAX_ORDERS 64     /* num_orders limit per episode */
 #define FJSP_ACTION_ABSENT 255 /* agent missing from the action dict (no execute_action call) */
 
@@ -54,6 +57,7 @@ extern "C" {
 /* action_mode for fjsp_step_many */
 #define FJSP_ACTIONS_UNMASKED 0  /* uniform over the full action space (action_space.sample()) */
 #define FJSP_ACTIONS_MASKED   1  /* uniform over the valid actions of the current mask */
+#define FJSP_ACTIONS_HEURISTIC 2 /* MultiAgentA2C._get_heuristic_actions (a2c.py:390-537) */
 
 typedef struct fjsp_config {
     int32_t num_trays;          /* CONFIG['num_trays'] 1000; pool = min(num_trays, 1000) (FJSPSimulation.py:96) */
@@ -111,6 +115,12 @@ typedef struct fjsp_out {
     int8_t* next_i8;
     float* next_f32;
     int8_t* next_masks;
+    /* a2c global-state features of the observation after auto-reset (the one the policy acts
+     * on next): f32 [T][38][N], columns in _get_global_state order (a2c.py:153-166): agents in
+     * possible_agents order, each agent's keys sorted, action_mask dropped (_flatten_obs
+     * a2c.py:137-151).  Agent a's actor input = columns [off_a, off_a + dim_a) with
+     * off = 0,7,20,23,26,29,32,35. */
+    float* feats;
 } fjsp_out;
 
 /* Host view of one env (fjsp_read_env). */
@@ -197,6 +207,20 @@ int fjsp_gae_f64(const double* rewards, const double* values, const uint8_t* don
 int fjsp_read_env(fjsp_handle* h, int32_t env, fjsp_env_view* out);
 /* Wait for all work queued on the handle's stream. */
 int fjsp_sync(fjsp_handle* h);
+/* a2c features (f32 [38][N], see fjsp_out.feats) and action masks (int8 [29][N]) of every env's
+ * current observation; either pointer may be NULL.  Stream-ordered. */
+int fjsp_pack_a2c(fjsp_handle* h, float* feats, int8_t* masks);
+/* Source of each a2c feature column: out[38] = index into [obs_i32(20) | obs_i8(12) | obs_f32(6)]
+ * (host-only; lets callers and tests check the layout). */
+int fjsp_a2c_layout(int32_t* out);
+/* Env-state snapshot (every env's packed state, order table, tray-slot arena and MT19937
+ * stream): fjsp_snapshot copies fjsp_snapshot_bytes(h) bytes to `dst` (device or host
+ * memory), fjsp_restore loads a snapshot taken from a handle with the same num_envs.  Both
+ * are stream-ordered (hipMemcpyAsync; pinned host memory for overlap).  The role of
+ * FJSPSimulation's Python objects being copied / pickled by a caller. */
+int64_t fjsp_snapshot_bytes(const fjsp_handle* h);
+int fjsp_snapshot(fjsp_handle* h, void* dst);
+int fjsp_restore(fjsp_handle* h, const void* src);
 /* Kernel timing of the last fjsp_step_many / fjsp_step launch in ms (hipEvents on the
  * handle's stream; synchronises). */
 int fjsp_last_kernel_ms(fjsp_handle* h, float* ms);

@@ -42,7 +42,7 @@ class fjsp_reward_weights(ctypes.Structure):
 
 OUT_FIELDS = ["obs_i32", "obs_i8", "obs_f32", "masks", "rewards", "term", "trunc", "results",
               "orders_completed", "packaged", "sim_time", "status",
-              "next_i32", "next_i8", "next_f32", "next_masks"]
+              "next_i32", "next_i8", "next_f32", "next_masks", "feats"]
 
 
 class fjsp_out(ctypes.Structure):
@@ -61,7 +61,9 @@ EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_c
            "fjsp_default_reward_weights", "fjsp_set_reward_weights",
            "fjsp_create", "fjsp_destroy", "fjsp_set_stream", "fjsp_set_option", "fjsp_num_envs", "fjsp_state_bytes",
            "fjsp_reset", "fjsp_step", "fjsp_step_many", "fjsp_gae", "fjsp_gae_f64", "fjsp_mt_get", "fjsp_mt_set",
-           "fjsp_read_env", "fjsp_sync", "fjsp_last_kernel_ms"]
+           "fjsp_read_env", "fjsp_sync", "fjsp_last_kernel_ms", "fjsp_pack_a2c", "fjsp_a2c_layout",
+           "fjsp_snapshot_bytes", "fjsp_snapshot", "fjsp_restore"]
+ABI_VERSION = 2
 
 _lib = None
 
@@ -120,12 +122,17 @@ def lib():
         "fjsp_read_env": (I, [P, I, ctypes.POINTER(fjsp_env_view)]),
         "fjsp_sync": (I, [P]),
         "fjsp_last_kernel_ms": (I, [P, ctypes.POINTER(ctypes.c_float)]),
+        "fjsp_pack_a2c": (I, [P, P, P]),
+        "fjsp_a2c_layout": (I, [P]),
+        "fjsp_snapshot_bytes": (ctypes.c_int64, [P]),
+        "fjsp_snapshot": (I, [P, P]),
+        "fjsp_restore": (I, [P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.fjsp_abi_version() != 1:
+    if L.fjsp_abi_version() != ABI_VERSION:
         raise FjspNativeError("libfjsp.so ABI version mismatch")
     _lib = L
     return L

@@ -688,6 +688,67 @@ FJSP_DEV void observe(Env& E, const Cfg& C, Sink& o) {
     compute_masks(E, C, o);
 }
 
+// ---------------------------------------------------------------- heuristic policy
+// MultiAgentA2C._get_heuristic_actions (a2c.py:390-537) on the packed state.  The reference
+// compares the AGV position with (2,3) small, (0,3) big, (0,0) pickup, (3,5) packaging and
+// (1,5) for storage; (1,5) is no location (STORAGE is (3,0), constants.py:9), so the
+// "at storage" tests are constant false, exactly as in the reference.  The AGV is never
+// mid-move at a step boundary (is_moving branch).
+FJSP_DEV int machine_available(const Env& E, int m) {   // not busy and len(tray_queue) < 3
+    return !E.m_busy(m) && E.ll(m == 0 ? L_M0Q : L_M1Q) < 3;
+}
+FJSP_DEV void heuristic_actions(const Env& E, const Tables& T, int* act) {
+    const int has_orders = E.next_order() < E.norders() || E.cur_order() >= 0;
+    act[0] = has_orders ? 1 : 0;
+    const int loc = E.loc();
+    int a = 0;
+    if (E.carry() != NIL) {
+        if (E.carry_np()) {
+            const int ty = E.carry_type();
+            const int m = (ty == 1 || ty == 2) ? 0 : 1;   // SMALL / MEDIUM -> small machine
+            if (machine_available(E, m)) a = loc == (m == 0 ? LOC_SMALL : LOC_BIG) ? 7 : (m == 0 ? 2 : 3);
+            else a = 4;                                    // "at storage" is never true
+        } else if (E.carry_nk()) {
+            a = loc == LOC_PACK ? 7 : 5;
+        }
+    } else if (E.ll(L_M0R) > 0) {
+        a = loc == LOC_SMALL ? 6 : 2;
+    } else if (E.ll(L_M1R) > 0) {
+        a = loc == LOC_BIG ? 6 : 3;
+    } else if (E.ll(L_STORAGE) > 0) {
+        // for storage_tray in storage.trays: first tray needing processing whose machine is
+        // available -> MOVE_TO_STORAGE (PICKUP needs the impossible (1,5)); else check pickup
+        int found = 0;
+        int s = E.lh(L_STORAGE);
+        for (int i = E.ll(L_STORAGE); i > 0 && !found; i--) {
+            const int c = T.scode[s * T.stride];
+            const uint32_t w = T.orders[tc_order(c) * T.stride], rg = tc_range(c);
+            if ((w & rg) != rg) {
+                const int ty = ow_type(w);
+                found = machine_available(E, (ty == 1 || ty == 2) ? 0 : 1);
+            }
+            s = T.snext[s * T.stride];
+        }
+        a = found ? 4 : (E.ll(L_PREADY) > 0 ? (loc == LOC_PICKUP ? 6 : 1) : 0);
+    } else if (E.ll(L_PREADY) > 0) {
+        a = loc == LOC_PICKUP ? 6 : 1;
+    } else if (E.m_busy(0) || E.m_cur(0) != NIL) {
+        a = loc == LOC_SMALL ? 0 : 2;
+    } else if (E.m_busy(1) || E.m_cur(1) != NIL) {
+        a = loc == LOC_BIG ? 0 : 3;
+    } else if (has_orders) {
+        a = loc == LOC_PICKUP ? 0 : 1;
+    }
+    act[1] = a;
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+        const int idle = !E.m_busy(m);
+        act[2 + m] = (E.ll(m == 0 ? L_M0Q : L_M1Q) > 0 && idle) ? 1 : (E.m_cur(m) != NIL && idle) ? 2 : 0;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; s++) act[4 + s] = (E.p_queued(s) > 0 && !E.p_busy(s)) ? 1 : 0;
+}
+
 // ---------------------------------------------------------------- reset
 // Fresh episode state (FJSPSimulation.reset: new agents, storage, tray pool); the MT cursor
 // (W3) is kept.

@@ -220,13 +220,31 @@ template <class V>
 __device__ __forceinline__ void st32(V* base, uint32_t elem, V v) {
     *reinterpret_cast<V*>(reinterpret_cast<char*>(base) + elem * (uint32_t)sizeof(V)) = v;
 }
+// a2c feature column of each observation field (a2c.py:137-166: agents in order, keys sorted,
+// action_mask dropped); checked against spec.a2c_feature_index by fjsp_a2c_layout's test.
+constexpr int NFEAT = 38;
+constexpr int8_t FEAT_OF_I32[NI32] = {5, 6, 4, 3, 2, 0, 1, 11, 12, 9, 18, 19, 17, 16, 10, 13, 7, 14, 8, 15};
+constexpr int8_t FEAT_OF_I8[NI8] = {20, 22, 23, 25, 26, 28, 29, 31, 32, 34, 35, 37};
+constexpr int8_t FEAT_OF_F32[NF32] = {21, 24, 27, 30, 33, 36};
+
 // Sink that stores each observation field as soon as it is computed (fjsp_env.h observe()).
 struct StoreSink {
     int32_t* pi32; int8_t* pi8; float* pf32; int8_t* pmk;
     uint32_t t, n, e;
-    __device__ __forceinline__ void i32(int f, int v) { if (pi32) st32(pi32, (t * NI32 + (uint32_t)f) * n + e, (int32_t)v); }
-    __device__ __forceinline__ void i8(int f, int v) { if (pi8) st32(pi8, (t * NI8 + (uint32_t)f) * n + e, (int8_t)v); }
-    __device__ __forceinline__ void f32(int f, float v) { if (pf32) st32(pf32, (t * NF32 + (uint32_t)f) * n + e, v); }
+    float* pfeat = nullptr;   // optional a2c features [T][38][N]
+    __device__ __forceinline__ void feat(int c, float v) { if (pfeat) st32(pfeat, (t * NFEAT + (uint32_t)c) * n + e, v); }
+    __device__ __forceinline__ void i32(int f, int v) {
+        if (pi32) st32(pi32, (t * NI32 + (uint32_t)f) * n + e, (int32_t)v);
+        feat(FEAT_OF_I32[f], (float)v);
+    }
+    __device__ __forceinline__ void i8(int f, int v) {
+        if (pi8) st32(pi8, (t * NI8 + (uint32_t)f) * n + e, (int8_t)v);
+        feat(FEAT_OF_I8[f], (float)(int8_t)v);
+    }
+    __device__ __forceinline__ void f32(int f, float v) {
+        if (pf32) st32(pf32, (t * NF32 + (uint32_t)f) * n + e, v);
+        feat(FEAT_OF_F32[f], v);
+    }
     __device__ __forceinline__ void mask(int f, int v) { if (pmk) st32(pmk, (t * NMASK + (uint32_t)f) * n + e, (int8_t)v); }
 };
 
@@ -250,10 +268,20 @@ __global__ void __launch_bounds__(BLOCK) k_reset(DevState S, Cfg C, const uint32
     if (seeds) { mt_seed(S.mt, S.n, e, seeds[e]); mti = 0; }
     E.set_mti(mti);
     env_reset(E, T, C, S, e, num_orders, s_mtbuf + threadIdx.x);
-    StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, 0u, (uint32_t)S.n, (uint32_t)e};
+    StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, 0u, (uint32_t)S.n, (uint32_t)e, out.feats};
     observe(E, C, sink);
     env_store(E, S.words, S.n, e);
     if (out.status) out.status[e] = E.status();
+}
+
+// fjsp_pack_a2c: features + masks of the current observation (no state change)
+__global__ void __launch_bounds__(BLOCK) k_pack(DevState S, Cfg C, float* __restrict__ feats, int8_t* __restrict__ masks) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= S.n) return;
+    Env E;
+    env_load(E, S.words, S.n, e);
+    StoreSink sink{nullptr, nullptr, nullptr, masks, 0u, (uint32_t)S.n, (uint32_t)e, feats};
+    observe(E, C, sink);
 }
 
 // fmix64 counter RNG for synthetic actions (oracle_actions spec)
@@ -265,7 +293,11 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t z) {
 }
 
 __device__ __forceinline__ void synth_actions(uint64_t seed, uint32_t gid, uint32_t step, int mode, const Env& E,
-                                              const Cfg& C, int* act) {
+                                              const Tables& T, const Cfg& C, int* act) {
+    if (mode == FJSP_ACTIONS_HEURISTIC) {
+        heuristic_actions(E, T, act);
+        return;
+    }
     const uint64_t h = fmix64(seed ^ fmix64(((uint64_t)gid << 32) | step));
     const int nact[NA] = {3, 8, 3, 3, 3, 3, 3, 3};
     if (mode == FJSP_ACTIONS_UNMASKED) {
@@ -402,8 +434,8 @@ __device__ __forceinline__ void step_and_emit(Env& E, const Tables& T, const Cfg
     E.set_step(E.step() + 1);
     if (autoreset && (all_done || truncated))
         E = env_reset_cold(E, T, C, S, e, nord, mtbuf);   // reset(seed=None) continues the MT stream
-    if (FULL && (out.next_i32 || out.next_i8 || out.next_f32 || out.next_masks)) {
-        StoreSink nsink{out.next_i32, out.next_i8, out.next_f32, out.next_masks, t, n, ue};
+    if (FULL && (out.next_i32 || out.next_i8 || out.next_f32 || out.next_masks || out.feats)) {
+        StoreSink nsink{out.next_i32, out.next_i8, out.next_f32, out.next_masks, t, n, ue, out.feats};
         observe(E, C, nsink);
     }
     FJSP_STAMP(E, 6);
@@ -477,7 +509,7 @@ __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, u
 #endif
     for (int k = 0; k < K; k++) {
         int act[NA];
-        synth_actions(seed, gid0 + (uint32_t)e, step0 + (uint32_t)k, mode, E, C, act);
+        synth_actions(seed, gid0 + (uint32_t)e, step0 + (uint32_t)k, mode, E, T, C, act);
         FJSP_STAMP(E, 0);
         if constexpr (STAGED)
             step_and_emit_staged(E, T, C, S, e, act, autoreset, out, (uint32_t)k, s_mtbuf + lane, &s_tile, lane);
@@ -780,16 +812,20 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
                    int32_t action_mode, int32_t autoreset, const fjsp_out* traj) {
     if (!h) return fail("null handle");
     if (K < 0) return fail("K must be >= 0");
-    if (action_mode != FJSP_ACTIONS_UNMASKED && action_mode != FJSP_ACTIONS_MASKED) return fail("bad action_mode");
+    if (action_mode != FJSP_ACTIONS_UNMASKED && action_mode != FJSP_ACTIONS_MASKED && action_mode != FJSP_ACTIONS_HEURISTIC)
+        return fail("bad action_mode");
     if (!h->has_reset) return fail("fjsp_step_many before fjsp_reset");
     if (K == 0) return 0;
-    if ((uint64_t)K * (uint64_t)h->n * 64ull >= (1ull << 32)) return fail("K * num_envs too large for one launch (< 2^26)");
+    const fjsp_out o = traj ? *traj : kNoOut;
+    // outputs are addressed with 32-bit byte offsets: the largest per-step block is the a2c
+    // features (38 x 4 B per env) or the rewards (8 x 8 B)
+    const uint64_t row_bytes = o.feats ? 4ull * NFEAT : 64ull;
+    if ((uint64_t)K * (uint64_t)h->n * row_bytes >= (1ull << 32)) return fail("K * num_envs too large for one launch");
     DeviceGuard g(h->device);
     dim3 grid((h->n + BLOCK - 1) / BLOCK);
     HIPCHK(hipEventRecord(h->ev0, h->stream));
-    const fjsp_out o = traj ? *traj : kNoOut;
     const bool full = o.results || o.orders_completed || o.packaged || o.sim_time || o.next_i32 || o.next_i8 ||
-                      o.next_f32 || o.next_masks;
+                      o.next_f32 || o.next_masks || o.feats;
     auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0, step0,
                            action_mode, autoreset, o);
@@ -846,6 +882,44 @@ extern "C" int fjsp_debug_stamps(unsigned long long* out) {
     return 0;
 }
 #endif
+
+int fjsp_pack_a2c(fjsp_handle* h, float* feats, int8_t* masks) {
+    if (!h) return fail("null handle");
+    if (!h->has_reset) return fail("fjsp_pack_a2c before fjsp_reset");
+    if (!feats && !masks) return 0;
+    DeviceGuard g(h->device);
+    Cfg C = h->dcfg;
+    C.lut = h->lut_dev;
+    k_pack<<<(h->n + BLOCK - 1) / BLOCK, BLOCK, 0, h->stream>>>(h->S, C, feats, masks);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int fjsp_a2c_layout(int32_t* out) {
+    if (!out) return fail("null argument");
+    for (int f = 0; f < NI32; f++) out[FEAT_OF_I32[f]] = f;
+    for (int f = 0; f < NI8; f++) out[FEAT_OF_I8[f]] = NI32 + f;
+    for (int f = 0; f < NF32; f++) out[FEAT_OF_F32[f]] = NI32 + NI8 + f;
+    return 0;
+}
+
+int64_t fjsp_snapshot_bytes(const fjsp_handle* h) { return h ? (int64_t)h->bytes : -1; }
+
+int fjsp_snapshot(fjsp_handle* h, void* dst) {
+    if (!h || !dst) return fail("null argument");
+    if (!h->has_reset) return fail("fjsp_snapshot before fjsp_reset");
+    DeviceGuard g(h->device);
+    HIPCHK(hipMemcpyAsync(dst, h->base, h->bytes, hipMemcpyDefault, h->stream));
+    return 0;
+}
+
+int fjsp_restore(fjsp_handle* h, const void* src) {
+    if (!h || !src) return fail("null argument");
+    DeviceGuard g(h->device);
+    HIPCHK(hipMemcpyAsync(h->base, src, h->bytes, hipMemcpyDefault, h->stream));
+    h->has_reset = 1;
+    return 0;
+}
 
 int fjsp_sync(fjsp_handle* h) {
     if (!h) return fail("null handle");

@@ -11,7 +11,8 @@ import torch
 from . import _native as nat
 from .spec import AGENTS
 
-NI32, NI8, NF32, NMASK, NA = 20, 12, 6, 29, 8
+NI32, NI8, NF32, NMASK, NA, NFEAT = 20, 12, 6, 29, 8, 38
+POLICIES = {"random": 0, "unmasked": 0, "masked": 1, "heuristic": 2}   # FJSP_ACTIONS_*
 
 
 def _ptr(t):
@@ -21,8 +22,20 @@ def _ptr(t):
 class Buffers:
     """Output tensors for T steps of N envs (T = 1 for step/reset)."""
 
-    def __init__(self, T, N, device, infos=True, next_obs=False):
+    def __init__(self, T, N, device, infos=True, next_obs=False, feats=False, obs=True):
         z = lambda *s, dt: torch.zeros(*s, dtype=dt, device=device)  # noqa: E731
+        # feats: a2c global-state features f32 [T, 38, N] of the post-auto-reset observation
+        self.feats = z(T, NFEAT, N, dt=torch.float32) if feats else None
+        if not obs:   # a2c-only outputs: features, post-reset masks, rewards, term, trunc
+            self.obs_i32 = self.obs_i8 = self.obs_f32 = self.masks = None
+            self.results = self.orders_completed = self.packaged = self.sim_time = None
+            self.next_i32 = self.next_i8 = self.next_f32 = None
+            self.next_masks = z(T, NMASK, N, dt=torch.int8)
+            self.rewards = z(T, NA, N, dt=torch.float64)
+            self.term = z(T, N, dt=torch.uint8)
+            self.trunc = z(T, N, dt=torch.uint8)
+            self.status = z(T, N, dt=torch.int32)
+            return
         self.obs_i32 = z(T, NI32, N, dt=torch.int32)
         self.obs_i8 = z(T, NI8, N, dt=torch.int8)
         self.obs_f32 = z(T, NF32, N, dt=torch.float32)
@@ -147,14 +160,48 @@ class FJSPVecEnv:
         nat.check(nat.lib().fjsp_step(self._h, _ptr(a), order, int(bool(autoreset)), ctypes.byref(out)))
         return buffers
 
-    def rollout(self, K, action_seed=0, step0=0, masked=False, autoreset=True, buffers=None, infos=False):
-        """K fused steps with on-device synthetic actions; returns [K, F, N] trajectories."""
+    def rollout(self, K, action_seed=0, step0=0, masked=False, autoreset=True, buffers=None, infos=False,
+                policy=None):
+        """K fused steps with on-device actions; returns [K, F, N] trajectories.
+
+        policy: "random" (uniform, action_space.sample()), "masked" (uniform over valid
+        actions) or "heuristic" (MultiAgentA2C._get_heuristic_actions, a2c.py:390-537)."""
         self._sync_stream()
+        mode = POLICIES[policy] if policy is not None else (1 if masked else 0)
         b = buffers or Buffers(K, self.num_envs, self.device, infos=infos)
         out = b.struct()
         nat.check(nat.lib().fjsp_step_many(self._h, int(K), int(action_seed) & (2**64 - 1), self.env_id_base,
-                                           int(step0), 1 if masked else 0, int(bool(autoreset)), ctypes.byref(out)))
+                                           int(step0), mode, int(bool(autoreset)), ctypes.byref(out)))
         return b
+
+    def pack_a2c(self, feats=None, masks=None):
+        """a2c features f32 [38, N] and masks int8 [29, N] of the current observations
+        (MultiAgentA2C._get_global_state, a2c.py:153-166)."""
+        self._sync_stream()
+        if feats is None:
+            feats = torch.empty(NFEAT, self.num_envs, dtype=torch.float32, device=self.device)
+        if masks is None:
+            masks = torch.empty(NMASK, self.num_envs, dtype=torch.int8, device=self.device)
+        nat.check(nat.lib().fjsp_pack_a2c(self._h, _ptr(feats), _ptr(masks)))
+        return feats, masks
+
+    def snapshot(self, out=None):
+        """Copy of every env's complete state (uint8 tensor; device unless `out` is given)."""
+        self._sync_stream()
+        nb = int(nat.lib().fjsp_snapshot_bytes(self._h))
+        if out is None:
+            out = torch.empty(nb, dtype=torch.uint8, device=self.device)
+        if out.numel() * out.element_size() != nb:
+            raise ValueError(f"snapshot needs {nb} bytes")
+        nat.check(nat.lib().fjsp_snapshot(self._h, _ptr(out)))
+        return out
+
+    def restore(self, snap):
+        self._sync_stream()
+        nb = int(nat.lib().fjsp_snapshot_bytes(self._h))
+        if snap.numel() * snap.element_size() != nb:
+            raise ValueError(f"snapshot of {snap.numel() * snap.element_size()} bytes, handle needs {nb}")
+        nat.check(nat.lib().fjsp_restore(self._h, _ptr(snap.contiguous())))
 
     def last_kernel_ms(self):
         ms = ctypes.c_float()

@@ -943,9 +943,67 @@ void oracle_actions(uint64_t seed, uint32_t env_gid, uint32_t step, const int8_t
     }
 }
 
+/* MultiAgentA2C._get_heuristic_actions (a2c.py:390-537), statement by statement.  Tuples
+ * the heuristic compares the AGV position with: small (2,3), big (0,3), pickup (0,0),
+ * packaging (3,5) and "storage" (1,5) -- the latter is not STORAGE's position (3,0,
+ * constants.py:9), so that comparison is always false in the reference and here. */
+static int at(const sim_t* s, int r, int c) { return s->pos_r == r && s->pos_c == c; }
+static int machine_available(const sim_t* s, int m) { return !s->m[m].busy && s->m[m].queue.len < 3; }
+void oracle_heuristic(void* h, uint8_t* out) {
+    const sim_t* s = (const sim_t*)h;
+    out[0] = (s->order_queue.len > 0 || s->cur_order >= 0) ? 1 : 0;
+    int a = 0;
+    if (s->is_moving) {
+        a = 0;
+    } else if (s->carrying >= 0) {
+        const int t = s->carrying;
+        if (tray_needs_processing(s, t)) {
+            const int ty = tray_type(s, t);                      /* 1 SMALL, 2 MEDIUM, 3 BIG */
+            const int m = (ty == 1 || ty == 2) ? 0 : 1;
+            const int tr = m == 0 ? 2 : 0, move = m == 0 ? 2 : 3;
+            if (machine_available(s, m)) a = at(s, tr, 3) ? 7 : move;
+            else a = at(s, 1, 5) ? 7 : 4;
+        } else if (tray_needs_packaging(s, t)) {
+            a = at(s, 3, 5) ? 7 : 5;
+        } else {
+            a = 0;
+        }
+    } else if (s->m[0].ready.len > 0) {
+        a = at(s, 2, 3) ? 6 : 2;
+    } else if (s->m[1].ready.len > 0) {
+        a = at(s, 0, 3) ? 6 : 3;
+    } else if (s->storage.len > 0) {
+        int found = 0;
+        for (int i = 0; i < s->storage.len && !found; i++) {
+            const int t = q_get((fifo*)&s->storage, i);
+            if (!tray_needs_processing(s, t)) continue;
+            const int ty = tray_type(s, t);
+            const int m = (ty == 1 || ty == 2) ? 0 : 1;
+            if (machine_available(s, m)) { a = at(s, 1, 5) ? 6 : 4; found = 1; }
+        }
+        if (!found) a = s->ps_ready.len > 0 ? (at(s, 0, 0) ? 6 : 1) : 0;   /* for ... else */
+    } else if (s->ps_ready.len > 0) {
+        a = at(s, 0, 0) ? 6 : 1;
+    } else if (s->m[0].busy || s->m[0].cur_tray >= 0) {
+        a = at(s, 2, 3) ? 0 : 2;
+    } else if (s->m[1].busy || s->m[1].cur_tray >= 0) {
+        a = at(s, 0, 3) ? 0 : 3;
+    } else if (s->order_queue.len > 0 || s->cur_order >= 0) {
+        a = at(s, 0, 0) ? 0 : 1;
+    }
+    out[1] = (uint8_t)a;
+    for (int m = 0; m < 2; m++) {
+        if (s->m[m].queue.len > 0 && !s->m[m].busy) out[2 + m] = 1;
+        else if (s->m[m].cur_tray >= 0 && !s->m[m].busy) out[2 + m] = 2;
+        else out[2 + m] = 0;
+    }
+    for (int st = 0; st < 4; st++) out[4 + st] = (s->p[st].queue.len > 0 && !s->p[st].busy) ? 1 : 0;
+}
+
 /* Rollout of n_envs independent envs (the CPU baseline and the bulk parity driver).
  * Env e: global id gid0+e, seeded seeds[e], `steps` steps, actions from the counter RNG
- * (policy 0 unmasked, 1 masked) or from `actions_in` [steps][n_envs][8] (policy 2);
+ * (policy 0 unmasked, 1 masked), from `actions_in` [steps][n_envs][8] (policy 2) or from
+ * oracle_heuristic (policy 3);
  * auto-reset with seed=None on term|trunc.  If `rec_out` is non-NULL it receives
  * [steps][n_envs] records (post-step obs); reset obs go to `reset_out` if non-NULL. */
 int oracle_rollout(const int32_t* cfg, int n_envs, uint32_t gid0, const uint32_t* seeds,
@@ -961,6 +1019,7 @@ int oracle_rollout(const int32_t* cfg, int n_envs, uint32_t gid0, const uint32_t
         for (int t = 0; t < steps; t++) {
             uint8_t act[8];
             if (policy == 2) memcpy(act, actions_in + ((size_t)t * n_envs + e) * 8, 8);
+            else if (policy == 3) oracle_heuristic(s, act);
             else oracle_actions(action_seed, gid0 + (uint32_t)e, (uint32_t)t, policy == 1 ? cur.masks : NULL, act);
             oracle_step(s, act, NULL, &rec);
             ck = ck * 0x100000001B3ull + (uint64_t)(rec.rewards[0] * 8.0) + (uint64_t)rec.obs_i32[14];

@@ -79,6 +79,7 @@ def lib():
         L.oracle_reset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Rec)]
         L.oracle_step.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Rec)]
         L.oracle_orders.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
+        L.oracle_heuristic.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_actions.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                      ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_rollout.argtypes = [ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.c_uint32,
@@ -131,6 +132,12 @@ class OracleEnv:
         lib().oracle_step(self._h, a, o, ctypes.byref(r))
         return rec_to_np(r)
 
+    def heuristic(self):
+        """MultiAgentA2C._get_heuristic_actions (a2c.py:390-537) on the current state."""
+        out = np.zeros(8, np.uint8)
+        lib().oracle_heuristic(self._h, out.ctypes.data)
+        return out
+
     def orders(self, max_orders=128):
         buf = (ctypes.c_uint32 * max_orders)()
         n = lib().oracle_orders(self._h, buf, max_orders)
@@ -148,7 +155,8 @@ def actions(seed, env_gid, step, masks=None):
 
 def rollout(n_envs, steps, seeds=None, gid0=0, num_orders=30, action_seed=0, policy=0,
             actions_in=None, record=True, record_resets=False, **cfg):
-    """Run n_envs envs x steps with auto-reset; returns (records [steps, n_envs], resets, checksum)."""
+    """Run n_envs envs x steps with auto-reset; returns (records [steps, n_envs], resets, checksum).
+    policy: 0 unmasked random, 1 masked random, 3 heuristic (a2c.py:390-537); actions_in -> 2."""
     seeds = np.arange(gid0, gid0 + n_envs, dtype=np.uint32) if seeds is None else np.asarray(seeds, np.uint32)
     rec = np.zeros((steps, n_envs), REC_DTYPE) if record else None
     rst = np.zeros((steps, n_envs), REC_DTYPE) if record_resets else None

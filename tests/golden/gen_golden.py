@@ -17,6 +17,9 @@ Outputs (all small, committed):
                       256 envs x 1000 unmasked-random steps (env i seeded i).
   scenarios.npz     — scripted traces with non-default configs (storage capacity 2, tray
                       capacity 3) and hand-written action scripts hitting the edge paths.
+  heur_probe.npz    — mixed heuristic / masked-random rollouts recording, at every step, the
+                      heuristic's proposal (a2c.py:390-537) and a2c's flattened global state
+                      (a2c.py:118-166) for the pre-step observation.
   gae.npz           — returns/advantages from transition_memory.MultiAgentTransitionMemory
                       (transition_memory.py:45-105) on recorded reward streams.
 
@@ -359,6 +362,39 @@ def gen_scenarios(W, a2c_mod):
     np.savez_compressed(os.path.join(HERE, "scenarios.npz"), **out)
 
 
+def gen_heur_probe(W, a2c_mod, steps=400, seeds=range(6)):
+    """States reached by a mix of heuristic and masked-random actions (the heuristic alone
+    never drops at storage: it compares the AGV position with (1, 5), constants.py:9 puts
+    STORAGE at (3, 0)), with the heuristic's proposal and a2c's global state at each step."""
+    out = {}
+    agent = a2c_mod.MultiAgentA2C.__new__(a2c_mod.MultiAgentA2C)
+    env0 = W.FJSPParallelEnv()
+    agent.possible_agents = list(env0.possible_agents)
+    agent.obs_dims = {a: agent._get_obs_dim(env0.observation_space(a)) for a in AGENTS}
+    for seed in seeds:
+        env = W.FJSPParallelEnv()
+        np.random.seed(seed)
+        with contextlib.redirect_stdout(io.StringIO()):
+            obs, _ = env.reset(seed=seed, options={"num_orders": 30})
+        acts, heur, gs = [], [], []
+        for t in range(steps):
+            hd = agent._get_heuristic_actions(env.unwrapped.simulation)
+            h = [int(hd[a]) for a in AGENTS]
+            gs.append(agent._get_global_state(obs, list(env.agents)).astype(np.float32))
+            use_h = (fmix64(seed * 7919 + t) >> 11) % 3 != 0
+            act = h if use_h else action_rng(seed + 100, seed, t, masks_of(obs))
+            with contextlib.redirect_stdout(io.StringIO()):
+                obs, rew, term, trunc, info = env.step({a: int(act[i]) for i, a in enumerate(AGENTS)})
+                if term[AGENTS[0]] or trunc[AGENTS[0]]:
+                    obs, _ = env.reset(options={"num_orders": 30})
+            acts.append(np.array(act, np.uint8))
+            heur.append(np.array(h, np.uint8))
+        out[f"s{seed}_actions"] = np.stack(acts)
+        out[f"s{seed}_heur"] = np.stack(heur)
+        out[f"s{seed}_gstate"] = np.stack(gs)
+    np.savez_compressed(os.path.join(HERE, "heur_probe.npz"), **out)
+
+
 def gen_gae(tm_mod):
     rng = np.random.default_rng(1234)
     cases = {}
@@ -410,6 +446,8 @@ def main():
         gen_reset_tables(W)
     if want("gae"):
         gen_gae(tm_mod)
+    if want("heur_probe"):
+        gen_heur_probe(W, a2c_mod)
     if want("scenarios"):
         gen_scenarios(W, a2c_mod)
     if want("traces"):

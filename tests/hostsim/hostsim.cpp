@@ -102,4 +102,13 @@ void hs_step(void* p, const uint8_t* actions, int autoreset, int32_t* i32, int8_
         obs_out(h, e, ri32, ri8, rf32, rmk);
     }
 }
+// heuristic proposals (a2c.py:390-537) for every env: out [n][8]
+void hs_heuristic(void* p, uint8_t* out) {
+    HS* h = (HS*)p;
+    for (int e = 0; e < h->n; e++) {
+        int act[8];
+        heuristic_actions(h->E[e], tabs(h, e), act);
+        for (int a = 0; a < 8; a++) out[8 * e + a] = (uint8_t)act[a];
+    }
+}
 }

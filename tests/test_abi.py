@@ -20,7 +20,7 @@ def test_library_exports_every_symbol():
     L = G.native.lib()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.fjsp_abi_version() == 1
+    assert L.fjsp_abi_version() == G.native.ABI_VERSION == 2
 
 
 def test_config_validation_without_gpu():
@@ -40,3 +40,12 @@ def test_kernels_compiled_for_gfx950():
     data = open(G.native.LIB_PATH, "rb").read()
     assert b"gfx950" in data
     assert b"k_step_many" in data or b"_Z" in data
+
+
+def test_a2c_layout_matches_spec():
+    """fjsp_out.feats column order == spec.a2c_feature_index (pinned against the reference's
+    _get_global_state by test_oracle_golden.py::test_oracle_heuristic_and_global_state)."""
+    out = (ctypes.c_int32 * 38)()
+    assert G.native.lib().fjsp_a2c_layout(out) == 0
+    spec = __import__("importlib").import_module("multi-agent-rl-for-fjsp_amd.spec")
+    assert list(out) == spec.a2c_feature_index()

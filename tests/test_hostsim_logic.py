@@ -30,6 +30,7 @@ def L():
     lib.hs_destroy.argtypes = [Pt]
     lib.hs_reset.argtypes = [Pt, Pt, ctypes.c_int, Pt, Pt, Pt, Pt]
     lib.hs_step.argtypes = [Pt, Pt, ctypes.c_int] + [Pt] * 13
+    lib.hs_heuristic.argtypes = [Pt, Pt]
     return lib
 
 
@@ -46,6 +47,11 @@ class HS:
 
     def __del__(self):
         self.L.hs_destroy(self.h)
+
+    def heuristic(self):
+        out = np.zeros((self.n, 8), np.uint8)
+        self.L.hs_heuristic(self.h, out.ctypes.data)
+        return out
 
     def reset(self, seeds, num_orders):
         s = np.ascontiguousarray(seeds, np.uint32)
@@ -101,3 +107,32 @@ def test_closed_form_vs_golden(L, tr):
                            ("rewards", hs.rew), ("results", hs.res)):
             assert P.bits_equal(mine[0], getattr(tr, name)[t]), (tr.name, t, name)
         assert P.bits_equal(hs.ri32[0], tr.reset_i32[t]), (tr.name, t)
+
+
+def test_heuristic_vs_golden_probe(L):
+    """heuristic_actions (the kernel's FJSP_ACTIONS_HEURISTIC) == a2c._get_heuristic_actions on
+    every pre-step state of the reference's mixed heuristic/random rollouts."""
+    d = np.load(f"{P.GOLDEN}/heur_probe.npz")
+    for seed in range(6):
+        acts, heur = d[f"s{seed}_actions"], d[f"s{seed}_heur"]
+        hs = HS(L, 1, {})
+        hs.reset([seed], 30)
+        for t in range(len(acts)):
+            assert hs.heuristic()[0].tolist() == heur[t].tolist(), (seed, t)
+            hs.step(acts[t:t + 1])
+
+
+def test_heuristic_vs_oracle_rollout(L):
+    """Closed-loop heuristic rollouts (policy 3): kernel logic and oracle agree step by step."""
+    n, steps, norders = 32, 600, 4
+    hs = HS(L, n, {})
+    seeds = np.arange(n, dtype=np.uint32) + 7
+    hs.reset(seeds, norders)
+    rec, _, _ = O.rollout(n, steps, seeds=seeds, num_orders=norders, policy=3)
+    done = 0
+    for t in range(steps):
+        hs.step(hs.heuristic())
+        for name, mine in (("obs_i32", hs.i32), ("masks", hs.mk), ("rewards", hs.rew), ("term", hs.term)):
+            assert mine.tobytes() == np.ascontiguousarray(rec[t][name]).tobytes(), (t, name)
+        done += int(hs.term.sum())
+    assert done > 0   # the heuristic finishes small episodes

@@ -92,3 +92,39 @@ def test_action_rng_matches_generator():
             masks[off] = 1
         ml = [masks[0:3], masks[3:11]] + [masks[11 + 3 * i: 14 + 3 * i] for i in range(6)]
         assert O.actions(seed, gid, step, masks).tolist() == action_rng(seed, gid, step, ml)
+
+
+def _heur_probe():
+    d = np.load(f"{P.GOLDEN}/heur_probe.npz")
+    return [(s, d[f"s{s}_actions"], d[f"s{s}_heur"], d[f"s{s}_gstate"]) for s in range(6)]
+
+
+@pytest.mark.parametrize("case", _heur_probe(), ids=lambda c: f"s{c[0]}")
+def test_oracle_heuristic_and_global_state(case):
+    """oracle_heuristic == a2c._get_heuristic_actions and the a2c feature layout (spec.py)
+    == a2c._get_global_state on every pre-step state of a mixed heuristic/random rollout."""
+    import importlib
+    spec = importlib.import_module("multi-agent-rl-for-fjsp_amd.spec")   # host-only module
+    seed, acts, heur, gstate = case
+    idx = spec.a2c_feature_index()
+    env = O.OracleEnv()
+    r = env.reset(seed=seed, num_orders=30)
+    for t in range(len(acts)):
+        assert env.heuristic().tolist() == heur[t].tolist(), (seed, t)
+        flat = np.concatenate([r["obs_i32"], r["obs_i8"], r["obs_f32"]]).astype(np.float32)
+        assert P.bits_equal(flat[idx], gstate[t]), (seed, t)
+        r = env.step(acts[t])
+        if r["term"] or r["trunc"]:
+            r = env.reset(num_orders=30)
+
+
+@pytest.mark.parametrize("tr", [t for t in P.load_traces() if "heuristic" in t.name] +
+                         [t for t in P.load_scenarios() if "heur" in t.name], ids=lambda t: t.name)
+def test_oracle_heuristic_drives_golden_traces(tr):
+    env = O.OracleEnv(**tr.cfg)
+    env.reset(seed=tr.seed, num_orders=tr.num_orders)
+    for t in range(tr.steps):
+        assert env.heuristic().tolist() == tr.actions[t].tolist(), (tr.name, t)
+        r = env.step(tr.actions[t])
+        if r["term"] or r["trunc"]:
+            env.reset(num_orders=tr.num_orders)
