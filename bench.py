@@ -38,8 +38,8 @@ HBM_PEAK_GBS = 8000.0                     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=None, help="default 2000 (step) / 4 A2C batches (a2c)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 200 (step) / 1 A2C batch (a2c)")
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--chunk", type=int, default=200, help="env steps per fused launch")
     ap.add_argument("--num-orders", type=int, default=30)
@@ -47,7 +47,17 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-step-mode", action="store_true", help="skip the one-launch-per-step measurement")
-    return ap.parse_args()
+    ap.add_argument("--workload", choices=["step", "a2c"], default="step",
+                    help="step: env-step throughput (the headline metric); a2c: the batched A2C "
+                         "training loop (BASELINE configs 4/5; one bench step = one A2C batch)")
+    ap.add_argument("--batch-size", type=int, default=256, help="A2C batch (vector steps per update)")
+    ap.add_argument("--no-a2c", action="store_true", help="skip the A2C training-loop leg of the step workload")
+    a = ap.parse_args()
+    if a.steps is None:
+        a.steps = 2000 if a.workload == "step" else 4
+    if a.warmup is None:
+        a.warmup = 200 if a.workload == "step" else 1
+    return a
 
 
 def cpu_baseline(args, workers):
@@ -94,6 +104,53 @@ def load_pmc(workload):
         return None
 
 
+def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=None, group=None):
+    """Batched A2C training loop (a2c_vec.VecMultiAgentA2C): env-steps/s over whole batches
+    (collect batch_size vector steps with the policy + GAE + one update)."""
+    A = importlib.import_module("multi-agent-rl-for-fjsp_amd.a2c_vec")
+    learner = A.VecMultiAgentA2C(env, batch_size=batch_size, seed=0, group=group)
+    base = env.env_id_base
+    learner.reset(seeds=torch.arange(base, base + N), num_orders=num_orders)
+
+    def batch():
+        learner.collect()
+        ret, adv = learner.advantages()
+        learner.update(ret, adv)
+        learner.roll_over()
+    for _ in range(warmup):
+        batch()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    tc = 0.0
+    for _ in range(batches):
+        c0 = time.perf_counter()
+        learner.collect()
+        torch.cuda.synchronize()
+        tc += time.perf_counter() - c0
+        ret, adv = learner.advantages()
+        learner.update(ret, adv)
+        learner.roll_over()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed, tc], device=env.device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, tc = float(t[0]), float(t[1])
+    steps = batches * batch_size * N * world
+    return {"value": steps / elapsed, "unit": "env-steps/s", "n_gpus": world, "batches": batches,
+            "batch_size": batch_size, "envs_per_gpu": N, "ms_per_batch": elapsed * 1e3 / batches,
+            "collect_ms_per_batch": tc * 1e3 / batches,
+            "update_ms_per_batch": (elapsed - tc) * 1e3 / batches,
+            "critic_loss_last": learner.critic_loss_history[-1],
+            "note": "predict (stacked-actor batched GEMMs + masked sampling) -> fjsp_step writing a2c "
+                    "features in HBM -> fp64 GAE kernel -> full-batch update (8 actors + critic, Adam); "
+                    "reference a2c.py loop: ~130 env-steps/s on one CPU core (SURVEY.md)"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,6 +170,24 @@ def main():
     N = args.envs
     base = rank * N
     env = vec_env.FJSPVecEnv(N, device=dev, env_id_base=base)
+    if args.workload == "a2c":
+        res = a2c_throughput(env, N, world, args.steps, args.warmup, args.batch_size, 25, dist,
+                             dist.group.WORLD if dist else None)
+        if rank == 0:
+            out = {"metric": "env-steps/sec of the A2C training loop (BASELINE configs 4/5)",
+                   "value": res["value"], "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+                   "warmup": args.warmup, "ms_per_step": res["ms_per_batch"], "higher_is_better": True,
+                   "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (networks) + int32/f64 (env)",
+                   "data": "synthetic: envs seeded by global id, random-init networks (torch.manual_seed(0))",
+                   "config": {"workload": f"a2c_{N}envs", "envs_per_gpu": N, "global_envs": N * world,
+                              "batch_size": args.batch_size, "num_orders": 25,
+                              "parallelism": f"env-shard x{world}, one flat gradient all_reduce per batch"},
+                   "a2c": res}
+            print(json.dumps(out), flush=True)
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     env.reset(seeds=torch.arange(base, base + N), num_orders=args.num_orders)
     chunk = max(1, min(args.chunk, args.steps))
     buf = vec_env.Buffers(chunk, N, dev, infos=False)
@@ -185,6 +260,15 @@ def main():
                     "achieved_GBs": ALGO_BYTES_STEP * N / (kms * 1e-3) / 1e9,
                     "note": "one launch per step, actions u8[8][N] resident in HBM (rank 0)"}
 
+    a2c = None
+    if world == 1 and not args.no_a2c:
+        try:
+            aenv = vec_env.FJSPVecEnv(N, device=dev)
+            a2c = a2c_throughput(aenv, N, 1, 2, 1, args.batch_size, 25)
+            del aenv
+        except Exception as e:   # the headline metric does not depend on this leg
+            a2c = {"error": f"{type(e).__name__}: {e}"}
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         try:
@@ -224,6 +308,7 @@ def main():
                          "env_steps_per_launch": N * steps_per_launch},
             "cpu_baseline": cpu,
             "per_step_launch": per_step,
+            "a2c_training": a2c,
             "state_bytes_per_env": env.state_bytes_per_env(),
         }
         print(json.dumps(out), flush=True)

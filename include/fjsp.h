@@ -156,7 +156,9 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
 /* Tuning knobs: "fused_lds" (0/1, default 0: stage the per-env tables of k_step_many in LDS,
  * one 64-env workgroup per CU); "staged_stores" (0/1, default 0: k_step_many stages each
  * step's obs / masks / rewards / term / trunc / status in LDS and writes them as 16-byte
- * chunks; used when only those outputs are requested, N % 64 == 0 and rows are aligned). */
+ * chunks; used when only those outputs are requested, N % 64 == 0 and rows are aligned);
+ * "timing" (0/1, default 1: bracket fjsp_step / fjsp_step_many launches with hipEvents for
+ * fjsp_last_kernel_ms; set 0 while capturing the calls into a hipGraph). */
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value);
 int fjsp_num_envs(const fjsp_handle* h);
 /* Bytes of device state per env (HBM footprint of the SoA state). */

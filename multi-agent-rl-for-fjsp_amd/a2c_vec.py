@@ -1,0 +1,495 @@
+"""Batched multi-agent A2C over N device-resident environments.
+
+Reference: MultiAgentA2C (a2c.py:15-731) with networks.py.  Same networks (one actor per agent,
+a centralised critic on the 38-dim global state), same predict rules (mask, renormalise,
+uniform fallback, a2c.py:197-229), same memory / GAE (transition_memory.py:83-105), same
+update (entropy bonus, per-agent advantage normalisation, gradient clipping, Adam,
+a2c.py:647-731) and the same checkpoint format (a2c.py:733-775) — restated for N envs:
+
+  * observations never leave HBM: the step kernel writes the a2c features f32 [38, N] and the
+    post-reset masks int8 [29, N] of the next observation (fjsp_out.feats / next_masks), the
+    policy reads them in place;
+  * the 8 actors are one stacked module (weights [8, ...], inputs padded to 13 features and
+    outputs to 8 actions): every layer is ONE batched GEMM (torch.baddbmm -> hipBLASLt) for
+    all agents and envs instead of 8 x N GEMVs;
+  * one update per `batch_size` vector steps uses all batch_size x N transitions; the loss
+    means / advantage statistics are over that whole batch (for N = 1 this is exactly the
+    reference's update);
+  * multi-GPU (config 5): every rank steps its own env shard, computes local sums and one
+    bucketed all_reduce (RCCL) of the gradients makes the update identical to a single learner
+    over all ranks' transitions (distributed.py).
+
+Padding is exact: padded input columns are zero and their weights receive zero gradient;
+padded action logits are -inf before the softmax.
+"""
+import ctypes
+import math
+
+import torch
+from torch import nn
+
+from . import _native as nat
+from .spec import AGENTS, N_ACTIONS
+
+NA = 8
+OBS_DIMS = [7, 13, 3, 3, 3, 3, 3, 3]          # _get_obs_dim per agent (a2c.py:118-134)
+OBS_OFFS = [0, 7, 20, 23, 26, 29, 32, 35]      # agent blocks of the 38-dim global state
+MASK_OFFS = [0, 3, 11, 14, 17, 20, 23, 26]     # agent blocks of the 29 mask bytes
+GLOBAL_DIM = 38
+DPAD, APAD = 13, 8
+
+
+# ---------------------------------------------------------------- reference-shaped networks
+class ActorNet(nn.Module):
+    """networks.ActorNetwork layout (state_dict keys net.0/2/4.*)."""
+
+    def __init__(self, d, a, hidden=256):
+        super().__init__()
+        self.net = nn.Sequential(nn.Linear(d, hidden), nn.ReLU(), nn.Linear(hidden, hidden), nn.ReLU(),
+                                 nn.Linear(hidden, a), nn.Softmax(dim=-1))
+
+    def forward(self, x):
+        return self.net(x)
+
+
+class CriticNet(nn.Module):
+    """networks.CentralizedCriticNetwork layout (state_dict keys net.0/2/4/6.*)."""
+
+    def __init__(self, d, hidden=256):
+        super().__init__()
+        self.net = nn.Sequential(nn.Linear(d, hidden), nn.ReLU(), nn.Linear(hidden, hidden), nn.ReLU(),
+                                 nn.Linear(hidden, hidden // 2), nn.ReLU(), nn.Linear(hidden // 2, 1))
+
+    def forward(self, x):
+        return self.net(x)
+
+
+class ActorStack(nn.Module):
+    """The 8 ActorNetworks as stacked, padded weights; forward is 3 batched GEMMs.
+
+    Layout "agent-major, batch last": x [8, 13, B] -> logits [8, 8, B]; the batch dimension is
+    the GEMM's N dimension so the kernel-written [38, N] features feed it without a transpose.
+    """
+
+    def __init__(self, hidden=256):
+        super().__init__()
+        self.hidden = hidden
+        self.W1 = nn.Parameter(torch.zeros(NA, hidden, DPAD))
+        self.b1 = nn.Parameter(torch.zeros(NA, hidden, 1))
+        self.W2 = nn.Parameter(torch.zeros(NA, hidden, hidden))
+        self.b2 = nn.Parameter(torch.zeros(NA, hidden, 1))
+        self.W3 = nn.Parameter(torch.zeros(NA, APAD, hidden))
+        self.b3 = nn.Parameter(torch.zeros(NA, APAD, 1))
+        pad = torch.full((NA, APAD, 1), float("-inf"))
+        for a, n in enumerate(N_ACTIONS):
+            pad[a, :n] = 0.0
+        self.register_buffer("logit_pad", pad)
+
+    def logits(self, x):
+        h = torch.relu(torch.baddbmm(self.b1, self.W1, x))
+        h = torch.relu(torch.baddbmm(self.b2, self.W2, h))
+        return torch.baddbmm(self.b3, self.W3, h) + self.logit_pad
+
+    def forward(self, x):
+        return torch.softmax(self.logits(x), dim=1)
+
+    @torch.no_grad()
+    def load_actor_nets(self, nets):
+        for a, net in enumerate(nets):
+            l1, l2, l3 = net.net[0], net.net[2], net.net[4]
+            d, n = OBS_DIMS[a], N_ACTIONS[a]
+            self.W1[a].zero_(); self.W1[a, :, :d].copy_(l1.weight)
+            self.b1[a, :, 0].copy_(l1.bias)
+            self.W2[a].copy_(l2.weight); self.b2[a, :, 0].copy_(l2.bias)
+            self.W3[a].zero_(); self.W3[a, :n].copy_(l3.weight)
+            self.b3[a].zero_(); self.b3[a, :n, 0].copy_(l3.bias)
+
+    @torch.no_grad()
+    def actor_state_dict(self, a):
+        d, n = OBS_DIMS[a], N_ACTIONS[a]
+        c = lambda t: t.detach().cpu().clone()  # noqa: E731
+        return {"net.0.weight": c(self.W1[a, :, :d]), "net.0.bias": c(self.b1[a, :, 0]),
+                "net.2.weight": c(self.W2[a]), "net.2.bias": c(self.b2[a, :, 0]),
+                "net.4.weight": c(self.W3[a, :n]), "net.4.bias": c(self.b3[a, :n, 0])}
+
+
+def gather_index(device):
+    """[8, 13] row indices into [features(38) | zero row] building the padded actor inputs."""
+    idx = torch.full((NA, DPAD), GLOBAL_DIM, dtype=torch.long)
+    for a in range(NA):
+        idx[a, :OBS_DIMS[a]] = torch.arange(OBS_OFFS[a], OBS_OFFS[a] + OBS_DIMS[a])
+    return idx.to(device)
+
+
+def mask_index(device):
+    """[8, 8] indices into [masks(29) | zero row] -> per-agent padded masks."""
+    idx = torch.full((NA, APAD), 29, dtype=torch.long)
+    for a in range(NA):
+        idx[a, :N_ACTIONS[a]] = torch.arange(MASK_OFFS[a], MASK_OFFS[a] + N_ACTIONS[a])
+    return idx.to(device)
+
+
+# ---------------------------------------------------------------- policy math (any device)
+def actor_inputs(feats, gidx):
+    """feats f32 [..., 38, B] -> padded actor inputs [8, 13, (...)*B]."""
+    lead = feats.shape[:-2]
+    B = feats.shape[-1]
+    z = torch.zeros(*lead, 1, B, dtype=feats.dtype, device=feats.device)
+    x = torch.cat([feats, z], dim=-2)[..., gidx, :]                 # [..., 8, 13, B]
+    if lead:
+        x = x.reshape(-1, NA, DPAD, B).permute(1, 2, 0, 3).reshape(NA, DPAD, -1)
+    return x
+
+
+def agent_masks(masks, midx):
+    """int8 masks [..., 29, B] -> float [8, 8, (...)*B] (padded actions are 0)."""
+    lead = masks.shape[:-2]
+    B = masks.shape[-1]
+    z = torch.zeros(*lead, 1, B, dtype=torch.float32, device=masks.device)
+    m = torch.cat([masks.to(torch.float32), z], dim=-2)[..., midx, :]
+    if lead:
+        m = m.reshape(-1, NA, APAD, B).permute(1, 2, 0, 3).reshape(NA, APAD, -1)
+    return m
+
+
+def masked_probs(probs, mask):
+    """a2c.py:204-220: zero invalid actions, renormalise; if nothing is left, uniform over
+    the valid actions."""
+    p = probs * mask
+    s = p.sum(dim=1, keepdim=True)
+    uni = mask / mask.sum(dim=1, keepdim=True)
+    return torch.where(s > 0, p / torch.where(s > 0, s, torch.ones_like(s)), uni)
+
+
+def categorical_log_prob(p, actions):
+    """Categorical(probs=p).log_prob(actions) batched, written out (no argument validation,
+    which would synchronise): probs / sum -> log(clamp(eps, 1 - eps)) -> gather.
+    p [8, 8, B], actions long [8, B] -> [8, B]."""
+    q = p / p.sum(dim=1, keepdim=True)
+    eps = torch.finfo(q.dtype).eps
+    return torch.log(q.clamp(min=eps, max=1 - eps)).gather(1, actions.unsqueeze(1)).squeeze(1)
+
+
+def sample_categorical(p, u=None):
+    """One draw per (agent, env) from p [8, 8, B] by inverse CDF: action = #{k : cdf_k < x}
+    with x = (1 - U) * cdf_last, U ~ [0, 1) -> x in (0, total]; a zero-probability action can
+    never be returned (its CDF step is empty), padded actions neither."""
+    if u is None:
+        u = torch.rand(p.shape[0], 1, p.shape[2], device=p.device, dtype=p.dtype)
+    cdf = torch.cumsum(p, dim=1)
+    x = (1.0 - u) * cdf[:, -1:, :]
+    return (cdf < x).sum(dim=1)
+
+
+def entropy_of(probs):
+    """_calculate_entropy (a2c.py:705-722): -(p * log(p + 1e-10)).sum() per observation."""
+    return -(probs * torch.log(probs + 1e-10)).sum(dim=1)         # [8, B]
+
+
+class A2CLosses:
+    """Loss sums for one (possibly sharded) batch; `count` = the GLOBAL sample count.
+
+    actor_loss_a = -(mean(adv_n * logp)) - c * mean(entropy) where adv_n uses the global
+    mean / unbiased std of agent a's advantages (calc_actor_loss, a2c.py:724-731); critic =
+    mean over (agent, sample) of (V - R)^2 (calc_critic_loss, a2c.py:713-722).  With shards,
+    every rank passes the global statistics and count, so summing the per-rank gradients
+    (all_reduce) gives the single-learner gradient."""
+
+    @staticmethod
+    def compute(actors, critic, feats, masks, actions, returns, adv, gidx, midx, entropy_coef,
+                adv_mean, adv_std, count):
+        x = actor_inputs(feats, gidx)                                # [8, 13, S]
+        probs = actors(x)                                            # [8, 8, S]
+        ent = entropy_of(probs)                                      # [8, S]
+        pm = masked_probs(probs, agent_masks(masks, midx))
+        logp = categorical_log_prob(pm, actions)                     # [8, S]
+        adv_n = (adv - adv_mean[:, None]) / (adv_std[:, None] + 1e-8) if count > 1 else adv
+        actor_losses = -(adv_n * logp).sum(dim=1) / count - entropy_coef * ent.sum(dim=1) / count
+        S = feats.shape[0] * feats.shape[-1] if feats.dim() == 3 else feats.shape[-1]
+        g = feats.permute(0, 2, 1).reshape(S, GLOBAL_DIM) if feats.dim() == 3 else feats.t()
+        v = critic(g).reshape(-1)                                    # [S]
+        critic_loss = ((v[None, :] - returns) ** 2).sum() / (NA * count)
+        return actor_losses, critic_loss
+
+
+def clip_per_agent_(actors, max_norm):
+    """torch.nn.utils.clip_grad_norm_ applied to each agent's actor separately (a2c.py:675-679)."""
+    grads = [p.grad for p in actors.parameters() if p.grad is not None]
+    sq = torch.zeros(NA, dtype=torch.float32, device=grads[0].device)
+    for g in grads:
+        sq += g.reshape(NA, -1).pow(2).sum(dim=1)
+    norm = sq.sqrt()
+    coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+    for g in grads:
+        g.mul_(coef.view(NA, *([1] * (g.dim() - 1))))
+    return norm
+
+
+def init_networks(seed=None, hidden=256, device="cpu"):
+    """Actor stack + critic initialised exactly like MultiAgentA2C.__init__ (a2c.py:87-103):
+    the 8 ActorNetworks in possible_agents order, then the critic, from torch's CPU generator
+    (torch.manual_seed(seed) first when seed is given), then moved to `device`."""
+    if seed is not None:
+        torch.manual_seed(seed)
+    nets = [ActorNet(OBS_DIMS[a], N_ACTIONS[a], hidden) for a in range(NA)]
+    critic = CriticNet(GLOBAL_DIM, hidden)
+    actors = ActorStack(hidden)
+    actors.load_actor_nets(nets)
+    return actors.to(device), critic.to(device)
+
+
+def update_step(actors, critic, optim_actor, optim_critic, feats, masks, actions, ret, adv, gidx, midx,
+                entropy_coef, max_grad_norm, group=None):
+    """One _update (a2c.py:647-703) on a [T, ., N] batch (this rank's shard of it).
+
+    feats f32 [T, 38, N], masks int8 [T, 29, N], actions u8 [T, 8, N], ret / adv f64 [T, 8, N].
+    Returns (actor losses per agent, critic loss) as Python floats (the loss histories)."""
+    from . import distributed as D
+    T, _, N = feats.shape
+    S = T * N
+    adv32 = adv.float().permute(1, 0, 2).reshape(NA, S)             # calc_actor_loss: FloatTensor(adv)
+    ret32 = ret.float().permute(1, 0, 2).reshape(NA, S)
+    acts = actions.long().permute(1, 0, 2).reshape(NA, S)
+    count, mean, std = D.adv_stats(adv32, group)
+    optim_actor.zero_grad(set_to_none=True)
+    optim_critic.zero_grad(set_to_none=True)
+    actor_losses, critic_loss = A2CLosses.compute(actors, critic, feats, masks, acts, ret32, adv32, gidx, midx,
+                                                  entropy_coef, mean, std, count)
+    (actor_losses.sum() + critic_loss).backward()
+    D.allreduce_grads(list(actors.parameters()) + list(critic.parameters()), group)
+    clip_per_agent_(actors, max_grad_norm)
+    torch.nn.utils.clip_grad_norm_(critic.parameters(), max_grad_norm)
+    optim_actor.step()
+    optim_critic.step()
+    al = D.allreduce_sum(actor_losses.detach(), group)
+    cl = D.allreduce_sum(critic_loss.detach().view(1), group)
+    return al.cpu().tolist(), float(cl.cpu()[0])
+
+
+class VecMultiAgentA2C:
+    """MultiAgentA2C for an FJSPVecEnv (N envs on this GPU; optionally one shard of a
+    multi-GPU job through `group`).
+
+    Hyper-parameters and their defaults follow train.py:57-98 (batch 256, gamma 0.99,
+    lambda 0.95, lr 3e-4 / 1e-3, entropy 0.01, clip 0.5)."""
+
+    def __init__(self, env, batch_size=256, gamma=0.99, lamb=0.95, lr_actor=3e-4, lr_critic=1e-3,
+                 use_gae=True, entropy_coef=0.01, max_grad_norm=0.5, hidden=256, seed=None, group=None,
+                 use_graph=True):
+        self.env = env
+        self.device = env.device
+        self.N = env.num_envs
+        self.batch_size = int(batch_size)
+        self.gamma, self.lamb = float(gamma), float(lamb)
+        self.use_gae = use_gae
+        self.entropy_coef = float(entropy_coef)
+        self.max_grad_norm = float(max_grad_norm)
+        self.group = group
+        self.possible_agents = list(AGENTS)
+        self.obs_dims = dict(zip(AGENTS, OBS_DIMS))
+        self.act_dims = dict(zip(AGENTS, N_ACTIONS))
+        self.global_obs_dim = GLOBAL_DIM
+        self.actors, self.critic = init_networks(seed, hidden, self.device)
+        self.optim_actor = torch.optim.Adam(self.actors.parameters(), lr=lr_actor)
+        self.optim_critic = torch.optim.Adam(self.critic.parameters(), lr=lr_critic)
+        self.gidx = gather_index(self.device)
+        self.midx = mask_index(self.device)
+        self.actor_loss_history = {a: [] for a in AGENTS}
+        self.critic_loss_history = []
+        self.episode_end_timesteps = []
+        self._bufs = None
+        self.use_graph = bool(use_graph) and self.device.type == "cuda"
+        self._graph = None
+        self._graph_det = None
+        self._eager_batches = 0
+
+    # ------------------------------------------------------------ rollout storage
+    def _alloc(self):
+        T, N, dev = self.batch_size, self.N, self.device
+        z = lambda *s, dt: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
+        b = {
+            "feats": z(T + 1, GLOBAL_DIM, N, dt=torch.float32),
+            "masks": z(T + 1, 29, N, dt=torch.int8),
+            "actions": z(T, NA, N, dt=torch.uint8),
+            "values": z(T + 1, N, dt=torch.float32),
+            "rewards": z(T, NA, N, dt=torch.float64),
+            "term": z(T, N, dt=torch.uint8),
+            "trunc": z(T, N, dt=torch.uint8),
+            "status": z(T, N, dt=torch.int32),
+        }
+        outs = []
+        for t in range(T):
+            o = nat.fjsp_out()
+            o.rewards = b["rewards"][t].data_ptr()
+            o.term = b["term"][t].data_ptr()
+            o.trunc = b["trunc"][t].data_ptr()
+            o.status = b["status"][t].data_ptr()
+            o.next_masks = b["masks"][t + 1].data_ptr()
+            o.feats = b["feats"][t + 1].data_ptr()
+            outs.append(o)
+        b["outs"] = outs
+        self._bufs = b
+
+    def reset(self, seeds=None, num_orders=25):
+        """env.reset + the first observation's features (a2c.py:269)."""
+        if self._bufs is None:
+            self._alloc()
+        b = self._bufs
+        o = nat.fjsp_out()
+        o.masks = b["masks"][0].data_ptr()
+        o.feats = b["feats"][0].data_ptr()
+        self.env._sync_stream()
+        s = None
+        if seeds is not None:
+            s = torch.as_tensor(seeds, device=self.device).to(torch.int64).bitwise_and(0xFFFFFFFF).to(torch.int32)
+        nat.check(nat.lib().fjsp_reset(self.env.handle, None if s is None else ctypes.c_void_p(s.data_ptr()),
+                                       None, int(num_orders), ctypes.byref(o)))
+        self.num_orders = int(num_orders)
+
+    # ------------------------------------------------------------ predict
+    @torch.no_grad()
+    def policy(self, feats, masks, deterministic=False):
+        """predict (a2c.py:168-252) for all agents and envs: actions long [8, B], the masked
+        probabilities [8, 8, B] and the critic's value [B]."""
+        pm = masked_probs(self.actors(actor_inputs(feats, self.gidx)), agent_masks(masks, self.midx))
+        act = torch.argmax(pm, dim=1) if deterministic else sample_categorical(pm)
+        v = self.critic(feats.t()).view(-1)
+        return act, pm, v
+
+    def predict(self, feats, masks, deterministic=False, train_returns=False):
+        """Actions u8 [8, B] (+ log-probs [8, B] and values [B] with train_returns)."""
+        act, pm, v = self.policy(feats, masks, deterministic)
+        if train_returns:
+            return act.to(torch.uint8), categorical_log_prob(pm, act), v
+        return act.to(torch.uint8)
+
+    # ------------------------------------------------------------ one batch
+    def collect(self, deterministic=False, action_fn=None):
+        """batch_size vector steps: predict -> fjsp_step (features + masks of the next
+        observation written in place) -> memory.  action_fn(t, masks) may override actions
+        (tests).  After one eager batch the whole batch (batch_size x (policy + step) plus the
+        bootstrap value, ~40 launches per step) is captured once into a hipGraph and replayed:
+        the buffers and parameters are static, Adam updates the weights in place."""
+        if action_fn is None and self.use_graph:
+            if self._graph is not None and self._graph_det == deterministic:
+                self._graph.replay()
+                return
+            if self._eager_batches >= 1:
+                self._capture(deterministic)
+                self._graph.replay()
+                return
+        self._collect_eager(deterministic, action_fn)
+        self._eager_batches += 1
+
+    def _capture(self, deterministic):
+        L = nat.lib()
+        h = self.env.handle
+        nat.check(L.fjsp_set_option(h, b"timing", 0))   # no hipEventRecord inside the capture
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g):
+                self._collect_eager(deterministic, None)
+        finally:
+            self.env._sync_stream()
+            nat.check(L.fjsp_set_option(h, b"timing", 1))
+        self._graph, self._graph_det = g, deterministic
+
+    def _collect_eager(self, deterministic, action_fn):
+        b = self._bufs
+        L = nat.lib()
+        h = self.env.handle
+        self.env._sync_stream()
+        for t in range(self.batch_size):
+            act, _, v = self.policy(b["feats"][t], b["masks"][t], deterministic)
+            if action_fn is not None:
+                act = action_fn(t, b["masks"][t]).to(self.device).long()
+            b["actions"][t].copy_(act)
+            b["values"][t].copy_(v)
+            nat.check(L.fjsp_step(h, ctypes.c_void_p(b["actions"][t].data_ptr()), None, 1,
+                                  ctypes.byref(b["outs"][t])))
+        with torch.no_grad():
+            b["values"][self.batch_size].copy_(self.critic(b["feats"][self.batch_size].t()).view(-1))
+
+    def advantages(self):
+        """finish_trajectory over the batch (transition_memory.py:45-105) with the fp64 GAE
+        kernel: an episode end bootstraps 0 (a2c.py:357), the batch end V(s_T) (a2c.py:321-332)."""
+        from .vec_env import gae
+        b = self._bufs
+        T, N = self.batch_size, self.N
+        done = (b["term"] | b["trunc"]).contiguous()
+        vals = b["values"][:T, None, :].expand(T, NA, N).contiguous()
+        boot = b["values"][T].double()[None, :].expand(NA, N).contiguous()
+        ret, adv = gae(b["rewards"].view(T, NA * N), vals.view(T, NA * N), done, boot.view(NA * N),
+                       self.gamma, self.lamb)
+        ret, adv = ret.view(T, NA, N), adv.view(T, NA, N)
+        if not self.use_gae:
+            adv = ret - vals.double()
+        return ret, adv
+
+    def update(self, ret, adv):
+        """_update (a2c.py:647-703) over the batch's T x N transitions."""
+        b = self._bufs
+        T = self.batch_size
+        al, cl = update_step(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
+                             b["masks"][:T], b["actions"], ret, adv, self.gidx, self.midx, self.entropy_coef,
+                             self.max_grad_norm, self.group)
+        for a, x in zip(AGENTS, al):
+            self.actor_loss_history[a].append(x)
+        self.critic_loss_history.append(cl)
+        return al, cl
+
+    def roll_over(self):
+        """The last observation of the batch becomes the first of the next."""
+        b = self._bufs
+        b["feats"][0].copy_(b["feats"][self.batch_size])
+        b["masks"][0].copy_(b["masks"][self.batch_size])
+
+    def learn(self, total_timesteps, num_orders=25, seeds=None, deterministic=False, action_fn=None):
+        """learn (a2c.py:254-388) on N envs: total_timesteps counts env-steps of this shard
+        (N per vector step); an update every batch_size vector steps."""
+        self.reset(seeds=seeds, num_orders=num_orders)
+        steps = 0
+        while steps < total_timesteps:
+            self.collect(deterministic, action_fn)
+            ret, adv = self.advantages()
+            self.update(ret, adv)
+            self.roll_over()
+            steps += self.batch_size * self.N
+        return self
+
+    # ------------------------------------------------------------ checkpoints (a2c.py:733-775)
+    def state_dicts(self):
+        return {
+            "actor_nets": {a: self.actors.actor_state_dict(i) for i, a in enumerate(AGENTS)},
+            "critic_net": {k: v.detach().cpu().clone() for k, v in self.critic.state_dict().items()},
+            "obs_dims": dict(self.obs_dims),
+            "act_dims": dict(self.act_dims),
+            "global_obs_dim": GLOBAL_DIM,
+            "possible_agents": list(AGENTS),
+        }
+
+    def save_model(self, path):
+        import os
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        torch.save(self.state_dicts(), path)
+
+    def load_model(self, path):
+        """Loads a reference checkpoint (or one written by save_model) without executing
+        anything from the file (weights_only=True)."""
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        self.load_state_dicts(ck)
+
+    def load_state_dicts(self, ck):
+        nets = []
+        for i, a in enumerate(AGENTS):
+            net = ActorNet(OBS_DIMS[i], N_ACTIONS[i], self.actors.hidden)
+            net.load_state_dict(ck["actor_nets"][a])
+            nets.append(net)
+        self.actors.load_actor_nets([n.to(self.device) for n in nets])
+        self.critic.load_state_dict(ck["critic_net"])
+
+
+def num_params(model):
+    return sum(math.prod(p.shape) for p in model.parameters())

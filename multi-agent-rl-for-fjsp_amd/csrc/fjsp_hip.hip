@@ -579,6 +579,7 @@ struct fjsp_handle {
     double lut_host[RLUT_SIZE];
     int use_lds;     // fused kernel variant (FJSP_FUSED_LDS env var / fjsp_set_option)
     int use_staged;  // LDS-staged wide output stores (FJSP_STAGED env var / fjsp_set_option)
+    int timing;      // hipEvent bracketing of step launches (off while graph-capturing)
 };
 
 static thread_local std::string g_err;
@@ -686,6 +687,7 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
         h->use_lds = v ? atoi(v) : 0;
         const char* st = getenv("FJSP_STAGED");
         h->use_staged = st ? atoi(st) : 0;   // measured: no faster than direct stores (opt-in)
+        h->timing = 1;
     }
     h->dcfg.step_size = c.step_size;
     h->dcfg.max_steps = c.max_episode_steps;
@@ -753,6 +755,7 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
     if (!h || !name) return fail("null argument");
     if (!strcmp(name, "fused_lds")) { h->use_lds = value != 0; return 0; }
     if (!strcmp(name, "staged_stores")) { h->use_staged = value != 0; return 0; }
+    if (!strcmp(name, "timing")) { h->timing = value != 0; if (!h->timing) h->timed = 0; return 0; }
     return fail("unknown option");
 }
 
@@ -795,7 +798,7 @@ int fjsp_step(fjsp_handle* h, const uint8_t* actions, const uint8_t* agent_order
     }
     DeviceGuard g(h->device);
     dim3 grid((h->n + BLOCK - 1) / BLOCK);
-    HIPCHK(hipEventRecord(h->ev0, h->stream));
+    if (h->timing) HIPCHK(hipEventRecord(h->ev0, h->stream));
     if (canon)
         hipLaunchKernelGGL(k_step<true>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, packed, autoreset,
                            out ? *out : kNoOut);
@@ -803,8 +806,10 @@ int fjsp_step(fjsp_handle* h, const uint8_t* actions, const uint8_t* agent_order
         hipLaunchKernelGGL(k_step<false>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, packed, autoreset,
                            out ? *out : kNoOut);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(h->ev1, h->stream));
-    h->timed = 1;
+    if (h->timing) {
+        HIPCHK(hipEventRecord(h->ev1, h->stream));
+        h->timed = 1;
+    }
     return 0;
 }
 
@@ -823,7 +828,7 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
     if ((uint64_t)K * (uint64_t)h->n * row_bytes >= (1ull << 32)) return fail("K * num_envs too large for one launch");
     DeviceGuard g(h->device);
     dim3 grid((h->n + BLOCK - 1) / BLOCK);
-    HIPCHK(hipEventRecord(h->ev0, h->stream));
+    if (h->timing) HIPCHK(hipEventRecord(h->ev0, h->stream));
     const bool full = o.results || o.orders_completed || o.packaged || o.sim_time || o.next_i32 || o.next_i8 ||
                       o.next_f32 || o.next_masks || o.feats;
     auto launch = [&](auto kern) {
@@ -845,8 +850,10 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
         else launch(k_step_many<false, false>);
     }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(h->ev1, h->stream));
-    h->timed = 1;
+    if (h->timing) {
+        HIPCHK(hipEventRecord(h->ev1, h->stream));
+        h->timed = 1;
+    }
     return 0;
 }
 
