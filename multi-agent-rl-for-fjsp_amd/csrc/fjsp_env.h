@@ -291,6 +291,41 @@ FJSP_DEV int list_pop(Env& E, const Tables& T) {
     E.set_list(L, n == 0 ? NIL : next, n == 0 ? NIL : E.lt(L), n);
     return s;
 }
+// Lists selected at run time (CAND = bitmask of the lists the index can name): the list word
+// is picked / written back with a select chain over the candidate registers, so lanes that
+// pop or push different lists share ONE memory round trip instead of one branch each.
+template <uint32_t CAND>
+FJSP_DEV uint32_t lword(const Env& E, int l) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < NLIST; i++)
+        if ((CAND >> i) & 1u) v = (l == i) ? E.w[7 + i] : v;
+    return v;
+}
+template <uint32_t CAND>
+FJSP_DEV void set_lword(Env& E, int l, uint32_t v) {
+#pragma unroll
+    for (int i = 0; i < NLIST; i++)
+        if ((CAND >> i) & 1u) E.w[7 + i] = (l == i) ? v : E.w[7 + i];
+}
+template <uint32_t CAND>
+FJSP_DEV void list_push_dyn(Env& E, const Tables& T, int l, int s) {
+    const uint32_t lw = lword<CAND>(E, l);
+    const uint32_t n = lw >> 16;
+    T.snext[s * T.stride] = (uint8_t)NIL;
+    if (n != 0) T.snext[((lw >> 8) & 0xFFu) * T.stride] = (uint8_t)s;
+    set_lword<CAND>(E, l, (n == 0 ? (uint32_t)s : (lw & 0xFFu)) | ((uint32_t)s << 8) | ((n + 1) << 16));
+}
+template <uint32_t CAND>
+FJSP_DEV int list_pop_dyn(Env& E, const Tables& T, int l) {   // list must be non-empty
+    const uint32_t lw = lword<CAND>(E, l);
+    const int s = (int)(lw & 0xFFu);
+    const uint32_t n = (lw >> 16) - 1u;
+    const uint32_t next = T.snext[s * T.stride];
+    set_lword<CAND>(E, l, n == 0 ? ((uint32_t)NIL | ((uint32_t)NIL << 8)) : (next | (lw & 0xFF00u) | (n << 16)));
+    return s;
+}
+
 // new tray slot holding `code` (bump allocator, reset per episode)
 FJSP_DEV int slot_new(Env& E, const Tables& T, int code) {
     const int s = E.slot_next();
@@ -303,96 +338,85 @@ FJSP_DEV int slot_new(Env& E, const Tables& T, int code) {
 // ---- reward / result bit layout (oracle/fjsp_oracle.c, RESULT_KEYS in gen_golden.py)
 constexpr uint32_t R_EXEC = 0x80u;
 
-// PickupStationAgent.execute_action (PickupStationAgent.py:190-276)
+// PickupStationAgent.execute_action (PickupStationAgent.py:190-276).  Every path that hands a
+// tray to ready_trays (order finished, tray full, SIGNAL, the unreachable order mismatch) sets
+// `push`; the one push at the end keeps its stores in a single code path.
 FJSP_DEV uint32_t pickup_execute(Env& E, const Tables& T, const Cfg& C, int action) {
     uint32_t r = R_EXEC;   // 1 success, 2 product_loaded, 4 tray_completed, 8 idle_with_orders
-    auto push_tray = [&]() {
-        const int s = slot_new(E, T, tc_make(E.tray_order(), E.tray_start(), E.tray_count()));
-        if (s >= 0) list_push<L_PREADY>(E, T, s);
-        E.set_tray_valid(0);
-    };
     if (action == 0) {
-        if (E.next_order() < E.norders() || E.cur_order() >= 0) r |= 8u;
-        r |= 1u;
+        const int has_orders = E.next_order() < E.norders() || E.cur_order() >= 0;
+        return r | 1u | (has_orders ? 8u : 0u);
+    }
+    bool push = false;
+    if (action == 2) {
+        push = E.tray_valid() && E.tray_count() > 0;
+        r |= push ? 1u : 0u;
     } else if (action == 1) {
+        bool ok = true;
         if (E.cur_order() < 0) {
             const int no = E.next_order();
-            if (no < E.norders()) {
+            ok = no < E.norders();
+            if (ok) {
                 E.set_next_order(no + 1);
                 E.set_cur_order(no);
                 E.set_cur_idx(0);
                 E.set_cur_info(T.orders[no * T.stride]);
-            } else {
-                return r;
             }
         }
-        if (!E.tray_valid()) {
+        if (ok && !E.tray_valid()) {
             const int pool = E.pool();
-            if (pool > 0) {
+            ok = pool > 0;
+            if (ok) {
                 E.set_pool(pool - 1);
                 E.set_tray_valid(1); E.set_tray_order(E.cur_order()); E.set_tray_start(E.cur_idx()); E.set_tray_count(0);
+            }
+        }
+        if (ok) {
+            const int cnt = E.tray_count();
+            if (cnt >= C.tray_cap || E.cur_order() != E.tray_order()) {   // full / :231-235 (unreachable)
+                push = true;
+                r |= 4u;
             } else {
-                return r;
+                E.set_tray_count(cnt + 1);
+                const int idx = E.cur_idx() + 1;
+                E.set_cur_idx(idx);
+                r |= 2u | 1u;
+                if (idx >= E.cur_n()) {
+                    push = true;
+                    E.set_cur_order(-1); E.set_cur_idx(0);
+                    r |= 4u;
+                } else if (cnt + 1 >= C.tray_cap) {
+                    push = true;
+                    r |= 4u;
+                }
             }
         }
-        const int cnt = E.tray_count();
-        if (cnt < C.tray_cap) {
-            if (E.cur_order() != E.tray_order()) {   // :231-235 (unreachable with the reference's flow)
-                push_tray();
-                return r | 4u;
-            }
-            E.set_tray_count(cnt + 1);
-            const int idx = E.cur_idx() + 1;
-            E.set_cur_idx(idx);
-            r |= 2u | 1u;
-            if (idx >= E.cur_n()) {
-                push_tray();
-                E.set_cur_order(-1); E.set_cur_idx(0);
-                return r | 4u;
-            }
-            if (cnt + 1 >= C.tray_cap) {
-                push_tray();
-                return r | 4u;
-            }
-        } else {
-            push_tray();
-            return r | 4u;
-        }
-    } else if (action == 2) {
-        if (E.tray_valid() && E.tray_count() > 0) {
-            push_tray();
-            r |= 1u;
-        }
+    }
+    if (push) {
+        const int s = slot_new(E, T, tc_make(E.tray_order(), E.tray_start(), E.tray_count()));
+        if (s >= 0) list_push<L_PREADY>(E, T, s);
+        E.set_tray_valid(0);
     }
     return r;
 }
 
 // FJSPSimulation.add_tray_to_packaging (FJSPSimulation.py:402-430): first station (dict order
-// blue_1, blue_2, red, green) whose colour matches and whose Resource has capacity.
-template <int S>
-FJSP_DEV void pkg_enqueue(Env& E, const Tables& T, int s, int n) {
-    list_push<L_PKG + S>(E, T, s);
-    if (E.p_qfirst(S) == NIL) E.set_p_qfirst(S, s);
-    E.set_p_queued(S, E.p_queued(S) + n);
-}
-FJSP_DEV void add_tray_to_packaging(Env& E, const Tables& T, const Cfg& C, int s, int code) {
-    const int color = E.carry_color();
-    // PackagingColor RED=1 BLUE=2 GREEN=3; stations 0,1 blue, 2 red, 3 green
-    const int n = tc_count(code);
-    if (color == 2 && E.p_inflight(0) < C.pkg_cap) pkg_enqueue<0>(E, T, s, n);
-    else if (color == 2 && E.p_inflight(1) < C.pkg_cap) pkg_enqueue<1>(E, T, s, n);
-    else if (color == 1 && E.p_inflight(2) < C.pkg_cap) pkg_enqueue<2>(E, T, s, n);
-    else if (color == 3 && E.p_inflight(3) < C.pkg_cap) pkg_enqueue<3>(E, T, s, n);
-    else E.flag(ST_PROD_LOST);
+// blue_1, blue_2, red, green) whose colour matches and whose Resource has capacity; -1 = none
+// (the products are lost).  PackagingColor RED=1 BLUE=2 GREEN=3.
+FJSP_DEV int pkg_station(const Env& E, const Cfg& C, int color) {
+    return (color == 2 && E.p_inflight(0) < C.pkg_cap) ? 0
+         : (color == 2 && E.p_inflight(1) < C.pkg_cap) ? 1
+         : (color == 1 && E.p_inflight(2) < C.pkg_cap) ? 2
+         : (color == 3 && E.p_inflight(3) < C.pkg_cap) ? 3 : -1;
 }
 
-template <int L>
-FJSP_DEV int pop_if_any(Env& E, const Tables& T) {
-    return E.ll(L) ? list_pop<L>(E, T) : -1;
-}
+constexpr uint32_t PICK_LISTS = (1u << L_PREADY) | (1u << L_STORAGE) | (1u << L_M0R) | (1u << L_M1R);
+constexpr uint32_t DROP_LISTS = (1u << L_STORAGE) | (1u << L_M0Q) | (1u << L_M1Q) | (0xFu << L_PKG);
 
 // AGVAgent.execute_action / _execute_pickup / _execute_drop (AGVAgent.py:180-368).
-// Returns the result word; *move_to receives the target location of a spawned move.
+// Returns the result word; *move_to receives the target location of a spawned move.  PICKUP and
+// DROP resolve their source / target list from the location first, so every lane performs (at
+// most) one list operation in one shared code path.
 FJSP_DEV uint32_t agv_execute(Env& E, const Tables& T, const Cfg& C, int action, int* move_to) {
     uint32_t r = R_EXEC;   // 1 success, 2 invalid, 4 moved, 8 pickup, 16 drop, 32 to packaging; 16.. distance
     const int loc = E.loc();
@@ -405,51 +429,59 @@ FJSP_DEV uint32_t agv_execute(Env& E, const Tables& T, const Cfg& C, int action,
         return r | 1u | 4u | ((uint32_t)d << 16);
     }
     if (action == 6) {
-        if (E.carry() != NIL || loc == LOC_PACK) return r | 2u;
-        int s;
-        switch (loc) {
-        case LOC_PICKUP: s = pop_if_any<L_PREADY>(E, T); break;
-        case LOC_SMALL: s = pop_if_any<L_M0R>(E, T); break;
-        case LOC_BIG: s = pop_if_any<L_M1R>(E, T); break;
-        default: s = pop_if_any<L_STORAGE>(E, T); break;
-        }
-        if (s < 0) return r | 2u;
+        const int src = loc == LOC_PICKUP ? L_PREADY : loc == LOC_SMALL ? L_M0R : loc == LOC_BIG ? L_M1R : L_STORAGE;
+        if (E.carry() != NIL || loc == LOC_PACK || (lword<PICK_LISTS>(E, src) >> 16) == 0) return r | 2u;
+        const int s = list_pop_dyn<PICK_LISTS>(E, T, src);
         const int code = T.scode[s * T.stride];
-        if (tc_count(code) > 0) {
-            const uint32_t w = T.orders[tc_order(code) * T.stride];
-            const uint32_t rg = tc_range(code);
-            E.set_carried(s, code, ow_type(w), ow_color(w), (w & rg) != rg, ((w >> 9) & rg) != rg);
-        } else {
-            E.set_carried(s, code, 0, 0, 0, 0);
-        }
+        const uint32_t w = T.orders[tc_order(code) * T.stride];
+        const uint32_t rg = tc_range(code);
+        if (tc_count(code) > 0) E.set_carried(s, code, ow_type(w), ow_color(w), (w & rg) != rg, ((w >> 9) & rg) != rg);
+        else E.set_carried(s, code, 0, 0, 0, 0);
         return r | 1u | 8u;
     }
     if (action == 7) {
         const int s = E.carry();
         if (s == NIL) return r | 2u;
         const int code = E.carry_code(), ty = E.carry_type(), np = E.carry_np();
-        switch (loc) {
-        case LOC_PICKUP:
-            if (tc_count(code) != 0) return r | 2u;
-            E.set_pool(E.pool() + 1);    // add_empty_tray
-            break;
-        case LOC_SMALL:
-            if (!(np && (ty == 1 || ty == 2))) return r | 2u;
-            list_push<L_M0Q>(E, T, s);
-            break;
-        case LOC_BIG:
-            if (!(np && (ty == 3 || ty == 2))) return r | 2u;
-            list_push<L_M1Q>(E, T, s);
-            break;
-        case LOC_STORAGE:
-            if (E.ll(L_STORAGE) < C.storage_cap) list_push<L_STORAGE>(E, T, s);
+        bool valid;
+        int dst = -1;   // list to push onto
+        int st = -1;    // packaging station
+        if (loc == LOC_PICKUP) {
+            valid = tc_count(code) == 0;                 // add_empty_tray
+            if (valid) E.set_pool(E.pool() + 1);
+        } else if (loc == LOC_SMALL) {
+            valid = np && (ty == 1 || ty == 2);
+            dst = L_M0Q;
+        } else if (loc == LOC_BIG) {
+            valid = np && (ty == 3 || ty == 2);
+            dst = L_M1Q;
+        } else if (loc == LOC_STORAGE) {
+            valid = true;
+            if (E.ll(L_STORAGE) < C.storage_cap) dst = L_STORAGE;
             else E.flag(ST_TRAY_LOST);
-            break;
-        default:   // PACKAGING
-            if (!(E.carry_nk() && !np)) return r | 2u;
-            add_tray_to_packaging(E, T, C, s, code);
-            r |= 32u;
-            break;
+        } else {                                         // PACKAGING
+            valid = E.carry_nk() && !np;
+            if (valid) {
+                r |= 32u;
+                st = pkg_station(E, C, E.carry_color());
+                if (st >= 0) dst = L_PKG + st;
+                else E.flag(ST_PROD_LOST);
+            }
+        }
+        if (!valid) return r | 2u;
+        if (dst >= 0) {
+            list_push_dyn<DROP_LISTS>(E, T, dst, s);
+            // PackagingAgent.add_tray: products join the queue (qfirst = first unqueued run).
+            // Written as a per-station select so the station words never become a
+            // dynamically indexed (scratch) array.
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t wk = E.w[20 + k];
+                const uint32_t qf = ((wk >> 2) & 0xFFu) == (uint32_t)NIL ? (uint32_t)s : ((wk >> 2) & 0xFFu);
+                const uint32_t nk = (wk & ~(0xFFu << 2) & 0x3FFFFu) | (qf << 2) |
+                                    (((wk >> 18) + (uint32_t)tc_count(code)) << 18);
+                E.w[20 + k] = (st == k) ? nk : wk;
+            }
         }
         E.set_carry(NIL);
         return r | 1u | 16u;
