@@ -802,12 +802,19 @@ FJSP_DEV void env_clear(Env& E, const Cfg& C) {
 
 // ---------------------------------------------------------------- one step
 // calculate_local_reward (utils/RewardModel.py:46-97) as one table lookup (build_reward_lut).
-FJSP_DEV double local_reward(const Cfg& C, int a, uint32_t r, int act) {
+FJSP_DEV uint32_t reward_index(int a, uint32_t r, int act) {
     const uint32_t a0 = act == 0;   // actions.get(agent_id, 0) == 0 (absent agents have r == 0)
     const uint32_t f = (r >> 1) & 7u;
-    const uint32_t idx = a == 0 ? (f | (a0 << 3)) : a == 1 ? 16u + ((r >> 1) & 31u)
-                                                           : (a <= 3 ? 48u : 64u) + (f | (a0 << 3));
-    return C.lut[idx];
+    return a == 0 ? (f | (a0 << 3)) : a == 1 ? 16u + ((r >> 1) & 31u) : (a <= 3 ? 48u : 64u) + (f | (a0 << 3));
+}
+FJSP_DEV double local_reward(const Cfg& C, int a, uint32_t r, int act) { return C.lut[reward_index(a, r, act)]; }
+
+// The int8 observation fields (queue lengths) overflow exactly when observe() would flag it;
+// lets a step that does not build the observation itself keep the sticky status bit.
+FJSP_DEV void flag_obs_overflow(Env& E) {
+    const bool ov = E.ll(L_M0Q) > 127 || E.ll(L_M1Q) > 127 || E.p_queued(0) > 127 || E.p_queued(1) > 127 ||
+                    E.p_queued(2) > 127 || E.p_queued(3) > 127;
+    if (ov) E.flag(ST_OBS_OVERFLOW | ST_DIVERGED);
 }
 
 // Actions in dict order, then env.run in closed form.  actions[a] for agent a (canonical order);

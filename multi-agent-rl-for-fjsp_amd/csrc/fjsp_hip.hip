@@ -292,19 +292,24 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t z) {
     return z;
 }
 
+__device__ __forceinline__ void synth_uniform(uint64_t seed, uint32_t gid, uint32_t step, int* act) {
+    const uint64_t h = fmix64(seed ^ fmix64(((uint64_t)gid << 32) | step));
+    const int nact[NA] = {3, 8, 3, 3, 3, 3, 3, 3};
+#pragma unroll
+    for (int a = 0; a < NA; a++) act[a] = (int)((((uint32_t)(h >> (8 * a)) & 0xFFu) * (uint32_t)nact[a]) >> 8);
+}
+
 __device__ __forceinline__ void synth_actions(uint64_t seed, uint32_t gid, uint32_t step, int mode, const Env& E,
                                               const Tables& T, const Cfg& C, int* act) {
     if (mode == FJSP_ACTIONS_HEURISTIC) {
         heuristic_actions(E, T, act);
         return;
     }
-    const uint64_t h = fmix64(seed ^ fmix64(((uint64_t)gid << 32) | step));
-    const int nact[NA] = {3, 8, 3, 3, 3, 3, 3, 3};
     if (mode == FJSP_ACTIONS_UNMASKED) {
-#pragma unroll
-        for (int a = 0; a < NA; a++) act[a] = (int)((((uint32_t)(h >> (8 * a)) & 0xFFu) * (uint32_t)nact[a]) >> 8);
+        synth_uniform(seed, gid, step, act);
         return;
     }
+    const uint64_t h = fmix64(seed ^ fmix64(((uint64_t)gid << 32) | step));
     MaskBits mb;
     compute_masks(E, C, mb);
 #pragma unroll
@@ -531,6 +536,120 @@ __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, u
 #endif
 }
 
+// K fused steps, pipelined over two wavefronts per 64-env workgroup (lean outputs only).
+// Wave 0 ("sim") advances the env state: actions, action phase, SimPy run, auto-reset; after
+// each step it leaves a snapshot of the pre-reset state (30 words), the 8 reward-table indices
+// and g/8 in LDS.  Wave 1 ("emit"), on another SIMD of the same CU, turns snapshot k into the
+// outputs of step k (rewards, observation, masks, term, trunc, status) while wave 0 already
+// computes step k+1, and precomputes the next step's actions when they do not depend on the
+// state (uniform random mode).  Snapshots and action slots are double-buffered; one
+// workgroup barrier per step orders them.
+struct alignas(16) PipeSnap {
+    double g8[BLOCK];
+    uint32_t w[NSTATE][BLOCK];
+    uint32_t ridx[2][BLOCK];   // reward_index of agents 0..3 / 4..7, one byte each
+};
+__device__ __forceinline__ uint32_t pack_actions(const int* act, int lo) {
+    return (uint32_t)act[lo] | ((uint32_t)act[lo + 1] << 8) | ((uint32_t)act[lo + 2] << 16) | ((uint32_t)act[lo + 3] << 24);
+}
+
+__global__ void __launch_bounds__(2 * BLOCK) k_step_pipe(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0,
+                                                         uint32_t step0, int mode, int autoreset, fjsp_out out) {
+    __shared__ PipeSnap snap[2];
+    __shared__ uint32_t s_act[2][2][BLOCK];
+    __shared__ uint32_t s_mtbuf[MTB * BLOCK];
+    __shared__ double s_lut[RLUT_SIZE];
+    for (int i = threadIdx.x; i < RLUT_SIZE; i += 2 * BLOCK) s_lut[i] = C.lut[i];
+    C.lut = s_lut;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / BLOCK);
+    const int lane = threadIdx.x % BLOCK;
+    const int e = blockIdx.x * BLOCK + lane;
+    const bool valid = e < S.n;
+    const bool pre = mode == FJSP_ACTIONS_UNMASKED;   // actions independent of the state
+    const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
+    if (wave == 1 && pre && K > 0) {
+        int act[NA];
+        synth_uniform(seed, gid0 + (uint32_t)e, step0, act);
+        s_act[0][0][lane] = pack_actions(act, 0);
+        s_act[0][1][lane] = pack_actions(act, 4);
+    }
+    __syncthreads();
+    if (wave == 0) {
+        Env E;
+        if (valid) env_load(E, S.words, S.n, e);
+        const Tables T = tables_of(S, valid ? e : 0);
+        for (int k = 0; k <= K; k++) {
+            if (k < K && valid) {
+                int act[NA];
+                if (pre) {
+                    const uint32_t a0 = s_act[k & 1][0][lane], a1 = s_act[k & 1][1][lane];
+#pragma unroll
+                    for (int a = 0; a < 4; a++) { act[a] = (a0 >> (8 * a)) & 0xFF; act[4 + a] = (a1 >> (8 * a)) & 0xFF; }
+                } else {
+                    synth_actions(seed, gid0 + (uint32_t)e, step0 + (uint32_t)k, mode, E, T, C, act);
+                }
+                uint32_t res[NA];
+                const double g8 = env_advance<true>(E, T, C, act, nullptr, res);
+                flag_obs_overflow(E);
+                PipeSnap& sp = snap[k & 1];
+                sp.g8[lane] = g8;
+#pragma unroll
+                for (int i = 0; i < NSTATE; i++) sp.w[i][lane] = E.w[i];
+                uint32_t r0 = 0, r1 = 0;
+#pragma unroll
+                for (int a = 0; a < 4; a++) {
+                    r0 |= reward_index(a, res[a], act[a]) << (8 * a);
+                    r1 |= reward_index(4 + a, res[4 + a], act[4 + a]) << (8 * a);
+                }
+                sp.ridx[0][lane] = r0;
+                sp.ridx[1][lane] = r1;
+                const int nord = E.norders();
+                const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
+                const int truncated = E.step() >= C.max_steps;
+                E.set_step(E.step() + 1);
+                if (autoreset && (all_done || truncated))
+                    E = env_reset_cold(E, T, C, S, e, nord, s_mtbuf + lane);   // reset(seed=None)
+            }
+            __syncthreads();
+        }
+        if (valid) env_store(E, S.words, S.n, e);
+    } else {
+        for (int k = 0; k <= K; k++) {
+            if (k > 0 && valid) {
+                const uint32_t t = (uint32_t)(k - 1);
+                const PipeSnap& sp = snap[(k - 1) & 1];
+                Env E;
+#pragma unroll
+                for (int i = 0; i < NSTATE; i++) E.w[i] = sp.w[i][lane];
+                const double g8 = sp.g8[lane];
+                if (out.rewards) {
+                    const uint32_t r0 = sp.ridx[0][lane], r1 = sp.ridx[1][lane];
+#pragma unroll
+                    for (int a = 0; a < NA; a++) {
+                        const uint32_t idx = ((a < 4 ? r0 : r1) >> (8 * (a & 3))) & 0xFFu;
+                        st32(out.rewards, (t * NA + (uint32_t)a) * n + ue, g8 + C.lut[idx]);
+                    }
+                }
+                StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, ue};
+                observe(E, C, sink);
+                const int nord = E.norders();
+                const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
+                const int truncated = E.step() >= C.max_steps;
+                if (out.term) st32(out.term, t * n + ue, (uint8_t)all_done);
+                if (out.trunc) st32(out.trunc, t * n + ue, (uint8_t)truncated);
+                if (out.status) st32(out.status, t * n + ue, E.status());
+            }
+            if (pre && k + 1 < K) {
+                int act[NA];
+                synth_uniform(seed, gid0 + (uint32_t)e, step0 + (uint32_t)(k + 1), act);
+                s_act[(k + 1) & 1][0][lane] = pack_actions(act, 0);
+                s_act[(k + 1) & 1][1][lane] = pack_actions(act, 4);
+            }
+            __syncthreads();
+        }
+    }
+}
+
 // transition_memory.py:83-105 over a [T][M] rollout buffer; column m = a*N + e
 template <class VT>
 __global__ void __launch_bounds__(256) k_gae(const double* __restrict__ r, const VT* __restrict__ v,
@@ -580,6 +699,7 @@ struct fjsp_handle {
     int use_lds;     // fused kernel variant (FJSP_FUSED_LDS env var / fjsp_set_option)
     int use_staged;  // LDS-staged wide output stores (FJSP_STAGED env var / fjsp_set_option)
     int timing;      // hipEvent bracketing of step launches (off while graph-capturing)
+    int use_pipe;    // two-wave pipelined k_step_many for lean outputs (FJSP_PIPE / fjsp_set_option)
 };
 
 static thread_local std::string g_err;
@@ -688,6 +808,8 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
         const char* st = getenv("FJSP_STAGED");
         h->use_staged = st ? atoi(st) : 0;   // measured: no faster than direct stores (opt-in)
         h->timing = 1;
+        const char* pp = getenv("FJSP_PIPE");
+        h->use_pipe = pp ? atoi(pp) : 1;
     }
     h->dcfg.step_size = c.step_size;
     h->dcfg.max_steps = c.max_episode_steps;
@@ -755,6 +877,7 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
     if (!h || !name) return fail("null argument");
     if (!strcmp(name, "fused_lds")) { h->use_lds = value != 0; return 0; }
     if (!strcmp(name, "staged_stores")) { h->use_staged = value != 0; return 0; }
+    if (!strcmp(name, "pipeline")) { h->use_pipe = value != 0; return 0; }
     if (!strcmp(name, "timing")) { h->timing = value != 0; if (!h->timing) h->timed = 0; return 0; }
     return fail("unknown option");
 }
@@ -840,7 +963,10 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
     const bool staged = h->use_staged && !full && h->n % BLOCK == 0 && al16(o.obs_i32) && al16(o.obs_i8) &&
                         al16(o.obs_f32) && al16(o.masks) && al16(o.rewards) && al16(o.term) && al16(o.trunc) &&
                         al16(o.status);
-    if (h->use_lds) {
+    if (h->use_pipe && !full && !staged) {
+        hipLaunchKernelGGL(k_step_pipe, grid, dim3(2 * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0,
+                           step0, action_mode, autoreset, o);
+    } else if (h->use_lds) {
         if (full) launch(k_step_many<true, true>);
         else if (staged) launch(k_step_many<true, false, true>);
         else launch(k_step_many<true, false>);

@@ -270,3 +270,22 @@ def test_staged_stores_match_direct_stores(G):
     rec, _, _ = O.rollout(n, steps, seeds=np.arange(n) + 5, gid0=0, num_orders=20, action_seed=11, policy=0)
     for k in ("obs_i32", "obs_i8", "obs_f32", "masks", "rewards"):
         assert P.bits_equal(outs[1][k], rec[k]), k
+
+
+@pytest.mark.parametrize("policy", ["random", "masked", "heuristic"])
+def test_pipelined_matches_single_wave(G, policy):
+    """The two-wave pipelined k_step_pipe (default for lean outputs) writes the same bytes and
+    leaves the same state as the single-wave k_step_many; N not a multiple of 64."""
+    n, steps = 1000, 333
+    outs = []
+    for pipe in (1, 0):
+        env = G.make_env(n)
+        G.native.check(G.native.lib().fjsp_set_option(env.handle, b"pipeline", pipe))
+        env.reset(seeds=torch.arange(n) * 3 + 1, num_orders=5 if policy == "heuristic" else 20)
+        r1 = G.to_np(env.rollout(steps, action_seed=21, policy=policy))
+        r2 = G.to_np(env.rollout(7, action_seed=21, step0=steps, policy=policy, infos=True))   # full path after
+        outs.append((r1, r2))
+    for k in outs[0][0]:
+        assert P.bits_equal(outs[0][0][k], outs[1][0][k]), k
+    for k in outs[0][1]:
+        assert P.bits_equal(outs[0][1][k], outs[1][1][k]), k
