@@ -153,8 +153,9 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
                 fjsp_handle** out);
 int fjsp_destroy(fjsp_handle* h);
 int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
-/* Tuning knobs: "fused_lds" (0/1, default 0: stage the per-env tables of k_step_many in LDS,
- * one 64-env workgroup per CU); "staged_stores" (0/1, default 0: k_step_many stages each
+/* Tuning knobs: "fused_lds" (-1/0/1, default -1 = auto, on while N <= 16384: stage the per-env
+ * tables of k_step_many in LDS, one 64-env workgroup per CU); "pipeline" (0/1, default 1: lean
+ * outputs use the two-wave pipelined kernel); "staged_stores" (0/1, default 0: k_step_many stages each
  * step's obs / masks / rewards / term / trunc / status in LDS and writes them as 16-byte
  * chunks; used when only those outputs are requested, N % 64 == 0 and rows are aligned);
  * "timing" (0/1, default 1: bracket fjsp_step / fjsp_step_many launches with hipEvents for

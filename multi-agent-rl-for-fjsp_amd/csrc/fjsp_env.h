@@ -72,8 +72,10 @@ enum : int { W_ORDER = 0, W_THROUGHPUT, W_TIME, W_PICK_LOAD, W_PICK_TRAY, W_PICK
 // Reward lookup table (device memory): the local reward of every (agent kind, result bits,
 // action == 0) combination, each summed from 0.0 in calculate_local_reward's order on the host,
 // plus the global-reward weights.  Layout: [0,16) pickup, [16,48) AGV, [48,64) machine,
-// [64,80) packaging, [80] ORDER, [81] THROUGHPUT, [82] TIME * step_size.
-constexpr int RLUT_SIZE = 96;
+// [64,80) packaging, [80] ORDER, [81] THROUGHPUT, [82] TIME * step_size, [96,160) progress.
+// [96, 160): (1.0 / n) * 100.0 for n < 64 (PackagingAgent START progress, in fp64).
+constexpr int RPROG = 96, RPROG_N = 64;
+constexpr int RLUT_SIZE = RPROG + RPROG_N;
 
 struct Cfg {
     int step_size, max_steps, tray_cap, mask_tray_cap, storage_cap, pool0, pkg_cap;
@@ -110,6 +112,7 @@ inline void build_reward_lut(const double* w, int step_size, double* lut) {
     lut[80] = w[W_ORDER];
     lut[81] = w[W_THROUGHPUT];
     lut[82] = w[W_TIME] * (double)step_size;   // TIME_PENALTY * time_elapsed (time_elapsed = step_size)
+    for (int n = 1; n < RPROG_N; n++) lut[RPROG + n] = (1.0 / (double)n) * 100.0;
 }
 
 // status bits (include/fjsp.h)
@@ -338,65 +341,59 @@ FJSP_DEV int slot_new(Env& E, const Tables& T, int code) {
 // ---- reward / result bit layout (oracle/fjsp_oracle.c, RESULT_KEYS in gen_golden.py)
 constexpr uint32_t R_EXEC = 0x80u;
 
-// PickupStationAgent.execute_action (PickupStationAgent.py:190-276).  Every path that hands a
-// tray to ready_trays (order finished, tray full, SIGNAL, the unreachable order mismatch) sets
-// `push`; the one push at the end keeps its stores in a single code path.
+// PickupStationAgent.execute_action (PickupStationAgent.py:190-276), predicated like
+// agv_execute: LOAD's outcome (start the next order, take an empty tray, load one product,
+// hand the tray to ready_trays when the order ends / the tray is full) and SIGNAL are
+// conditions; the only memory operations are the next order's word (when an order starts)
+// and the single tray push.
 FJSP_DEV uint32_t pickup_execute(Env& E, const Tables& T, const Cfg& C, int action) {
-    uint32_t r = R_EXEC;   // 1 success, 2 product_loaded, 4 tray_completed, 8 idle_with_orders
-    if (action == 0) {
-        const int has_orders = E.next_order() < E.norders() || E.cur_order() >= 0;
-        return r | 1u | (has_orders ? 8u : 0u);
-    }
-    bool push = false;
-    if (action == 2) {
-        push = E.tray_valid() && E.tray_count() > 0;
-        r |= push ? 1u : 0u;
-    } else if (action == 1) {
-        bool ok = true;
-        if (E.cur_order() < 0) {
-            const int no = E.next_order();
-            ok = no < E.norders();
-            if (ok) {
-                E.set_next_order(no + 1);
-                E.set_cur_order(no);
-                E.set_cur_idx(0);
-                E.set_cur_info(T.orders[no * T.stride]);
-            }
-        }
-        if (ok && !E.tray_valid()) {
-            const int pool = E.pool();
-            ok = pool > 0;
-            if (ok) {
-                E.set_pool(pool - 1);
-                E.set_tray_valid(1); E.set_tray_order(E.cur_order()); E.set_tray_start(E.cur_idx()); E.set_tray_count(0);
-            }
-        }
-        if (ok) {
-            const int cnt = E.tray_count();
-            if (cnt >= C.tray_cap || E.cur_order() != E.tray_order()) {   // full / :231-235 (unreachable)
-                push = true;
-                r |= 4u;
-            } else {
-                E.set_tray_count(cnt + 1);
-                const int idx = E.cur_idx() + 1;
-                E.set_cur_idx(idx);
-                r |= 2u | 1u;
-                if (idx >= E.cur_n()) {
-                    push = true;
-                    E.set_cur_order(-1); E.set_cur_idx(0);
-                    r |= 4u;
-                } else if (cnt + 1 >= C.tray_cap) {
-                    push = true;
-                    r |= 4u;
-                }
-            }
-        }
-    }
+    const int co = E.cur_order(), no = E.next_order();
+    const bool more = no < E.norders();
+    const bool has_orders = more || co >= 0;
+    const bool a1 = action == 1;
+    // order (PickupStationAgent.py:210-215)
+    const bool start = a1 && co < 0 && more;
+    if (start) E.set_cur_info(T.orders[no * T.stride]);
+    E.set_next_order(no + (start ? 1 : 0));
+    const int co1 = start ? no : co;
+    const int idx1 = start ? 0 : E.cur_idx();
+    const bool ok_order = a1 && co1 >= 0;
+    // tray (:217-222)
+    const bool tv = E.tray_valid();
+    const int pool = E.pool();
+    const bool take = ok_order && !tv && pool > 0;
+    const bool ok = ok_order && (tv || pool > 0);
+    const int cnt = take ? 0 : E.tray_count();
+    const int torder = take ? co1 : E.tray_order();
+    const int tstart = take ? idx1 : E.tray_start();
+    // load one product (:224-262)
+    const bool blocked = ok && (cnt >= C.tray_cap || co1 != torder);   // full / :231-235 (unreachable)
+    const bool load = ok && !blocked;
+    const int cnt2 = cnt + (load ? 1 : 0);
+    const int idx2 = idx1 + (load ? 1 : 0);
+    const bool finished = load && idx2 >= E.cur_n();
+    const bool trayfull = load && !finished && cnt2 >= C.tray_cap;
+    // SIGNAL (:264-272)
+    const bool sig = action == 2 && tv && E.tray_count() > 0;
+    const bool push = (ok && (blocked || finished || trayfull)) || sig;
+    // state
+    E.set_pool(pool - (take ? 1 : 0));
+    E.set_cur_order(finished ? -1 : co1);
+    E.set_cur_idx(finished ? 0 : idx2);
+    E.set_tray_order(torder);
+    E.set_tray_start(tstart);
+    E.set_tray_count(cnt2);
+    E.set_tray_valid((tv || take) && !push);
     if (push) {
-        const int s = slot_new(E, T, tc_make(E.tray_order(), E.tray_start(), E.tray_count()));
+        const int s = slot_new(E, T, tc_make(torder, tstart, cnt2));
         if (s >= 0) list_push<L_PREADY>(E, T, s);
-        E.set_tray_valid(0);
     }
+    // result: 1 success, 2 product_loaded, 4 tray_completed, 8 idle_with_orders
+    uint32_t r = R_EXEC;
+    r |= action == 0 ? (1u | (has_orders ? 8u : 0u)) : 0u;
+    r |= load ? 3u : 0u;
+    r |= (ok && (blocked || finished || trayfull)) ? 4u : 0u;
+    r |= sig ? 1u : 0u;
     return r;
 }
 
@@ -414,79 +411,93 @@ constexpr uint32_t PICK_LISTS = (1u << L_PREADY) | (1u << L_STORAGE) | (1u << L_
 constexpr uint32_t DROP_LISTS = (1u << L_STORAGE) | (1u << L_M0Q) | (1u << L_M1Q) | (0xFu << L_PKG);
 
 // AGVAgent.execute_action / _execute_pickup / _execute_drop (AGVAgent.py:180-368).
-// Returns the result word; *move_to receives the target location of a spawned move.  PICKUP and
-// DROP resolve their source / target list from the location first, so every lane performs (at
-// most) one list operation in one shared code path.
+// Returns the result word; *move_to receives the target location of a spawned move.
+// Written predicated (straight-line): every action's outcome is computed as a condition and the
+// state words are updated with selects, so a wavefront whose lanes take all 8 actions executes
+// one path instead of the union of 8 branchy ones.  Only the memory operations sit in (two)
+// small guarded blocks: the PICKUP pop's loads and the DROP push's stores.
 FJSP_DEV uint32_t agv_execute(Env& E, const Tables& T, const Cfg& C, int action, int* move_to) {
-    uint32_t r = R_EXEC;   // 1 success, 2 invalid, 4 moved, 8 pickup, 16 drop, 32 to packaging; 16.. distance
     const int loc = E.loc();
-    if (action == 0) return r | 1u;
-    if (action >= 1 && action <= 5) {
-        const int l = move_loc(action);
-        const int d = manhattan(loc, l);
-        if (d == 0) return r | 1u;
-        *move_to = l;
-        return r | 1u | 4u | ((uint32_t)d << 16);
+    const int carry = E.carry();
+    const bool has = carry != NIL;
+    // 1..5: moves (AGVAgent.py:218-252); distance 0 is a successful no-op
+    const bool is_move = action >= 1 && action <= 5;
+    const int ml = move_loc(action);
+    const int d = manhattan(loc, ml);
+    const bool moved = is_move && d != 0;
+    // 6: PICKUP, FIFO front of the list at this location (_execute_pickup :254-293)
+    const int src = loc == LOC_PICKUP ? L_PREADY : loc == LOC_SMALL ? L_M0R : loc == LOC_BIG ? L_M1R : L_STORAGE;
+    const uint32_t lws = lword<PICK_LISTS>(E, src);
+    const bool ok6 = action == 6 && !has && loc != LOC_PACK && (lws >> 16) != 0;
+    // 7: DROP (_execute_drop :295-368)
+    const int code = E.carry_code(), ty = E.carry_type(), np = E.carry_np(), nk = E.carry_nk();
+    const bool at_pick = loc == LOC_PICKUP, at_small = loc == LOC_SMALL, at_big = loc == LOC_BIG;
+    const bool at_store = loc == LOC_STORAGE, at_pack = loc == LOC_PACK;
+    const bool valid7 = (at_pick && tc_count(code) == 0) || (at_small && np && (ty == 1 || ty == 2)) ||
+                        (at_big && np && (ty == 3 || ty == 2)) || at_store || (at_pack && nk && !np);
+    const bool ok7 = action == 7 && has && valid7;
+    const bool store_full = E.ll(L_STORAGE) >= C.storage_cap;
+    const int st = pkg_station(E, C, E.carry_color());
+    const int dst = at_small ? L_M0Q : at_big ? L_M1Q : at_store ? (store_full ? -1 : L_STORAGE)
+                  : at_pack ? (st >= 0 ? L_PKG + st : -1) : -1;
+    // memory: pop (loads) / push (stores)
+    uint32_t next = 0, scode = 0, ow = 0;
+    const int ps = (int)(lws & 0xFFu);
+    if (ok6) {
+        next = T.snext[ps * T.stride];
+        scode = T.scode[ps * T.stride];
+        ow = T.orders[tc_order((int)scode) * T.stride];
     }
-    if (action == 6) {
-        const int src = loc == LOC_PICKUP ? L_PREADY : loc == LOC_SMALL ? L_M0R : loc == LOC_BIG ? L_M1R : L_STORAGE;
-        if (E.carry() != NIL || loc == LOC_PACK || (lword<PICK_LISTS>(E, src) >> 16) == 0) return r | 2u;
-        const int s = list_pop_dyn<PICK_LISTS>(E, T, src);
-        const int code = T.scode[s * T.stride];
-        const uint32_t w = T.orders[tc_order(code) * T.stride];
-        const uint32_t rg = tc_range(code);
-        if (tc_count(code) > 0) E.set_carried(s, code, ow_type(w), ow_color(w), (w & rg) != rg, ((w >> 9) & rg) != rg);
-        else E.set_carried(s, code, 0, 0, 0, 0);
-        return r | 1u | 8u;
+    const bool push = ok7 && dst >= 0;
+    const uint32_t lwd = lword<DROP_LISTS>(E, dst);
+    if (push) {
+        T.snext[carry * T.stride] = (uint8_t)NIL;
+        if ((lwd >> 16) != 0) T.snext[((lwd >> 8) & 0xFFu) * T.stride] = (uint8_t)carry;
     }
-    if (action == 7) {
-        const int s = E.carry();
-        if (s == NIL) return r | 2u;
-        const int code = E.carry_code(), ty = E.carry_type(), np = E.carry_np();
-        bool valid;
-        int dst = -1;   // list to push onto
-        int st = -1;    // packaging station
-        if (loc == LOC_PICKUP) {
-            valid = tc_count(code) == 0;                 // add_empty_tray
-            if (valid) E.set_pool(E.pool() + 1);
-        } else if (loc == LOC_SMALL) {
-            valid = np && (ty == 1 || ty == 2);
-            dst = L_M0Q;
-        } else if (loc == LOC_BIG) {
-            valid = np && (ty == 3 || ty == 2);
-            dst = L_M1Q;
-        } else if (loc == LOC_STORAGE) {
-            valid = true;
-            if (E.ll(L_STORAGE) < C.storage_cap) dst = L_STORAGE;
-            else E.flag(ST_TRAY_LOST);
-        } else {                                         // PACKAGING
-            valid = E.carry_nk() && !np;
-            if (valid) {
-                r |= 32u;
-                st = pkg_station(E, C, E.carry_color());
-                if (st >= 0) dst = L_PKG + st;
-                else E.flag(ST_PROD_LOST);
-            }
-        }
-        if (!valid) return r | 2u;
-        if (dst >= 0) {
-            list_push_dyn<DROP_LISTS>(E, T, dst, s);
-            // PackagingAgent.add_tray: products join the queue (qfirst = first unqueued run).
-            // Written as a per-station select so the station words never become a
-            // dynamically indexed (scratch) array.
+    // list words
+    const uint32_t n6 = (lws >> 16) - 1u;
+    const uint32_t popped = n6 == 0 ? ((uint32_t)NIL | ((uint32_t)NIL << 8)) : (next | (lws & 0xFF00u) | (n6 << 16));
+    const uint32_t nd = lwd >> 16;
+    const uint32_t pushed = (nd == 0 ? (uint32_t)carry : (lwd & 0xFFu)) | ((uint32_t)carry << 8) | ((nd + 1) << 16);
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t wk = E.w[20 + k];
-                const uint32_t qf = ((wk >> 2) & 0xFFu) == (uint32_t)NIL ? (uint32_t)s : ((wk >> 2) & 0xFFu);
-                const uint32_t nk = (wk & ~(0xFFu << 2) & 0x3FFFFu) | (qf << 2) |
-                                    (((wk >> 18) + (uint32_t)tc_count(code)) << 18);
-                E.w[20 + k] = (st == k) ? nk : wk;
-            }
-        }
-        E.set_carry(NIL);
-        return r | 1u | 16u;
+    for (int i = 0; i < NLIST; i++) {
+        if (!(((PICK_LISTS | DROP_LISTS) >> i) & 1u)) continue;
+        uint32_t v = E.w[7 + i];
+        if ((PICK_LISTS >> i) & 1u) v = (ok6 && src == i) ? popped : v;
+        if ((DROP_LISTS >> i) & 1u) v = (push && dst == i) ? pushed : v;
+        E.w[7 + i] = v;
     }
-    return r | 2u;
+    // packaging station: the dropped tray's products join its queue (PackagingAgent.add_tray)
+    const bool to_st = push && at_pack;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t wk = E.w[20 + k];
+        const uint32_t qf = ((wk >> 2) & 0xFFu) == (uint32_t)NIL ? (uint32_t)carry : ((wk >> 2) & 0xFFu);
+        const uint32_t nw = (wk & ~(0xFFu << 2) & 0x3FFFFu) | (qf << 2) | (((wk >> 18) + (uint32_t)tc_count(code)) << 18);
+        E.w[20 + k] = (to_st && st == k) ? nw : wk;
+    }
+    // AGV word: carried tray (pickup) / empty hands (drop)
+    const uint32_t rg = tc_range((int)scode);
+    const bool full6 = tc_count((int)scode) > 0;
+    const uint32_t carried = (E.w[6] & 7u) | ((uint32_t)ps << 3) | (scode << 11) |
+                             (full6 ? (((uint32_t)ow_type(ow) << 24) | ((uint32_t)ow_color(ow) << 26) |
+                                       ((uint32_t)((ow & rg) != rg) << 28) | ((uint32_t)(((ow >> 9) & rg) != rg) << 29))
+                                    : 0u);
+    const uint32_t dropped = (E.w[6] & ~(0xFFu << 3)) | ((uint32_t)NIL << 3);
+    E.w[6] = ok6 ? carried : ok7 ? dropped : E.w[6];
+    // add_empty_tray at the pickup station; lost tray / products flags
+    E.set_pool(E.pool() + ((ok7 && at_pick) ? 1 : 0));
+    uint32_t fl = (ok7 && at_store && store_full) ? ST_TRAY_LOST : 0u;
+    fl |= (ok7 && at_pack && st < 0) ? ST_PROD_LOST : 0u;
+    E.w[2] |= fl;
+    if (moved) *move_to = ml;
+    // result: 1 success, 2 invalid, 4 moved, 8 pickup, 16 drop, 32 to packaging; 16.. distance
+    const bool success = action == 0 || is_move || ok6 || ok7;
+    uint32_t r = R_EXEC | (success ? 1u : 2u);
+    r |= moved ? (4u | ((uint32_t)d << 16)) : 0u;
+    r |= ok6 ? 8u : 0u;
+    r |= ok7 ? (16u | (at_pack ? 32u : 0u)) : 0u;
+    return r;
 }
 
 // MachineAgent.execute_action (MachineAgent.py:99-139); grant happens in the run.
@@ -516,21 +527,20 @@ FJSP_DEV uint32_t machine_execute(Env& E, const Tables& T, int action, int* star
 
 // PackagingAgent.execute_action (PackagingAgent.py:301-335)
 template <int S>
-FJSP_DEV uint32_t pack_execute(Env& E, int action, int* started) {
-    uint32_t r = R_EXEC;   // 1 success, 2 started, 4 completed, 8 idle_with_queue; 16.. completed count
+FJSP_DEV uint32_t pack_execute(Env& E, const Cfg& C, int action, int* started) {
     const int n = E.p_queued(S);
-    if (action == 0) {
-        r |= 1u | ((n > 0 && !E.p_busy(S)) ? 8u : 0u);
-    } else if (action == 1) {
-        if (n > 0) {
-            *started = 1;
-            // self.processing_progress = (i / len(self.product_queue)) * 100 with i == 1
-            E.set_p_prog(S, (float)((1.0 / (double)n) * 100.0));
-            r |= 2u | 1u;
-        }
-    } else if (action == 2) {
-        if (!E.p_busy(S) && E.p_hascur(S)) r |= 4u | ((uint32_t)E.p_completed(S) << 16);
-    }
+    const bool busy = E.p_busy(S);
+    const bool go = action == 1 && n > 0;
+    // self.processing_progress = (i / len(self.product_queue)) * 100 with i == 1, in fp64 then
+    // float32 (tabulated for n < 64 in the LDS reward table; exact either way)
+    const double pd = n < RPROG_N ? C.lut[RPROG + n] : (1.0 / (double)n) * 100.0;
+    E.w[26 + S] = go ? __float_as_uint_fjsp((float)pd) : E.w[26 + S];
+    *started = go ? 1 : *started;
+    // 1 success, 2 started, 4 completed, 8 idle_with_queue; 16.. completed count
+    uint32_t r = R_EXEC;
+    r |= action == 0 ? (1u | ((n > 0 && !busy) ? 8u : 0u)) : 0u;
+    r |= go ? 3u : 0u;
+    r |= (action == 2 && !busy && E.p_hascur(S)) ? (4u | ((uint32_t)E.p_completed(S) << 16)) : 0u;
     return r;
 }
 
@@ -836,10 +846,10 @@ FJSP_DEV double env_advance(Env& E, const Tables& T, const Cfg& C, const int* ac
             case 1: r = agv_execute(E, T, C, ac, &move_to); break;
             case 2: r = machine_execute<0>(E, T, ac, &m_start[0]); break;
             case 3: r = machine_execute<1>(E, T, ac, &m_start[1]); break;
-            case 4: r = pack_execute<0>(E, ac, &p_started[0]); break;
-            case 5: r = pack_execute<1>(E, ac, &p_started[1]); break;
-            case 6: r = pack_execute<2>(E, ac, &p_started[2]); break;
-            default: r = pack_execute<3>(E, ac, &p_started[3]); break;
+            case 4: r = pack_execute<0>(E, C, ac, &p_started[0]); break;
+            case 5: r = pack_execute<1>(E, C, ac, &p_started[1]); break;
+            case 6: r = pack_execute<2>(E, C, ac, &p_started[2]); break;
+            default: r = pack_execute<3>(E, C, ac, &p_started[3]); break;
             }
         }
         res[a] = r;

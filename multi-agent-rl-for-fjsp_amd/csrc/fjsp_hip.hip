@@ -553,8 +553,13 @@ __device__ __forceinline__ uint32_t pack_actions(const int* act, int lo) {
     return (uint32_t)act[lo] | ((uint32_t)act[lo + 1] << 8) | ((uint32_t)act[lo + 2] << 16) | ((uint32_t)act[lo + 3] << 24);
 }
 
+template <bool LDS>
 __global__ void __launch_bounds__(2 * BLOCK) k_step_pipe(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0,
                                                          uint32_t step0, int mode, int autoreset, fjsp_out out) {
+    __shared__ uint32_t s_orders[LDS ? MAX_ORDERS * BLOCK : 1];
+    __shared__ uint16_t s_code[LDS ? MAX_SLOTS * BLOCK : 1];
+    __shared__ uint8_t s_next[LDS ? MAX_SLOTS * BLOCK : 1];
+    __shared__ uint16_t s_cstep[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ PipeSnap snap[2];
     __shared__ uint32_t s_act[2][2][BLOCK];
     __shared__ uint32_t s_mtbuf[MTB * BLOCK];
@@ -577,7 +582,26 @@ __global__ void __launch_bounds__(2 * BLOCK) k_step_pipe(DevState S, Cfg C, int 
     if (wave == 0) {
         Env E;
         if (valid) env_load(E, S.words, S.n, e);
-        const Tables T = tables_of(S, valid ? e : 0);
+        Tables T = tables_of(S, valid ? e : 0);
+        if constexpr (LDS) {   // the env's order table and used slot prefix live in LDS for the launch
+            T.orders = s_orders + lane;
+            T.scode = s_code + lane;
+            T.snext = s_next + lane;
+            T.scstep = s_cstep + lane;
+            T.stride = BLOCK;
+            if (valid) {
+                for (int o = 0; o < E.norders(); o++) T.orders[o * BLOCK] = S.orders[(size_t)o * S.n + e];
+                for (int q = 0; q < E.slot_next(); q++) {
+                    T.scode[q * BLOCK] = S.scode[(size_t)q * S.n + e];
+                    T.snext[q * BLOCK] = S.snext[(size_t)q * S.n + e];
+                    T.scstep[q * BLOCK] = S.scstep[(size_t)q * S.n + e];
+                }
+            }
+        }
+#ifdef FJSP_STAMPS
+        for (int i = 0; i < 8; i++) E.st_acc[i] = 0;
+        E.st_t0 = __builtin_amdgcn_s_memtime();
+#endif
         for (int k = 0; k <= K; k++) {
             if (k < K && valid) {
                 int act[NA];
@@ -588,6 +612,7 @@ __global__ void __launch_bounds__(2 * BLOCK) k_step_pipe(DevState S, Cfg C, int 
                 } else {
                     synth_actions(seed, gid0 + (uint32_t)e, step0 + (uint32_t)k, mode, E, T, C, act);
                 }
+                FJSP_STAMP(E, 0);
                 uint32_t res[NA];
                 const double g8 = env_advance<true>(E, T, C, act, nullptr, res);
                 flag_obs_overflow(E);
@@ -606,13 +631,29 @@ __global__ void __launch_bounds__(2 * BLOCK) k_step_pipe(DevState S, Cfg C, int 
                 const int nord = E.norders();
                 const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
                 const int truncated = E.step() >= C.max_steps;
+                FJSP_STAMP(E, 3);
                 E.set_step(E.step() + 1);
                 if (autoreset && (all_done || truncated))
                     E = env_reset_cold(E, T, C, S, e, nord, s_mtbuf + lane);   // reset(seed=None)
+                FJSP_STAMP(E, 6);
             }
             __syncthreads();
         }
-        if (valid) env_store(E, S.words, S.n, e);
+        if (valid) {
+            if constexpr (LDS) {
+                for (int o = 0; o < E.norders(); o++) S.orders[(size_t)o * S.n + e] = T.orders[o * BLOCK];
+                for (int q = 0; q < E.slot_next(); q++) {
+                    S.scode[(size_t)q * S.n + e] = T.scode[q * BLOCK];
+                    S.snext[(size_t)q * S.n + e] = T.snext[q * BLOCK];
+                    S.scstep[(size_t)q * S.n + e] = T.scstep[q * BLOCK];
+                }
+            }
+            env_store(E, S.words, S.n, e);
+        }
+#ifdef FJSP_STAMPS
+        if (lane == 0)
+            for (int i = 0; i < 8; i++) atomicAdd((unsigned long long*)&g_stamps[i], (unsigned long long)E.st_acc[i]);
+#endif
     } else {
         for (int k = 0; k <= K; k++) {
             if (k > 0 && valid) {
@@ -804,7 +845,7 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
         // the LDS variant (97.5 KB per 64-env workgroup) measured no faster than the
         // global-table variant once resets stopped draining the store queue; opt-in only
         const char* v = getenv("FJSP_FUSED_LDS");
-        h->use_lds = v ? atoi(v) : 0;
+        h->use_lds = v ? atoi(v) : -1;   // -1: auto (LDS tables when every workgroup gets a CU)
         const char* st = getenv("FJSP_STAGED");
         h->use_staged = st ? atoi(st) : 0;   // measured: no faster than direct stores (opt-in)
         h->timing = 1;
@@ -875,7 +916,7 @@ int fjsp_destroy(fjsp_handle* h) {
 
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
     if (!h || !name) return fail("null argument");
-    if (!strcmp(name, "fused_lds")) { h->use_lds = value != 0; return 0; }
+    if (!strcmp(name, "fused_lds")) { h->use_lds = value < 0 ? -1 : value != 0; return 0; }
     if (!strcmp(name, "staged_stores")) { h->use_staged = value != 0; return 0; }
     if (!strcmp(name, "pipeline")) { h->use_pipe = value != 0; return 0; }
     if (!strcmp(name, "timing")) { h->timing = value != 0; if (!h->timing) h->timed = 0; return 0; }
@@ -963,10 +1004,16 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
     const bool staged = h->use_staged && !full && h->n % BLOCK == 0 && al16(o.obs_i32) && al16(o.obs_i8) &&
                         al16(o.obs_f32) && al16(o.masks) && al16(o.rewards) && al16(o.term) && al16(o.trunc) &&
                         al16(o.status);
+    // LDS tables (97.5 KB per 64-env workgroup) pay while every workgroup has a CU of its own
+    const bool lds = h->use_lds < 0 ? h->n <= 256 * BLOCK : h->use_lds != 0;
     if (h->use_pipe && !full && !staged) {
-        hipLaunchKernelGGL(k_step_pipe, grid, dim3(2 * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0,
-                           step0, action_mode, autoreset, o);
-    } else if (h->use_lds) {
+        if (lds)
+            hipLaunchKernelGGL(k_step_pipe<true>, grid, dim3(2 * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed,
+                               env_gid0, step0, action_mode, autoreset, o);
+        else
+            hipLaunchKernelGGL(k_step_pipe<false>, grid, dim3(2 * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed,
+                               env_gid0, step0, action_mode, autoreset, o);
+    } else if (lds) {
         if (full) launch(k_step_many<true, true>);
         else if (staged) launch(k_step_many<true, false, true>);
         else launch(k_step_many<true, false>);

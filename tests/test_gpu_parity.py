@@ -278,14 +278,16 @@ def test_pipelined_matches_single_wave(G, policy):
     leaves the same state as the single-wave k_step_many; N not a multiple of 64."""
     n, steps = 1000, 333
     outs = []
-    for pipe in (1, 0):
+    for pipe, lds in ((1, -1), (0, 0), (1, 0)):
         env = G.make_env(n)
         G.native.check(G.native.lib().fjsp_set_option(env.handle, b"pipeline", pipe))
+        G.native.check(G.native.lib().fjsp_set_option(env.handle, b"fused_lds", lds))
         env.reset(seeds=torch.arange(n) * 3 + 1, num_orders=5 if policy == "heuristic" else 20)
         r1 = G.to_np(env.rollout(steps, action_seed=21, policy=policy))
         r2 = G.to_np(env.rollout(7, action_seed=21, step0=steps, policy=policy, infos=True))   # full path after
         outs.append((r1, r2))
-    for k in outs[0][0]:
-        assert P.bits_equal(outs[0][0][k], outs[1][0][k]), k
-    for k in outs[0][1]:
-        assert P.bits_equal(outs[0][1][k], outs[1][1][k]), k
+    for o in outs[1:]:
+        for k in outs[0][0]:
+            assert P.bits_equal(outs[0][0][k], o[0][k]), k
+        for k in outs[0][1]:
+            assert P.bits_equal(outs[0][1][k], o[1][k]), k
