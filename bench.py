@@ -7,7 +7,8 @@ actions (action_space.sample() semantics) from the on-device counter RNG, auto-r
 truncation/termination (MT19937 stream continued like reset(seed=None)).  One bench "step" =
 one FJSPSimulation.step() of every env on this GPU; obs (reference dtypes), fp64 rewards,
 term and trunc of every step are written to an HBM trajectory slab.  Steps are executed by
-the fused kernel k_step_many in launches of --chunk steps.
+the fused step kernel (k_step_pipe: two-wave pipelined, LDS tables) in launches of --chunk
+steps; the variant launched is reported in config.kernel.
 
 Multi-GPU (torchrun): one process per GPU, envs sharded by global id (rank * envs + e) with
 no data-path collective ("scaling": "weak"); the only collectives are the barrier and the
@@ -208,6 +209,7 @@ def main():
         return step0 + nsteps
 
     s0 = run(args.warmup, 0)
+    kernel_name = env.last_kernel()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -280,7 +282,8 @@ def main():
     workload = f"fjsp_step_{N}envs"
     pmc = load_pmc(workload)
     traffic = None
-    if pmc and pmc.get("steps_per_launch") == steps_per_launch and pmc.get("envs") == N:
+    if (pmc and pmc.get("steps_per_launch") == steps_per_launch and pmc.get("envs") == N
+            and pmc.get("kernel_variant") == kernel_name):
         traffic = pmc.get("hbm_bytes_per_launch")
     if rank == 0:
         out = {
@@ -298,12 +301,12 @@ def main():
             "data": "synthetic: random actions from the on-device counter RNG, envs seeded by global id",
             "config": {"workload": workload, "envs_per_gpu": N, "global_envs": N * world,
                        "num_orders": args.num_orders, "policy": "masked-random" if args.masked else "random",
-                       "steps_per_launch": steps_per_launch, "kernel": "k_step_many",
+                       "steps_per_launch": steps_per_launch, "kernel": kernel_name,
                        "parallelism": f"env-shard x{world} (no data-path collective)"},
             "agent_steps_per_s": value * 8,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_step_many", "avg_launch_ms": avg_launch_ms,
+                         "kernel": kernel_name, "avg_launch_ms": avg_launch_ms,
                          "algo_bytes_per_env_step": ALGO_BYTES_FUSED,
                          "env_steps_per_launch": N * steps_per_launch},
             "cpu_baseline": cpu,

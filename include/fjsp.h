@@ -227,6 +227,9 @@ int fjsp_restore(fjsp_handle* h, const void* src);
 /* Kernel timing of the last fjsp_step_many / fjsp_step launch in ms (hipEvents on the
  * handle's stream; synchronises). */
 int fjsp_last_kernel_ms(fjsp_handle* h, float* ms);
+/* Name of the kernel variant the last fjsp_step / fjsp_step_many launched ("" before any):
+ * e.g. "k_step_pipe<lds>" (rocprof shows it as k_step_pipe). */
+const char* fjsp_last_kernel(const fjsp_handle* h);
 
 #ifdef __cplusplus
 }

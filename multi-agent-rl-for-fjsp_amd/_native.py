@@ -62,7 +62,7 @@ EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_c
            "fjsp_create", "fjsp_destroy", "fjsp_set_stream", "fjsp_set_option", "fjsp_num_envs", "fjsp_state_bytes",
            "fjsp_reset", "fjsp_step", "fjsp_step_many", "fjsp_gae", "fjsp_gae_f64", "fjsp_mt_get", "fjsp_mt_set",
            "fjsp_read_env", "fjsp_sync", "fjsp_last_kernel_ms", "fjsp_pack_a2c", "fjsp_a2c_layout",
-           "fjsp_snapshot_bytes", "fjsp_snapshot", "fjsp_restore"]
+           "fjsp_snapshot_bytes", "fjsp_snapshot", "fjsp_restore", "fjsp_last_kernel"]
 ABI_VERSION = 2
 
 _lib = None
@@ -127,6 +127,7 @@ def lib():
         "fjsp_snapshot_bytes": (ctypes.c_int64, [P]),
         "fjsp_snapshot": (I, [P, P]),
         "fjsp_restore": (I, [P, P]),
+        "fjsp_last_kernel": (ctypes.c_char_p, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

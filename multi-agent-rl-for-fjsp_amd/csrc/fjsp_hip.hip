@@ -741,6 +741,7 @@ struct fjsp_handle {
     int use_staged;  // LDS-staged wide output stores (FJSP_STAGED env var / fjsp_set_option)
     int timing;      // hipEvent bracketing of step launches (off while graph-capturing)
     int use_pipe;    // two-wave pipelined k_step_many for lean outputs (FJSP_PIPE / fjsp_set_option)
+    const char* last_kernel;   // name of the last step kernel launched (fjsp_last_kernel)
 };
 
 static thread_local std::string g_err;
@@ -963,6 +964,7 @@ int fjsp_step(fjsp_handle* h, const uint8_t* actions, const uint8_t* agent_order
     DeviceGuard g(h->device);
     dim3 grid((h->n + BLOCK - 1) / BLOCK);
     if (h->timing) HIPCHK(hipEventRecord(h->ev0, h->stream));
+    h->last_kernel = canon ? "k_step<canon>" : "k_step<ordered>";
     if (canon)
         hipLaunchKernelGGL(k_step<true>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, packed, autoreset,
                            out ? *out : kNoOut);
@@ -1006,6 +1008,10 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
                         al16(o.status);
     // LDS tables (97.5 KB per 64-env workgroup) pay while every workgroup has a CU of its own
     const bool lds = h->use_lds < 0 ? h->n <= 256 * BLOCK : h->use_lds != 0;
+    h->last_kernel = (h->use_pipe && !full && !staged) ? (lds ? "k_step_pipe<lds>" : "k_step_pipe")
+                   : full ? (lds ? "k_step_many<lds,full>" : "k_step_many<full>")
+                   : staged ? (lds ? "k_step_many<lds,staged>" : "k_step_many<staged>")
+                   : (lds ? "k_step_many<lds>" : "k_step_many");
     if (h->use_pipe && !full && !staged) {
         if (lds)
             hipLaunchKernelGGL(k_step_pipe<true>, grid, dim3(2 * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed,
@@ -1099,6 +1105,10 @@ int fjsp_restore(fjsp_handle* h, const void* src) {
     HIPCHK(hipMemcpyAsync(h->base, src, h->bytes, hipMemcpyDefault, h->stream));
     h->has_reset = 1;
     return 0;
+}
+
+const char* fjsp_last_kernel(const fjsp_handle* h) {
+    return (h && h->last_kernel) ? h->last_kernel : "";
 }
 
 int fjsp_sync(fjsp_handle* h) {

@@ -203,6 +203,10 @@ class FJSPVecEnv:
             raise ValueError(f"snapshot of {snap.numel() * snap.element_size()} bytes, handle needs {nb}")
         nat.check(nat.lib().fjsp_restore(self._h, _ptr(snap.contiguous())))
 
+    def last_kernel(self):
+        """Name of the kernel variant of the last step launch (e.g. "k_step_pipe<lds>")."""
+        return nat.lib().fjsp_last_kernel(self._h).decode()
+
     def last_kernel_ms(self):
         ms = ctypes.c_float()
         nat.check(nat.lib().fjsp_last_kernel_ms(self._h, ctypes.byref(ms)))

@@ -21,7 +21,7 @@ def per_kernel(path, kernel, grid):
     vals = []
     with open(path) as f:
         for row in csv.DictReader(f):
-            if row["Kernel_Name"].startswith(kernel) and int(row["Grid_Size"]) == grid:
+            if row["Kernel_Name"].startswith(kernel) and int(row["Grid_Size"]) in (grid, 2 * grid):
                 vals.append(float(row["Counter_Value"]))
     return vals
 
@@ -32,7 +32,8 @@ def main():
     ap.add_argument("--src", default=os.path.join(REPO, "gpurun_out", "prof"))
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--steps-per-launch", type=int, default=200)
-    ap.add_argument("--kernel", default="k_step_many")
+    ap.add_argument("--kernel", default="k_step_pipe")
+    ap.add_argument("--variant", default="k_step_pipe<lds>", help="fjsp_last_kernel name of the profiled launch")
     ap.add_argument("--algo-bytes-per-env-step", type=int, default=211)
     a = ap.parse_args()
     dst = os.path.join(REPO, "profiles", a.round)
@@ -66,6 +67,7 @@ def main():
         "envs": a.envs,
         "steps_per_launch": a.steps_per_launch,
         "kernel": a.kernel,
+        "kernel_variant": a.variant,
         "launches": len(fetch),
         "FETCH_SIZE_kB_per_launch": fk,
         "WRITE_SIZE_kB_per_launch": wk,
