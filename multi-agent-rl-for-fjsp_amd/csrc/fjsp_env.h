@@ -38,12 +38,20 @@ enum : int { L_PREADY = 0, L_STORAGE = 1, L_M0Q = 2, L_M0R = 3, L_M1Q = 4, L_M1R
 
 // locations (enums/LocationType.py values) and coordinates (constants.py:5-11)
 enum : int { LOC_PICKUP = 1, LOC_BIG = 2, LOC_SMALL = 3, LOC_STORAGE = 4, LOC_PACK = 5 };
-FJSP_DEV int loc_row(int l) { return (l == LOC_SMALL) ? 2 : (l >= LOC_STORAGE ? 3 : 0); }
-FJSP_DEV int loc_col(int l) { return (l == LOC_PICKUP || l == LOC_STORAGE) ? 0 : (l == LOC_PACK ? 5 : 3); }
-// AGV move action a (1..5) -> location (AGVAgent.py:218-224)
-FJSP_DEV int move_loc(int a) {
-    return a == 1 ? LOC_PICKUP : a == 2 ? LOC_SMALL : a == 3 ? LOC_BIG : a == 4 ? LOC_STORAGE : LOC_PACK;
+// Small integer maps are 4-bit fields of a constant word (nib): a chain of `x == k ? ...`
+// on one variable is turned into a switch by the compiler, i.e. branches on a wavefront.
+constexpr uint32_t nibs(int a0, int a1, int a2, int a3, int a4, int a5, int a6 = 0, int a7 = 0) {
+    return (uint32_t)a0 | ((uint32_t)a1 << 4) | ((uint32_t)a2 << 8) | ((uint32_t)a3 << 12) | ((uint32_t)a4 << 16) |
+           ((uint32_t)a5 << 20) | ((uint32_t)a6 << 24) | ((uint32_t)a7 << 28);
 }
+FJSP_DEV int nib(uint32_t table, int i) { return (int)((table >> (4 * i)) & 0xFu); }
+constexpr uint32_t ROW_TAB = nibs(0, 0, 0, 2, 3, 3);   // location -> grid row
+constexpr uint32_t COL_TAB = nibs(0, 0, 3, 3, 0, 5);   // location -> grid column
+FJSP_DEV int loc_row(int l) { return nib(ROW_TAB, l); }
+FJSP_DEV int loc_col(int l) { return nib(COL_TAB, l); }
+// AGV move action a (1..5) -> location (AGVAgent.py:218-224)
+constexpr uint32_t MOVE_TAB = nibs(0, LOC_PICKUP, LOC_SMALL, LOC_BIG, LOC_STORAGE, LOC_PACK);
+FJSP_DEV int move_loc(int a) { return nib(MOVE_TAB, a & 7); }
 FJSP_DEV int iabs(int x) { return x < 0 ? -x : x; }
 FJSP_DEV int manhattan(int a, int b) {
     return iabs(loc_row(a) - loc_row(b)) + iabs(loc_col(a) - loc_col(b));
@@ -401,10 +409,11 @@ FJSP_DEV uint32_t pickup_execute(Env& E, const Tables& T, const Cfg& C, int acti
 // blue_1, blue_2, red, green) whose colour matches and whose Resource has capacity; -1 = none
 // (the products are lost).  PackagingColor RED=1 BLUE=2 GREEN=3.
 FJSP_DEV int pkg_station(const Env& E, const Cfg& C, int color) {
-    return (color == 2 && E.p_inflight(0) < C.pkg_cap) ? 0
-         : (color == 2 && E.p_inflight(1) < C.pkg_cap) ? 1
-         : (color == 1 && E.p_inflight(2) < C.pkg_cap) ? 2
-         : (color == 3 && E.p_inflight(3) < C.pkg_cap) ? 3 : -1;
+    const uint32_t room = (uint32_t)(E.p_inflight(0) < C.pkg_cap) | ((uint32_t)(E.p_inflight(1) < C.pkg_cap) << 1) |
+                          ((uint32_t)(E.p_inflight(2) < C.pkg_cap) << 2) | ((uint32_t)(E.p_inflight(3) < C.pkg_cap) << 3);
+    // stations of each colour: RED -> {red}, BLUE -> {blue_1, blue_2}, GREEN -> {green}
+    const uint32_t cand = (uint32_t)nib(nibs(0, 0x4, 0x3, 0x8, 0, 0), color & 3) & room;
+    return __builtin_ffs((int)cand) - 1;   // first in dict order; -1 = none
 }
 
 constexpr uint32_t PICK_LISTS = (1u << L_PREADY) | (1u << L_STORAGE) | (1u << L_M0R) | (1u << L_M1R);
@@ -421,25 +430,27 @@ FJSP_DEV uint32_t agv_execute(Env& E, const Tables& T, const Cfg& C, int action,
     const int carry = E.carry();
     const bool has = carry != NIL;
     // 1..5: moves (AGVAgent.py:218-252); distance 0 is a successful no-op
-    const bool is_move = action >= 1 && action <= 5;
+    const bool is_move = (unsigned)(action - 1) < 5u;
     const int ml = move_loc(action);
     const int d = manhattan(loc, ml);
     const bool moved = is_move && d != 0;
     // 6: PICKUP, FIFO front of the list at this location (_execute_pickup :254-293)
-    const int src = loc == LOC_PICKUP ? L_PREADY : loc == LOC_SMALL ? L_M0R : loc == LOC_BIG ? L_M1R : L_STORAGE;
+    const int src = nib(nibs(0, L_PREADY, L_M1R, L_M0R, L_STORAGE, L_STORAGE), loc);
     const uint32_t lws = lword<PICK_LISTS>(E, src);
     const bool ok6 = action == 6 && !has && loc != LOC_PACK && (lws >> 16) != 0;
-    // 7: DROP (_execute_drop :295-368)
+    // 7: DROP (_execute_drop :295-368): validity per location as one bit vector indexed by loc
     const int code = E.carry_code(), ty = E.carry_type(), np = E.carry_np(), nk = E.carry_nk();
-    const bool at_pick = loc == LOC_PICKUP, at_small = loc == LOC_SMALL, at_big = loc == LOC_BIG;
-    const bool at_store = loc == LOC_STORAGE, at_pack = loc == LOC_PACK;
-    const bool valid7 = (at_pick && tc_count(code) == 0) || (at_small && np && (ty == 1 || ty == 2)) ||
-                        (at_big && np && (ty == 3 || ty == 2)) || at_store || (at_pack && nk && !np);
-    const bool ok7 = action == 7 && has && valid7;
+    const uint32_t cond = ((uint32_t)(tc_count(code) == 0) << LOC_PICKUP) |
+                          ((uint32_t)(np && (ty == 1 || ty == 2)) << LOC_SMALL) |
+                          ((uint32_t)(np && (ty == 3 || ty == 2)) << LOC_BIG) | (1u << LOC_STORAGE) |
+                          ((uint32_t)(nk && !np) << LOC_PACK);
+    const bool ok7 = action == 7 && has && ((cond >> loc) & 1u);
+    const bool at_pick = loc == LOC_PICKUP, at_store = loc == LOC_STORAGE, at_pack = loc == LOC_PACK;
     const bool store_full = E.ll(L_STORAGE) >= C.storage_cap;
     const int st = pkg_station(E, C, E.carry_color());
-    const int dst = at_small ? L_M0Q : at_big ? L_M1Q : at_store ? (store_full ? -1 : L_STORAGE)
-                  : at_pack ? (st >= 0 ? L_PKG + st : -1) : -1;
+    const int base = nib(nibs(0xF, 0xF, L_M1Q, L_M0Q, L_STORAGE, L_PKG), loc);
+    const bool no_dst = base == 0xF || (at_store && store_full) || (at_pack && st < 0);
+    const int dst = no_dst ? -1 : base + (at_pack ? st : 0);
     // memory: pop (loads) / push (stores)
     uint32_t next = 0, scode = 0, ow = 0;
     const int ps = (int)(lws & 0xFFu);
@@ -505,23 +516,21 @@ template <int M>
 FJSP_DEV uint32_t machine_execute(Env& E, const Tables& T, int action, int* start_slot) {
     constexpr int LQ = M == 0 ? L_M0Q : L_M1Q;
     constexpr int LR = M == 0 ? L_M0R : L_M1R;
-    uint32_t r = R_EXEC;   // 1 success, 2 started, 4 completed, 8 idle_with_queue
-    const int idle_q = E.ll(LQ) > 0 && !E.m_busy(M);
-    if (action == 0) {
-        r |= 1u | (idle_q ? 8u : 0u);
-    } else if (action == 1) {
-        if (idle_q) {
-            *start_slot = list_pop<LQ>(E, T);
-            r |= 2u | 1u;
-        }
-    } else if (action == 2) {
-        const int cur = E.m_cur(M);
-        if (!E.m_busy(M) && cur != NIL) {
-            list_push<LR>(E, T, cur);
-            E.set_m_cur(M, NIL);
-            r |= 4u | 1u;
-        }
+    const bool busy = E.m_busy(M);
+    const bool idle_q = E.ll(LQ) > 0 && !busy;
+    const int cur = E.m_cur(M);
+    const bool go = action == 1 && idle_q;            // START: pop the queue front
+    const bool sig = action == 2 && !busy && cur != NIL;   // SIGNAL: current tray -> ready_trays
+    if (go) *start_slot = list_pop<LQ>(E, T);
+    if (sig) {
+        list_push<LR>(E, T, cur);
+        E.set_m_cur(M, NIL);
     }
+    // 1 success, 2 started, 4 completed, 8 idle_with_queue
+    uint32_t r = R_EXEC;
+    r |= action == 0 ? (1u | (idle_q ? 8u : 0u)) : 0u;
+    r |= go ? 3u : 0u;
+    r |= sig ? 5u : 0u;
     return r;
 }
 
@@ -545,32 +554,58 @@ FJSP_DEV uint32_t pack_execute(Env& E, const Cfg& C, int action, int* started) {
 }
 
 // ---------------------------------------------------------------- run phase (T, T+step]
-// Machine: completion due this step (old NORMAL event) else grant of a START.
+// Machines: a product completion due this step (old NORMAL event), then the grant of this
+// step's START (MachineAgent.py:151-169).  Both machines' memory reads (the completing
+// product's order word, the granted tray's code) are issued together; two completions of
+// the same order update its word once.
 template <int M>
-FJSP_DEV void machine_run(Env& E, const Tables& T, const Cfg& C, int start_slot) {
-    const int ptk = M == 0 ? C.ptk_small : C.ptk_big;
+FJSP_DEV void machine_done(Env& E, const Cfg& C, int step) {
+    const int k = E.m_k(M);
+    E.set_m_k(M, k + 1);
+    if (k + 1 >= tc_count(E.m_code(M))) { E.set_m_busy(M, 0); E.set_m_prog(M, 1); }
+    else E.set_m_next(M, step + (M == 0 ? C.ptk_small : C.ptk_big));
+}
+template <int M>
+FJSP_DEV void machine_grant(Env& E, const Cfg& C, int slot, int code, int step) {
+    if (E.m_cur(M) != NIL) E.flag(ST_OVERWRITE);
+    const int busy = tc_count(code) > 0;   // an empty tray's loop body never runs
+    E.set_m_grant(M, slot, code, busy);
+    if (busy) E.set_m_next(M, step + (M == 0 ? C.ptk_small : C.ptk_big));
+    else E.set_m_prog(M, 1);
+}
+FJSP_DEV void machines_run(Env& E, const Tables& T, const Cfg& C, int s0, int s1) {
     const int step = E.step();
-    if (E.m_busy(M) && E.m_next(M) == step) {
-        const int code = E.m_code(M);
-        const int k = E.m_k(M);
-        T.orders[tc_order(code) * T.stride] |= 1u << (tc_start(code) + k);   // product.is_processed = True
-        E.set_m_k(M, k + 1);
-        if (k + 1 >= tc_count(code)) { E.set_m_busy(M, 0); E.set_m_prog(M, 1); }
-        else E.set_m_next(M, step + ptk);
-    }
-    if (start_slot >= 0) {   // grant at T: is_busy, current_tray := tray (MachineAgent.py:159-160)
-        if (E.m_cur(M) != NIL) E.flag(ST_OVERWRITE);
-        const int code = T.scode[start_slot * T.stride];
-        const int busy = tc_count(code) > 0;   // an empty tray's loop body never runs
-        E.set_m_grant(M, start_slot, code, busy);
-        if (busy) E.set_m_next(M, step + ptk);
-        else E.set_m_prog(M, 1);
-    }
+    const bool due0 = E.m_busy(0) && E.m_next(0) == step, due1 = E.m_busy(1) && E.m_next(1) == step;
+    const int c0 = E.m_code(0), c1 = E.m_code(1);
+    const int o0 = tc_order(c0), o1 = tc_order(c1);
+    // independent loads (addresses clamped to valid entries when unused)
+    const uint32_t w0 = T.orders[(due0 ? o0 : 0) * T.stride];
+    const uint32_t w1 = T.orders[(due1 ? o1 : 0) * T.stride];
+    const int g0 = T.scode[(s0 >= 0 ? s0 : 0) * T.stride];
+    const int g1 = T.scode[(s1 >= 0 ? s1 : 0) * T.stride];
+    const uint32_t b0 = 1u << (tc_start(c0) + E.m_k(0)), b1 = 1u << (tc_start(c1) + E.m_k(1));
+    // product.is_processed = True
+    if (due0) T.orders[o0 * T.stride] = w0 | b0;
+    if (due1) T.orders[o1 * T.stride] = ((due0 && o0 == o1) ? (w0 | b0) : w1) | b1;
+    if (due0) machine_done<0>(E, C, step);
+    if (s0 >= 0) machine_grant<0>(E, C, s0, g0, step);
+    if (due1) machine_done<1>(E, C, step);
+    if (s1 >= 0) machine_grant<1>(E, C, s1, g1, step);
 }
 
 // Packaging: completions of the batch due this step, then grants of this step's START.
+// `due` = the in-flight head run completes now (pack_due: the four stations' head checks are
+// issued as one batch of independent loads).
 template <int S>
-FJSP_DEV void pack_run(Env& E, const Tables& T, const Cfg& C, int started, int* orders_done) {
+FJSP_DEV bool pack_due(const Env& E, const Tables& T, int step) {
+    constexpr int L = L_PKG + S;
+    const int h = E.lh(L);
+    const bool inflight = E.ll(L) > 0 && h != E.p_qfirst(S);
+    const uint16_t cs = T.scstep[(inflight ? h : 0) * T.stride];   // slot 0 always exists
+    return inflight && cs == (uint16_t)step;
+}
+template <int S>
+FJSP_DEV void pack_run(Env& E, const Tables& T, const Cfg& C, int started, bool due, int* orders_done) {
     constexpr int L = L_PKG + S;
     const int step = E.step();
     const int qfirst = E.p_qfirst(S);
@@ -578,7 +613,7 @@ FJSP_DEV void pack_run(Env& E, const Tables& T, const Cfg& C, int started, int* 
         E.flag(ST_PKG_WAIT | ST_DIVERGED);   // Request would wait (users == capacity)
     // completions (PackagingAgent.py:143-147)
     int done = 0;
-    while (E.ll(L) > 0 && E.lh(L) != qfirst && T.scstep[E.lh(L) * T.stride] == (uint16_t)step) {
+    while (due) {
         const int s = list_pop<L>(E, T);
         const int code = T.scode[s * T.stride];
         const int o = tc_order(code);
@@ -590,6 +625,7 @@ FJSP_DEV void pack_run(Env& E, const Tables& T, const Cfg& C, int started, int* 
         }
         T.orders[o * T.stride] = w;
         done += tc_count(code);
+        due = E.ll(L) > 0 && E.lh(L) != qfirst && T.scstep[E.lh(L) * T.stride] == (uint16_t)step;
     }
     if (done) {
         E.set_p_completed(S, E.p_completed(S) + done);
@@ -858,13 +894,15 @@ FJSP_DEV double env_advance(Env& E, const Tables& T, const Cfg& C, const int* ac
     FJSP_STAMP(E, 1);
     // 2. env.run(until=now+step_size) in closed form
     if (move_to) E.set_loc(move_to);
-    machine_run<0>(E, T, C, m_start[0]);
-    machine_run<1>(E, T, C, m_start[1]);
+    machines_run(E, T, C, m_start[0], m_start[1]);
     int orders_done = 0;
-    pack_run<0>(E, T, C, p_started[0], &orders_done);
-    pack_run<1>(E, T, C, p_started[1], &orders_done);
-    pack_run<2>(E, T, C, p_started[2], &orders_done);
-    pack_run<3>(E, T, C, p_started[3], &orders_done);
+    const int step = E.step();
+    const bool due0 = pack_due<0>(E, T, step), due1 = pack_due<1>(E, T, step);
+    const bool due2 = pack_due<2>(E, T, step), due3 = pack_due<3>(E, T, step);
+    pack_run<0>(E, T, C, p_started[0], due0, &orders_done);
+    pack_run<1>(E, T, C, p_started[1], due1, &orders_done);
+    pack_run<2>(E, T, C, p_started[2], due2, &orders_done);
+    pack_run<3>(E, T, C, p_started[3], due3, &orders_done);
     E.set_ncompleted(E.ncompleted() + orders_done);
     FJSP_STAMP(E, 2);
     // 3. calculate_global_reward; combine_rewards divides it by len(self.agents)
