@@ -80,9 +80,9 @@ enum : int { W_ORDER = 0, W_THROUGHPUT, W_TIME, W_PICK_LOAD, W_PICK_TRAY, W_PICK
 // Reward lookup table (device memory): the local reward of every (agent kind, result bits,
 // action == 0) combination, each summed from 0.0 in calculate_local_reward's order on the host,
 // plus the global-reward weights.  Layout: [0,16) pickup, [16,48) AGV, [48,64) machine,
-// [64,80) packaging, [80] ORDER, [81] THROUGHPUT, [82] TIME * step_size, [96,160) progress.
-// [96, 160): (1.0 / n) * 100.0 for n < 64 (PackagingAgent START progress, in fp64).
-constexpr int RPROG = 96, RPROG_N = 64;
+// [64,80) packaging, [80] ORDER, [81] THROUGHPUT, [82] TIME * step_size, [96,352) progress.
+// [96, 352): (1.0 / n) * 100.0 for n < 256 (PackagingAgent START progress, in fp64).
+constexpr int RPROG = 96, RPROG_N = 256;
 constexpr int RLUT_SIZE = RPROG + RPROG_N;
 
 struct Cfg {
@@ -176,7 +176,7 @@ constexpr int NWORDS = 40;   // rows of the HBM state buffer (30 used)
 //   W7+l   list l: head[0,8) tail[8,16) len[16,32)
 //   W17+m  machine m: busy[0] cur[1,9) code[9,22) prog[22] k[23,27)     W19 next[0]|next[1] << 16
 //   W20+s  packaging s: busy[0] hascur[1] qfirst[2,10) inflight[10,18) queued[18,32)
-//   W24/25 completed[0..3] (16 bits each)                               W26+s progress (f32 bits)
+//   W24/25 completed[0..3] (16 bits each)                W26+s queue length at the last START
 constexpr int NSTATE = 30;
 
 struct Env {
@@ -275,8 +275,9 @@ struct Env {
     FJSP_DEV void set_p_queued(int s, int v) { sbf(20 + s, 18, 14, v); }
     FJSP_DEV int p_completed(int s) const { return bf(24 + (s >> 1), 16 * (s & 1), 16); }
     FJSP_DEV void set_p_completed(int s, int v) { sbf(24 + (s >> 1), 16 * (s & 1), 16, v); }
-    FJSP_DEV float p_prog(int s) const { return __uint_as_float_fjsp(w[26 + s]); }
-    FJSP_DEV void set_p_prog(int s, float v) { w[26 + s] = __float_as_uint_fjsp(v); }
+    // queue length at the last START (0 = never started); the float progress of the observation
+    // is derived from it (pack_progress), so the step itself never computes it
+    FJSP_DEV int p_startn(int s) const { return (int)w[26 + s]; }
 };
 
 // ---- table accessors: element i of a per-env table = base[i * stride]
@@ -416,6 +417,7 @@ FJSP_DEV int pkg_station(const Env& E, const Cfg& C, int color) {
     return __builtin_ffs((int)cand) - 1;   // first in dict order; -1 = none
 }
 
+constexpr uint16_t PKG_CONT = 0xFFFF;   // scstep of a run that is not the first of its batch
 constexpr uint32_t PICK_LISTS = (1u << L_PREADY) | (1u << L_STORAGE) | (1u << L_M0R) | (1u << L_M1R);
 constexpr uint32_t DROP_LISTS = (1u << L_STORAGE) | (1u << L_M0Q) | (1u << L_M1Q) | (0xFu << L_PKG);
 
@@ -463,6 +465,7 @@ FJSP_DEV uint32_t agv_execute(Env& E, const Tables& T, const Cfg& C, int action,
     const uint32_t lwd = lword<DROP_LISTS>(E, dst);
     if (push) {
         T.snext[carry * T.stride] = (uint8_t)NIL;
+        if (at_pack) T.scstep[carry * T.stride] = PKG_CONT;
         if ((lwd >> 16) != 0) T.snext[((lwd >> 8) & 0xFFu) * T.stride] = (uint8_t)carry;
     }
     // list words
@@ -536,14 +539,11 @@ FJSP_DEV uint32_t machine_execute(Env& E, const Tables& T, int action, int* star
 
 // PackagingAgent.execute_action (PackagingAgent.py:301-335)
 template <int S>
-FJSP_DEV uint32_t pack_execute(Env& E, const Cfg& C, int action, int* started) {
+FJSP_DEV uint32_t pack_execute(Env& E, int action, int* started) {
     const int n = E.p_queued(S);
     const bool busy = E.p_busy(S);
     const bool go = action == 1 && n > 0;
-    // self.processing_progress = (i / len(self.product_queue)) * 100 with i == 1, in fp64 then
-    // float32 (tabulated for n < 64 in the LDS reward table; exact either way)
-    const double pd = n < RPROG_N ? C.lut[RPROG + n] : (1.0 / (double)n) * 100.0;
-    E.w[26 + S] = go ? __float_as_uint_fjsp((float)pd) : E.w[26 + S];
+    E.w[26 + S] = go ? (uint32_t)n : E.w[26 + S];   // progress = pack_progress(n), see observe
     *started = go ? 1 : *started;
     // 1 success, 2 started, 4 completed, 8 idle_with_queue; 16.. completed count
     uint32_t r = R_EXEC;
@@ -594,6 +594,10 @@ FJSP_DEV void machines_run(Env& E, const Tables& T, const Cfg& C, int s0, int s1
 }
 
 // Packaging: completions of the batch due this step, then grants of this step's START.
+// A batch (every run queued at one START) is a contiguous stretch of the station's list: its
+// first run's scstep holds the completion step, the other runs PKG_CONT (written when the AGV
+// drops them), so a START is one store and a completion pops runs until the next batch start
+// or the first ungranted run (qfirst).
 // `due` = the in-flight head run completes now (pack_due: the four stations' head checks are
 // issued as one batch of independent loads).
 template <int S>
@@ -625,7 +629,8 @@ FJSP_DEV void pack_run(Env& E, const Tables& T, const Cfg& C, int started, bool 
         }
         T.orders[o * T.stride] = w;
         done += tc_count(code);
-        due = E.ll(L) > 0 && E.lh(L) != qfirst && T.scstep[E.lh(L) * T.stride] == (uint16_t)step;
+        // the batch continues while the next run is granted (not qfirst) and not a batch start
+        due = E.ll(L) > 0 && E.lh(L) != qfirst && T.scstep[E.lh(L) * T.stride] == PKG_CONT;
     }
     if (done) {
         E.set_p_completed(S, E.p_completed(S) + done);
@@ -634,9 +639,8 @@ FJSP_DEV void pack_run(Env& E, const Tables& T, const Cfg& C, int started, bool 
         E.set_p_busy(S, 0);
     }
     // grants: every queued product, in queue order (PackagingAgent.py:136-141)
-    if (started) {
-        const uint16_t cs = (uint16_t)(step + C.ptk_pack);
-        for (int s = qfirst; s != NIL; s = T.snext[s * T.stride]) T.scstep[s * T.stride] = cs;
+    if (started) {   // the whole queue [qfirst, tail] is one batch: mark its first run
+        T.scstep[qfirst * T.stride] = (uint16_t)(step + C.ptk_pack);
         const int inflight = E.p_inflight(S) + E.p_queued(S);
         // busy = 1, hascur = 1, qfirst = NIL, inflight += queued, queued = 0
         E.w[20 + S] = 3u | ((uint32_t)NIL << 2) | ((uint32_t)(inflight & 0xFF) << 10);
@@ -717,6 +721,13 @@ FJSP_DEV void compute_masks(const Env& E, const Cfg& C, Sink& m) {
     }
 }
 
+// PackagingAgent START: self.processing_progress = (i / len(self.product_queue)) * 100 with
+// i == 1, in fp64 then float32 (tabulated for n < 256 in the reward table; exact either way).
+FJSP_DEV float pack_progress(const Cfg& C, int n) {
+    if (__builtin_expect(n >= RPROG_N, 0)) return (float)((1.0 / (double)n) * 100.0);   // n > packaging_capacity
+    return (float)C.lut[RPROG + n];   // lut[RPROG] = 0.0: never started
+}
+
 FJSP_DEV int obs_i8_checked(Env& E, int v) {
     if (v > 127) E.flag(ST_OBS_OVERFLOW | ST_DIVERGED);
     return (int)(int8_t)v;
@@ -761,7 +772,7 @@ FJSP_DEV void observe(Env& E, const Cfg& C, Sink& o) {
     for (int s = 0; s < 4; s++) {
         o.i8(4 + 2 * s, E.p_busy(s));
         o.i8(5 + 2 * s, obs_i8_checked(E, E.p_queued(s)));
-        o.f32(2 + s, E.p_prog(s));
+        o.f32(2 + s, pack_progress(C, E.p_startn(s)));
     }
     compute_masks(E, C, o);
 }
@@ -882,10 +893,10 @@ FJSP_DEV double env_advance(Env& E, const Tables& T, const Cfg& C, const int* ac
             case 1: r = agv_execute(E, T, C, ac, &move_to); break;
             case 2: r = machine_execute<0>(E, T, ac, &m_start[0]); break;
             case 3: r = machine_execute<1>(E, T, ac, &m_start[1]); break;
-            case 4: r = pack_execute<0>(E, C, ac, &p_started[0]); break;
-            case 5: r = pack_execute<1>(E, C, ac, &p_started[1]); break;
-            case 6: r = pack_execute<2>(E, C, ac, &p_started[2]); break;
-            default: r = pack_execute<3>(E, C, ac, &p_started[3]); break;
+            case 4: r = pack_execute<0>(E, ac, &p_started[0]); break;
+            case 5: r = pack_execute<1>(E, ac, &p_started[1]); break;
+            case 6: r = pack_execute<2>(E, ac, &p_started[2]); break;
+            default: r = pack_execute<3>(E, ac, &p_started[3]); break;
             }
         }
         res[a] = r;

@@ -544,6 +544,10 @@ __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, u
 // computes step k+1, and precomputes the next step's actions when they do not depend on the
 // state (uniform random mode).  Snapshots and action slots are double-buffered; one
 // workgroup barrier per step orders them.
+// State words the observation / masks / term / trunc / status read (observe, compute_masks):
+// all but the MT cursor (W3), the packaging run lists (W13-16), the machines' next-event steps
+// (W19) and the packaging completion counters (W24-25).
+constexpr uint32_t SNAP_WORDS = ((1u << NSTATE) - 1u) & ~((1u << 3) | (0xFu << 13) | (1u << 19) | (3u << 24));
 struct alignas(16) PipeSnap {
     double g8[BLOCK];
     uint32_t w[NSTATE][BLOCK];
@@ -619,7 +623,8 @@ __global__ void __launch_bounds__(2 * BLOCK) k_step_pipe(DevState S, Cfg C, int 
                 PipeSnap& sp = snap[k & 1];
                 sp.g8[lane] = g8;
 #pragma unroll
-                for (int i = 0; i < NSTATE; i++) sp.w[i][lane] = E.w[i];
+                for (int i = 0; i < NSTATE; i++)
+                    if ((SNAP_WORDS >> i) & 1u) sp.w[i][lane] = E.w[i];
                 uint32_t r0 = 0, r1 = 0;
 #pragma unroll
                 for (int a = 0; a < 4; a++) {
@@ -661,7 +666,7 @@ __global__ void __launch_bounds__(2 * BLOCK) k_step_pipe(DevState S, Cfg C, int 
                 const PipeSnap& sp = snap[(k - 1) & 1];
                 Env E;
 #pragma unroll
-                for (int i = 0; i < NSTATE; i++) E.w[i] = sp.w[i][lane];
+                for (int i = 0; i < NSTATE; i++) E.w[i] = ((SNAP_WORDS >> i) & 1u) ? sp.w[i][lane] : 0u;
                 const double g8 = sp.g8[lane];
                 if (out.rewards) {
                     const uint32_t r0 = sp.ridx[0][lane], r1 = sp.ridx[1][lane];
