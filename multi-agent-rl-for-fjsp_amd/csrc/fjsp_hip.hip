@@ -6,7 +6,7 @@
 //   scode  u16 [255][N]           tray-slot arena: tray code
 //   snext  u8  [255][N]           tray-slot arena: next slot of the FIFO the slot is in
 //   scstep u16 [255][N]           tray-slot arena: completion step of an in-flight run
-//   mt     u32 [624][N]           per-env MT19937 state (numpy legacy RandomState)
+//   mt     u32 [N][624]           per-env MT19937 state (numpy legacy RandomState), env-major
 // Kernels: one lane per env, 64-lane workgroups (one wavefront; 4096 envs -> 64 CUs).
 //   k_reset      FJSPSimulation.reset (FJSPSimulation.py:286-323)
 //   k_step       FJSPSimulation.step  (FJSPSimulation.py:144-242), actions from HBM
@@ -57,108 +57,85 @@ __device__ __forceinline__ void env_store(const Env& E, uint32_t* __restrict__ w
 static_assert(NWORDS >= NSTATE, "state buffer rows");
 
 // ---------------------------------------------------------------- MT19937, lazily twisted
-// State word: mti (bits 0..9) | g (bits 16..25).  Words [0, g) of the array already hold the
+// Per-env state: 624 words, env-major (row e = mt + e * 624, 16-byte aligned), so the words a
+// lane streams through are contiguous for that lane (lanes of a wave sit at different stream
+// positions: a word-major layout would make every load touch 64 rows).
+// Cursor word W3: mti (bits 0..9) | g (bits 16..25).  Words [0, g) of the row already hold the
 // current block, [g, 624) still the previous one; mti <= g is the next word to consume.
-// Word i of a new block is generated on demand with the same in-place recurrence as
-// numpy's sequential twist (mt[i+1] is still old, mt[i+397 mod 624] is new iff i >= 227),
-// so the k-th draw equals numpy's k-th draw while touching 3 words instead of 624.
+// Word i of a new block is generated on demand with the same in-place recurrence as numpy's
+// sequential twist (mt[i+1] is still old, mt[i+397 mod 624] is new iff i >= 227), so the k-th
+// draw equals numpy's k-th draw.
 // Standard numpy (key, pos): pos == 624 <-> (mti, g) = (0, 0); pos < 624 <-> (pos, 624).
-__device__ __forceinline__ uint32_t mt_draw(uint32_t* __restrict__ mt, int n, int e, int& st) {
-    int i = st & 0x3FF, g = (st >> 16) & 0x3FF;
-    uint32_t v;
-    if (i < g) {
-        v = mt[i * n + e];
-    } else {
-        const int i1 = (i + 1 == MT_N) ? 0 : i + 1;
-        const int im = (i + 397 >= MT_N) ? i + 397 - MT_N : i + 397;
-        const uint32_t a = mt[i * n + e], b = mt[i1 * n + e], c = mt[im * n + e];
-        const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
-        v = c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-        mt[i * n + e] = v;
-        g = i + 1;
-    }
-    i += 1;
-    if (i == MT_N) { i = 0; g = 0; }
-    st = i | (g << 16);
-    uint32_t t = v;
-    t ^= t >> 11;
-    t ^= (t << 7) & 0x9d2c5680u;
-    t ^= (t << 15) & 0xefc60000u;
-    t ^= t >> 18;
-    return t;
-}
-// numpy masked-rejection bounded draw (rng <= 0xFFFFFFFF, use_masked=True)
-__device__ __forceinline__ int mt_bounded(uint32_t* mt, int n, int e, int& st, uint32_t rng, uint32_t mask) {
-    uint32_t v;
-    do { v = mt_draw(mt, n, e, st) & mask; } while (v > rng);
-    return (int)v;
-}
-
-__device__ void mt_seed(uint32_t* __restrict__ mt, int n, int e, uint32_t seed) {
+__device__ void mt_seed(uint32_t* __restrict__ mt, int e, uint32_t seed) {
+    uint4* row = reinterpret_cast<uint4*>(mt + (size_t)e * MT_N);
     uint32_t x = seed;
-    mt[e] = x;
-    for (int i = 1; i < MT_N; i++) {
-        x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
-        mt[i * n + e] = x;
+    for (int q = 0; q < MT_N / 4; q++) {
+        uint32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int i = 4 * q + j;
+            if (i > 0) x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
+            v[j] = x;
+        }
+        row[q] = make_uint4(v[0], v[1], v[2], v[3]);
     }
 }
 
-// Batched reader of the lazily twisted MT19937 stream for resets.  A refill issues every load
-// of up to MTB words at once (mt[i..i+MTB] and mt[i+397..]) and waits once, instead of one
-// dependent round trip per draw: inside the step kernels every wait also drains the lane's
-// outstanding output stores.  Regenerated words are stored back (same in-place recurrence as
-// mt_draw); tempered outputs are staged in a per-lane LDS buffer `buf` (stride BLOCK).
-// Consumption (the rejection loops, divergent across lanes) only reads LDS; refills happen at
-// one wave-uniform point, so the lanes of a wave share each memory round trip.
+// Batched reader of the lazily twisted stream for resets.  A refill starts at the 16-byte
+// aligned word pa = pos & ~3 and loads the words it needs as two runs of nine uint4 (words
+// [pa, pa+36) and [pa+396, pa+432), wrapped into the row; 624 is a multiple of 4 so no uint4
+// straddles the wrap), regenerates and tempers MTB words into the lane's LDS buffer `buf`
+// (stride BLOCK) and writes the regenerated words back; the pos - pa words already consumed
+// are skipped (bi starts at pos - pa).  Consumption (the rejection loops, divergent across
+// lanes) only reads LDS; refills happen at one wave-uniform point.
 constexpr int MTB = 32;
 struct MtReader {
     uint32_t* mt;
     uint32_t* buf;   // LDS, element j at buf[j * BLOCK]
     int n, e;
     int pos, g;      // next word to consume, regenerated prefix of the current block
-    int bi, bcnt;    // consumption index / size of the staged batch
+    int bi, bcnt;    // consumption index / end of the staged batch
 
-    // Branch-free: every load is issued unconditionally (indices wrapped into the block) so
-    // the 2*MTB + 1 loads leave back to back and the lane waits once; stores are predicated.
     __device__ __forceinline__ void fill() {
-        const int cnt = (MT_N - pos) < MTB ? (MT_N - pos) : MTB;
-        uint32_t a[MTB + 1], c[MTB];
+        const uint4* row = reinterpret_cast<const uint4*>(mt + (size_t)e * MT_N);
+        uint32_t* roww = mt + (size_t)e * MT_N;
+        const int pa = pos & ~3;
+        const int cnt = (MT_N - pa) < MTB ? (MT_N - pa) : MTB;
+        uint32_t a[MTB + 4], c[MTB + 4];
 #pragma unroll
-        for (int j = 0; j <= MTB; j++) {
-            int idx = pos + j;
-            idx = idx >= MT_N ? idx - MT_N : idx;   // j == cnt at the block end reads mt[0] (new word 0)
-            a[j] = mt[idx * n + e];
+        for (int q = 0; q < (MTB + 4) / 4; q++) {
+            int ia = pa + 4 * q;
+            ia = ia >= MT_N ? ia - MT_N : ia;
+            int ic = pa + 396 + 4 * q;
+            ic = ic >= MT_N ? ic - MT_N : ic;
+            ic = ic >= MT_N ? ic - MT_N : ic;
+            const uint4 va = row[ia >> 2], vc = row[ic >> 2];
+            a[4 * q] = va.x; a[4 * q + 1] = va.y; a[4 * q + 2] = va.z; a[4 * q + 3] = va.w;
+            c[4 * q] = vc.x; c[4 * q + 1] = vc.y; c[4 * q + 2] = vc.z; c[4 * q + 3] = vc.w;
         }
 #pragma unroll
         for (int j = 0; j < MTB; j++) {
-            int im = pos + j + 397;
-            im = im >= MT_N ? im - MT_N : im;
-            c[j] = mt[im * n + e];
-        }
-#pragma unroll
-        for (int j = 0; j < MTB; j++) {
-            const int idx = pos + j;
-            const uint32_t y = (a[j] & 0x80000000u) | (a[j + 1] & 0x7fffffffu);
-            const uint32_t regen = c[j] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+            const int idx = pa + j;
+            const uint32_t y = (a[j] & 0x80000000u) | (a[j + 1] & 0x7fffffffu);   // a[cnt] = word 0 at the wrap
+            const uint32_t regen = c[j + 1] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);   // word idx + 397
             const bool fresh = idx >= g;
             uint32_t v = fresh ? regen : a[j];
-            if (fresh && j < cnt) mt[idx * n + e] = v;
+            if (fresh && j < cnt) roww[idx] = v;
             v ^= v >> 11;
             v ^= (v << 7) & 0x9d2c5680u;
             v ^= (v << 15) & 0xefc60000u;
             v ^= v >> 18;
             buf[j * BLOCK] = v;
         }
-        if (pos + cnt > g) g = pos + cnt;
-        bi = 0;
+        if (pa + cnt > g) g = pa + cnt;
+        bi = pos - pa;
         bcnt = cnt;
     }
-    __device__ __forceinline__ uint32_t next() {   // caller guarantees bi < bcnt
-        const uint32_t v = buf[bi * BLOCK];
+    __device__ __forceinline__ uint32_t peek(int j) const { return buf[(bi + j) * BLOCK]; }   // bi + j < bcnt
+    __device__ __forceinline__ void consume() {
         bi += 1;
         pos += 1;
         if (pos == MT_N) { pos = 0; g = 0; }
-        return v;
     }
 };
 
@@ -172,18 +149,27 @@ __device__ __forceinline__ void env_reset(Env& E, const Tables& T, const Cfg& C,
     env_clear(E, C);
     E.set_norders(num_orders);
     MtReader R{S.mt, mtbuf, S.n, e, E.mti() & 0x3FF, (E.mti() >> 16) & 0x3FF, 0, 0};
-    const int nf = 3 * num_orders;
-    int f = 0, k = 0, np = 0, ty = 0;
+    int o = 0, k = 0, np = 0, ty = 0;   // order index, field within the order (n, type, colour)
+    // One draw: numpy's masked rejection (rng 8 / mask 15 for n, rng 2 / mask 3 otherwise).
+    auto take = [&](uint32_t v) {
+        R.consume();
+        const uint32_t x = v & (k == 0 ? 15u : 3u);
+        if (x > (k == 0 ? 8u : 2u)) return;   // rejected draw
+        if (k == 0) { np = 1 + (int)x; k = 1; }
+        else if (k == 1) { ty = 1 + (int)x; k = 2; }
+        else { T.orders[o * T.stride] = ow_make(np, ty, 1 + (int)x); k = 0; o += 1; }
+    };
     for (;;) {
-        while (f < nf && R.bi < R.bcnt) {   // LDS-only consumption
-            const uint32_t x = R.next() & (k == 0 ? 15u : 3u);
-            if (x > (k == 0 ? 8u : 2u)) continue;   // rejected draw
-            if (k == 0) { np = 1 + (int)x; k = 1; }
-            else if (k == 1) { ty = 1 + (int)x; k = 2; }
-            else { T.orders[(f / 3) * T.stride] = ow_make(np, ty, 1 + (int)x); k = 0; }
-            f += 1;
+        // four staged draws per LDS round trip (their reads are independent of the rejections)
+        while (o < num_orders && R.bi + 4 <= R.bcnt) {
+            const uint32_t v0 = R.peek(0), v1 = R.peek(1), v2 = R.peek(2), v3 = R.peek(3);
+            take(v0);
+            if (o < num_orders) take(v1);
+            if (o < num_orders) take(v2);
+            if (o < num_orders) take(v3);
         }
-        const bool need = f < nf;
+        while (o < num_orders && R.bi < R.bcnt) take(R.peek(0));
+        const bool need = o < num_orders;
         if (!__any(need)) break;   // wave-uniform refill point
         if (need) R.fill();
     }
@@ -252,7 +238,7 @@ struct StoreSink {
 __global__ void __launch_bounds__(BLOCK) k_seed(DevState S, const uint32_t* __restrict__ seeds, uint32_t seed_base) {
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     if (e >= S.n) return;
-    mt_seed(S.mt, S.n, e, seeds ? seeds[e] : seed_base + (uint32_t)e);
+    mt_seed(S.mt, e, seeds ? seeds[e] : seed_base + (uint32_t)e);
     S.words[3 * S.n + e] = 0;
 }
 
@@ -265,7 +251,7 @@ __global__ void __launch_bounds__(BLOCK) k_reset(DevState S, Cfg C, const uint32
     Tables T = tables_of(S, e);
     Env E;
     int mti = (int)S.words[3 * S.n + e];
-    if (seeds) { mt_seed(S.mt, S.n, e, seeds[e]); mti = 0; }
+    if (seeds) { mt_seed(S.mt, e, seeds[e]); mti = 0; }
     E.set_mti(mti);
     env_reset(E, T, C, S, e, num_orders, s_mtbuf + threadIdx.x);
     StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, 0u, (uint32_t)S.n, (uint32_t)e, out.feats};
@@ -1140,7 +1126,7 @@ int fjsp_mt_get(fjsp_handle* h, int32_t env, uint32_t* key, int32_t* pos) {
     HIPCHK(hipStreamSynchronize(h->stream));
     uint32_t st = 0;
     HIPCHK(hipMemcpy(&st, h->S.words + (size_t)3 * h->n + env, 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy2D(key, 4, h->S.mt + env, (size_t)h->n * 4, 4, MT_N, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(key, h->S.mt + (size_t)env * MT_N, 4 * MT_N, hipMemcpyDeviceToHost));
     int mti = (int)(st & 0x3FF), gg = (int)((st >> 16) & 0x3FF);
     if (gg == 0) { *pos = MT_N; return 0; }
     for (int i = gg; i < MT_N; i++) {   // finish the in-place twist of the current block
@@ -1160,7 +1146,7 @@ int fjsp_mt_set(fjsp_handle* h, int32_t env, const uint32_t* key, int32_t pos) {
     DeviceGuard g(h->device);
     HIPCHK(hipStreamSynchronize(h->stream));
     const uint32_t st = pos >= MT_N ? 0u : ((uint32_t)pos | ((uint32_t)MT_N << 16));
-    HIPCHK(hipMemcpy2D(h->S.mt + env, (size_t)h->n * 4, key, 4, 4, MT_N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->S.mt + (size_t)env * MT_N, key, 4 * MT_N, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->S.words + (size_t)3 * h->n + env, &st, 4, hipMemcpyHostToDevice));
     return 0;
 }
