@@ -222,6 +222,25 @@ int fjsp_a2c_layout(int32_t* out);
  * are stream-ordered (hipMemcpyAsync; pinned host memory for overlap).  The role of
  * FJSPSimulation's Python objects being copied / pickled by a caller. */
 int64_t fjsp_snapshot_bytes(const fjsp_handle* h);
+
+/* ---- fused A2C policy step (a2c.py:168-252 predict for all agents and envs; networks.py) ----
+ * feats f32 [38][N] (fjsp_out.feats layout), masks int8 [29][N]; weights pre-packed:
+ *   actor_w: 8 agents x FJSP_POLICY_ACTOR_FLOATS: W1 [256][16] (inputs zero-padded) | b1 [256] |
+ *            W2 MFMA-packed [8 row tiles][128 k-steps][64 lanes], element (t, s, l) =
+ *            W2[32 t + (l & 31)][2 s + (l >> 5)] | b2 [256] | W3 [8][256] (rows >= n_a zero) | b3 [16]
+ *   critic_w: W1 [256][40] | b1 [256] | W2 packed [8][128][64] | b2 [256] | W3 packed [4][128][64] |
+ *            b3 [128] | W4 [128] | b4 [16]
+ * Out: actions u8 [8][N] (argmax if deterministic, else an inverse-CDF draw from the masked
+ * distribution keyed by (*seed, env, step, agent); `seed` is a DEVICE pointer so a captured
+ * hipGraph can be re-keyed between replays), values f32 [N], optional masked
+ * probabilities f32 [8][8][N] (NULL to skip).  Stream-ordered on `stream`. */
+#define FJSP_POLICY_ACTOR_DPAD 16
+#define FJSP_POLICY_CRITIC_DPAD 40
+#define FJSP_POLICY_ACTOR_FLOATS (256 * 16 + 256 + 256 * 256 + 256 + 8 * 256 + 16)
+#define FJSP_POLICY_CRITIC_FLOATS (256 * 40 + 256 + 256 * 256 + 256 + 128 * 256 + 128 + 128 + 16)
+int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const float* actor_w, const float* critic_w,
+                    const uint64_t* seed, uint32_t step, int32_t deterministic, uint8_t* actions, float* values,
+                    float* probs, void* stream);
 int fjsp_snapshot(fjsp_handle* h, void* dst);
 int fjsp_restore(fjsp_handle* h, const void* src);
 /* Kernel timing of the last fjsp_step_many / fjsp_step launch in ms (hipEvents on the

@@ -13,6 +13,7 @@ REPO = os.path.dirname(HERE)
 # FJSP_LIB selects a diagnostic build (e.g. libfjsp_stamps.so); default: the product library
 LIB_PATH = os.environ.get("FJSP_LIB") or os.path.join(HERE, "libfjsp.so")
 SRC = os.path.join(HERE, "csrc", "fjsp_hip.hip")
+SRCS = [SRC, os.path.join(HERE, "csrc", "fjsp_policy.hip")]
 HEADERS = [os.path.join(HERE, "csrc", "fjsp_env.h"), os.path.join(REPO, "include", "fjsp.h")]
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
@@ -62,7 +63,9 @@ EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_c
            "fjsp_create", "fjsp_destroy", "fjsp_set_stream", "fjsp_set_option", "fjsp_num_envs", "fjsp_state_bytes",
            "fjsp_reset", "fjsp_step", "fjsp_step_many", "fjsp_gae", "fjsp_gae_f64", "fjsp_mt_get", "fjsp_mt_set",
            "fjsp_read_env", "fjsp_sync", "fjsp_last_kernel_ms", "fjsp_pack_a2c", "fjsp_a2c_layout",
-           "fjsp_snapshot_bytes", "fjsp_snapshot", "fjsp_restore", "fjsp_last_kernel"]
+           "fjsp_snapshot_bytes", "fjsp_snapshot", "fjsp_restore", "fjsp_last_kernel", "fjsp_a2c_policy"]
+POLICY_ACTOR_FLOATS = 256 * 16 + 256 + 256 * 256 + 256 + 8 * 256 + 16
+POLICY_CRITIC_FLOATS = 256 * 40 + 256 + 256 * 256 + 256 + 128 * 256 + 128 + 128 + 16
 ABI_VERSION = 2
 
 _lib = None
@@ -72,14 +75,14 @@ def _stale():
     if not os.path.exists(LIB_PATH):
         return True
     t = os.path.getmtime(LIB_PATH)
-    return any(os.path.getmtime(p) > t for p in [SRC] + HEADERS)
+    return any(os.path.getmtime(p) > t for p in SRCS + HEADERS)
 
 
 def build(force=False, verbose=False):
     """Compile libfjsp.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
     if not force and not _stale():
         return LIB_PATH
-    cmd = ["hipcc"] + HIPCC_FLAGS + ["-o", LIB_PATH, SRC]
+    cmd = ["hipcc"] + HIPCC_FLAGS + ["-o", LIB_PATH] + SRCS
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise FjspNativeError("hipcc failed:\n" + r.stderr[-4000:])
@@ -128,6 +131,7 @@ def lib():
         "fjsp_snapshot": (I, [P, P]),
         "fjsp_restore": (I, [P, P]),
         "fjsp_last_kernel": (ctypes.c_char_p, [P]),
+        "fjsp_a2c_policy": (I, [P, P, I, P, P, P, U32, I, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -225,6 +225,38 @@ def clip_per_agent_(actors, max_norm):
     return norm
 
 
+# ---------------------------------------------------------------- fused policy kernel weights
+def pack_mfma(W):
+    """[..., R, K] -> [..., R/32, K/2, 64] with (t, s, l) = W[32 t + (l & 31)][2 s + (l >> 5)]:
+    the lane order of the A operand of v_mfma_f32_32x32x2_f32 (csrc/fjsp_policy.hip)."""
+    *lead, R, K = W.shape
+    nl = len(lead)
+    W = W.reshape(*lead, R // 32, 32, K // 2, 2)
+    W = W.permute(*range(nl), nl, nl + 2, nl + 3, nl + 1)
+    return W.reshape(*lead, R // 32, K // 2, 64)
+
+
+@torch.no_grad()
+def pack_policy_weights(actors, critic, out_actor=None, out_critic=None):
+    """Actor stack + critic -> the flat f32 buffers fjsp_a2c_policy reads (include/fjsp.h)."""
+    dev = actors.W1.device
+    z = lambda *s: torch.zeros(*s, device=dev)  # noqa: E731
+    w1 = torch.cat([actors.W1, z(NA, actors.hidden, 16 - DPAD)], dim=2)            # [8, 256, 16]
+    b3 = torch.cat([actors.b3[:, :, 0], z(NA, 8)], dim=1)                             # [8, 16]
+    a = torch.cat([w1.reshape(NA, -1), actors.b1.reshape(NA, -1), pack_mfma(actors.W2).reshape(NA, -1),
+                   actors.b2.reshape(NA, -1), actors.W3.reshape(NA, -1), b3], dim=1).reshape(-1)
+    n = critic.net
+    c = torch.cat([torch.cat([n[0].weight, z(256, 2)], dim=1).reshape(-1), n[0].bias,
+                   pack_mfma(n[2].weight).reshape(-1), n[2].bias, pack_mfma(n[4].weight).reshape(-1), n[4].bias,
+                   n[6].weight.reshape(-1), torch.cat([n[6].bias, z(15)])])
+    assert a.numel() == NA * nat.POLICY_ACTOR_FLOATS and c.numel() == nat.POLICY_CRITIC_FLOATS
+    if out_actor is None:
+        return a.contiguous(), c.contiguous()
+    out_actor.copy_(a)
+    out_critic.copy_(c)
+    return out_actor, out_critic
+
+
 def init_networks(seed=None, hidden=256, device="cpu"):
     """Actor stack + critic initialised exactly like MultiAgentA2C.__init__ (a2c.py:87-103):
     the 8 ActorNetworks in possible_agents order, then the critic, from torch's CPU generator
@@ -275,7 +307,7 @@ class VecMultiAgentA2C:
 
     def __init__(self, env, batch_size=256, gamma=0.99, lamb=0.95, lr_actor=3e-4, lr_critic=1e-3,
                  use_gae=True, entropy_coef=0.01, max_grad_norm=0.5, hidden=256, seed=None, group=None,
-                 use_graph=True):
+                 use_graph=True, fused_policy=True):
         self.env = env
         self.device = env.device
         self.N = env.num_envs
@@ -299,6 +331,13 @@ class VecMultiAgentA2C:
         self.episode_end_timesteps = []
         self._bufs = None
         self.use_graph = bool(use_graph) and self.device.type == "cuda"
+        # fused policy kernel (csrc/fjsp_policy.hip): one launch per vector step
+        self.fused_policy = bool(fused_policy) and self.device.type == "cuda" and hidden == 256
+        if self.fused_policy:
+            self._pw_actor, self._pw_critic = pack_policy_weights(self.actors, self.critic)
+            self._rng = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self._rng_host = int.from_bytes(__import__("os").urandom(7), "little") if seed is None else int(seed)
+            self._rng.fill_(self._rng_host)
         self._graph = None
         self._graph_det = None
         self._eager_batches = 0
@@ -348,6 +387,22 @@ class VecMultiAgentA2C:
 
     # ------------------------------------------------------------ predict
     @torch.no_grad()
+    def policy_fused(self, feats, masks, t, deterministic, act_out, val_out, probs_out=None):
+        """fjsp_a2c_policy on this stream: actions u8 [8, N] -> act_out, values -> val_out."""
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        P = lambda x: None if x is None else ctypes.c_void_p(x.data_ptr())  # noqa: E731
+        rc = nat.lib().fjsp_a2c_policy(P(feats), P(masks), int(feats.shape[-1]), P(self._pw_actor),
+                                       P(self._pw_critic), P(self._rng), int(t), int(bool(deterministic)),
+                                       P(act_out), P(val_out), P(probs_out), ctypes.c_void_p(stream))
+        if rc != 0:
+            raise nat.FjspNativeError(f"fjsp_a2c_policy failed ({rc})")
+
+    def repack(self):
+        """Refresh the fused kernel's packed weights (after an update / load)."""
+        if self.fused_policy:
+            pack_policy_weights(self.actors, self.critic, self._pw_actor, self._pw_critic)
+
+    @torch.no_grad()
     def policy(self, feats, masks, deterministic=False):
         """predict (a2c.py:168-252) for all agents and envs: actions long [8, B], the masked
         probabilities [8, 8, B] and the critic's value [B]."""
@@ -370,6 +425,9 @@ class VecMultiAgentA2C:
         (tests).  After one eager batch the whole batch (batch_size x (policy + step) plus the
         bootstrap value, ~40 launches per step) is captured once into a hipGraph and replayed:
         the buffers and parameters are static, Adam updates the weights in place."""
+        if self.fused_policy:
+            self._rng_host += 1
+            self._rng.fill_(self._rng_host)   # re-keys the sampling of the (captured) batch
         if action_fn is None and self.use_graph:
             if self._graph is not None and self._graph_det == deterministic:
                 self._graph.replay()
@@ -400,11 +458,14 @@ class VecMultiAgentA2C:
         h = self.env.handle
         self.env._sync_stream()
         for t in range(self.batch_size):
-            act, _, v = self.policy(b["feats"][t], b["masks"][t], deterministic)
-            if action_fn is not None:
-                act = action_fn(t, b["masks"][t]).to(self.device).long()
-            b["actions"][t].copy_(act)
-            b["values"][t].copy_(v)
+            if self.fused_policy and action_fn is None:
+                self.policy_fused(b["feats"][t], b["masks"][t], t, deterministic, b["actions"][t], b["values"][t])
+            else:
+                act, _, v = self.policy(b["feats"][t], b["masks"][t], deterministic)
+                if action_fn is not None:
+                    act = action_fn(t, b["masks"][t]).to(self.device).long()
+                b["actions"][t].copy_(act)
+                b["values"][t].copy_(v)
             nat.check(L.fjsp_step(h, ctypes.c_void_p(b["actions"][t].data_ptr()), None, 1,
                                   ctypes.byref(b["outs"][t])))
         with torch.no_grad():
@@ -436,6 +497,7 @@ class VecMultiAgentA2C:
         for a, x in zip(AGENTS, al):
             self.actor_loss_history[a].append(x)
         self.critic_loss_history.append(cl)
+        self.repack()
         return al, cl
 
     def roll_over(self):
@@ -489,6 +551,8 @@ class VecMultiAgentA2C:
             nets.append(net)
         self.actors.load_actor_nets([n.to(self.device) for n in nets])
         self.critic.load_state_dict(ck["critic_net"])
+        if getattr(self, "fused_policy", False):
+            self.repack()
 
 
 def num_params(model):

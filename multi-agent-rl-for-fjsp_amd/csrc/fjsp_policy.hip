@@ -1,0 +1,228 @@
+// fjsp_policy.hip — fused A2C policy step for gfx950 (one launch per vector step).
+//
+// Replaces the ~40 PyTorch launches of a2c_vec.VecMultiAgentA2C.policy (reference predict,
+// a2c.py:168-252): for every env, the 8 actor MLPs (networks.ActorNetwork: d -> 256 -> 256 ->
+// n_a, softmax), the action mask / renormalisation / uniform fallback (a2c.py:204-220), the
+// action draw (inverse CDF over the masked probabilities, or argmax) and the centralised
+// critic (networks.CentralizedCriticNetwork: 38 -> 256 -> 256 -> 128 -> 1).
+//
+// Grid: blockIdx.y = role (0..7 actor of agent y, 8 critic), blockIdx.x = tile of 64 envs;
+// 256 threads = 4 wavefronts.  The hidden activations never leave LDS:
+//   x   [40][64]  inputs of the tile (feature rows of the kernel-written [38][N] slab)
+//   h1  [256][64] layer 1 (K <= 40: f32 VALU FMAs)
+//   h2  [256][64] layer 2 (K = 256: v_mfma_f32_32x32x2_f32, exact f32 fma chains; each wave
+//                 owns 64 output rows = 2 x 2 tiles of 32 x 32, 128 k-steps of 2)
+//   critic h3 [128][64] (MFMA again, one 32-row tile per wave), then the 128 -> 1 dot.
+// MFMA A operands (weights) are pre-packed on the host per (row tile, k-step) in lane order
+// (fjsp_pack_policy_weights layout below), so each k-step's A fragment is one coalesced
+// 256-byte load; B fragments (activations) are conflict-free LDS reads.
+// f32 arithmetic throughout (the reference networks are f32); summation order differs from
+// PyTorch's GEMMs only by rounding (tests: 1e-5).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fjsp.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int TILE = 64;       // envs per workgroup
+constexpr int HID = 256;
+constexpr int NAG = 8;
+constexpr int KS2 = HID / 2;   // k-steps of 2 for a 256-wide contraction
+
+__constant__ int c_obs_off[NAG] = {0, 7, 20, 23, 26, 29, 32, 35};
+__constant__ int c_obs_dim[NAG] = {7, 13, 3, 3, 3, 3, 3, 3};
+__constant__ int c_mask_off[NAG] = {0, 3, 11, 14, 17, 20, 23, 26};
+__constant__ int c_nact[NAG] = {3, 8, 3, 3, 3, 3, 3, 3};
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t z) {
+    z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27; z *= 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return z;
+}
+
+// acc += W (rows [32*rt0, 32*rt0 + 64), packed) . act (LDS [256][64], rows = k), 2 x 2 tiles.
+__device__ __forceinline__ void mfma_rows64(const float* __restrict__ wp, int rt0, const float* act, int lane,
+                                            f32x16 acc[2][2]) {
+    const float* a0 = wp + ((size_t)(rt0 + 0) * KS2) * 64 + lane;
+    const float* a1 = wp + ((size_t)(rt0 + 1) * KS2) * 64 + lane;
+    const int kr = lane >> 5, cl = lane & 31;
+    float na0 = a0[0], na1 = a1[0];
+#pragma unroll 4
+    for (int ks = 0; ks < KS2; ks++) {
+        const float fa0 = na0, fa1 = na1;
+        if (ks + 1 < KS2) { na0 = a0[(ks + 1) * 64]; na1 = a1[(ks + 1) * 64]; }
+        const float b0 = act[(2 * ks + kr) * TILE + cl];
+        const float b1 = act[(2 * ks + kr) * TILE + 32 + cl];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1, b1, acc[1][1], 0, 0, 0);
+    }
+}
+
+// relu(acc + bias) -> out LDS [rows][64]; C/D layout of the 32x32 f32 MFMA: col = lane & 31,
+// row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
+__device__ __forceinline__ void store_tile(const f32x16& acc, int row0, int col0, const float* __restrict__ bias,
+                                           float* out, int lane) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const float v = acc[r] + bias[row];
+        out[row * TILE + col0 + (lane & 31)] = v > 0.0f ? v : 0.0f;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_policy(const float* __restrict__ feats, const int8_t* __restrict__ masks, int n,
+                                                const float* __restrict__ actor_w, const float* __restrict__ critic_w,
+                                                const uint64_t* __restrict__ seedp, uint32_t step, int deterministic,
+                                                uint8_t* __restrict__ actions, float* __restrict__ values,
+                                                float* __restrict__ probs_out) {
+    __shared__ float s_x[40 * TILE];
+    __shared__ float s_h1[HID * TILE];
+    __shared__ float s_h2[HID * TILE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int role = blockIdx.y;
+    const int e0 = blockIdx.x * TILE;
+    const bool critic = role == NAG;
+    const int din = critic ? 38 : c_obs_dim[role];
+    const int off = critic ? 0 : c_obs_off[role];
+    const int dpad = critic ? FJSP_POLICY_CRITIC_DPAD : FJSP_POLICY_ACTOR_DPAD;
+    // inputs
+    for (int i = tid; i < dpad * TILE; i += 256) {
+        const int k = i / TILE, c = i % TILE;
+        s_x[i] = (k < din && e0 + c < n) ? feats[(size_t)(off + k) * n + e0 + c] : 0.0f;
+    }
+    __syncthreads();
+    const float* W = critic ? critic_w : actor_w + (size_t)role * FJSP_POLICY_ACTOR_FLOATS;
+    const float* W1 = W;                                   // [256][dpad]
+    const float* B1 = W1 + HID * dpad;                     // [256]
+    const float* W2 = B1 + HID;                            // packed [8][128][64]
+    const float* B2 = W2 + HID * HID;                      // [256]
+    // layer 1 (VALU): lane -> env column c, wave -> rows r = wave + 4 i (weights wave-uniform)
+    {
+        const int c = lane;
+        const int wv = __builtin_amdgcn_readfirstlane(wave);
+        float x[40];
+#pragma unroll
+        for (int k = 0; k < 40; k++) x[k] = k < dpad ? s_x[k * TILE + c] : 0.0f;
+        for (int i = 0; i < HID / 4; i++) {
+            const int r = wv + 4 * i;
+            float acc = B1[r];
+#pragma unroll
+            for (int k = 0; k < 40; k++)
+                if (k < dpad) acc = fmaf(W1[r * dpad + k], x[k], acc);
+            s_h1[r * TILE + c] = acc > 0.0f ? acc : 0.0f;
+        }
+    }
+    __syncthreads();
+    // layer 2 (MFMA): wave w -> rows [64w, 64w + 64)
+    {
+        f32x16 acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[i][j][r] = 0.0f;
+        mfma_rows64(W2, 2 * wave, s_h1, lane, acc);
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) store_tile(acc[i][j], 64 * wave + 32 * i, 32 * j, B2, s_h2, lane);
+    }
+    __syncthreads();
+    if (critic) {
+        const float* W3 = B2 + HID;                        // packed [4][128][64]
+        const float* B3 = W3 + 128 * HID;                  // [128]
+        const float* W4 = B3 + 128;                        // [128]
+        const float* B4 = W4 + 128;                        // [1]
+        f32x16 acc[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[j][r] = 0.0f;
+        const float* a0 = W3 + ((size_t)wave * KS2) * 64 + lane;
+        const int kr = lane >> 5, cl = lane & 31;
+        for (int ks = 0; ks < KS2; ks++) {
+            const float fa = a0[ks * 64];
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, s_h2[(2 * ks + kr) * TILE + cl], acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, s_h2[(2 * ks + kr) * TILE + 32 + cl], acc[1], 0, 0, 0);
+        }
+        // h3 [128][64] reuses s_h1
+        store_tile(acc[0], 32 * wave, 0, B3, s_h1, lane);
+        store_tile(acc[1], 32 * wave, 32, B3, s_h1, lane);
+        __syncthreads();
+        if (tid < TILE && e0 + tid < n) {
+            float v = B4[0];
+            for (int k = 0; k < 128; k++) v = fmaf(W4[k], s_h1[k * TILE + tid], v);
+            values[e0 + tid] = v;
+        }
+        return;
+    }
+    // actor layer 3: logits [8][64]; thread -> (action pair, env)
+    const float* W3 = B2 + HID;                            // [8][256]
+    const float* B3 = W3 + 8 * HID;                        // [8]
+    float* s_logit = s_x;                                  // [8][64]
+    {
+        const int c = tid & 63, r0 = (tid >> 6) * 2;
+        float l0 = B3[r0], l1 = B3[r0 + 1];
+        for (int k = 0; k < HID; k++) {
+            const float h = s_h2[k * TILE + c];
+            l0 = fmaf(W3[r0 * HID + k], h, l0);
+            l1 = fmaf(W3[(r0 + 1) * HID + k], h, l1);
+        }
+        s_logit[r0 * TILE + c] = l0;
+        s_logit[(r0 + 1) * TILE + c] = l1;
+    }
+    __syncthreads();
+    if (tid < TILE && e0 + tid < n) {
+        const int c = tid, e = e0 + tid;
+        const int na = c_nact[role], mo = c_mask_off[role];
+        float p[8], m[8];
+        float mx = -INFINITY;
+        for (int j = 0; j < na; j++) mx = fmaxf(mx, s_logit[j * TILE + c]);
+        float s = 0.0f;
+        for (int j = 0; j < na; j++) { p[j] = expf(s_logit[j * TILE + c] - mx); s += p[j]; }
+        float s2 = 0.0f, ms = 0.0f;
+        for (int j = 0; j < na; j++) {
+            m[j] = (float)masks[(size_t)(mo + j) * n + e];
+            p[j] = (p[j] / s) * m[j];
+            s2 += p[j];
+            ms += m[j];
+        }
+        for (int j = 0; j < na; j++) p[j] = s2 > 0.0f ? p[j] / s2 : m[j] / ms;
+        int act = 0;
+        if (deterministic) {
+            float best = p[0];
+            for (int j = 1; j < na; j++) if (p[j] > best) { best = p[j]; act = j; }
+        } else {
+            const uint64_t seed = *seedp;
+            const uint64_t h = fmix64(seed ^ fmix64(((uint64_t)(uint32_t)e << 32) | step) ^ (uint64_t)(role + 1) * 0x9E3779B97F4A7C15ull);
+            const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+            float cdf[8], tot = 0.0f;
+            for (int j = 0; j < na; j++) { tot += p[j]; cdf[j] = tot; }
+            const float x = (1.0f - u) * tot;
+            for (int j = 0; j < na; j++) act += cdf[j] < x;
+            if (act >= na) act = na - 1;
+        }
+        actions[(size_t)role * n + e] = (uint8_t)act;
+        if (probs_out)
+            for (int j = 0; j < 8; j++) probs_out[((size_t)role * 8 + j) * n + e] = j < na ? p[j] : 0.0f;
+    }
+}
+
+}  // namespace
+
+extern "C" int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const float* actor_w,
+                               const float* critic_w, const uint64_t* seed, uint32_t step, int32_t deterministic,
+                               uint8_t* actions, float* values, float* probs, void* stream) {
+    if (n <= 0 || !feats || !masks || !actor_w || !critic_w || !seed || !actions || !values) return -1;
+    dim3 grid((n + TILE - 1) / TILE, NAG + 1);
+    hipLaunchKernelGGL(k_policy, grid, dim3(256), 0, (hipStream_t)stream, feats, masks, n, actor_w, critic_w, seed, step,
+                       deterministic, actions, values, probs);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -132,3 +132,37 @@ def test_graph_replay_equals_eager(M):
     assert runs[1][0] == runs[0][0] and runs[1][1] == runs[0][1]
     for i in (2, 3, 4):
         assert torch.equal(runs[0][i], runs[1][i])
+
+
+def test_fused_policy_kernel_matches_torch_policy(M):
+    """fjsp_a2c_policy (one MFMA kernel per step) == the PyTorch policy path: masked
+    probabilities and values within 1e-5, greedy actions equal (up to near-ties), sampled
+    actions valid and distributed like the probabilities."""
+    A, V = M["A"], M["V"]
+    n = 1000                                                          # not a multiple of 64
+    env = V.FJSPVecEnv(n)
+    learner = A.VecMultiAgentA2C(env, batch_size=8, seed=3, use_graph=False)
+    learner.learn(2 * 8 * n, num_orders=25, seeds=torch.arange(n))   # two updates: trained weights
+    feats, masks = env.pack_a2c()
+    act_t, pm_t, v_t = learner.policy(feats, masks, deterministic=True)
+    act = torch.zeros(8, n, dtype=torch.uint8, device=env.device)
+    val = torch.zeros(n, dtype=torch.float32, device=env.device)
+    probs = torch.zeros(8, 8, n, dtype=torch.float32, device=env.device)
+    learner.policy_fused(feats, masks, 0, True, act, val, probs)
+    torch.cuda.synchronize()
+    assert torch.allclose(probs, pm_t, atol=1e-5), float((probs - pm_t).abs().max())
+    assert torch.allclose(val, v_t, atol=1e-5, rtol=1e-5), float((val - v_t).abs().max())
+    top2 = torch.topk(pm_t, 2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 1e-5
+    assert bool((act.long() == act_t)[clear].all())
+    # sampling: valid actions, frequencies ~ probabilities
+    ma = A.agent_masks(masks, learner.midx)
+    counts = torch.zeros(8, 8, n, device=env.device)
+    R = 400
+    for r in range(R):
+        learner._rng.fill_(1000 + r)
+        learner.policy_fused(feats, masks, 0, False, act, val)
+        assert bool((ma.gather(1, act.long().unsqueeze(1)) == 1).all())
+        counts.scatter_add_(1, act.long().unsqueeze(1), torch.ones(8, 1, n, device=env.device))
+    freq = counts / R
+    assert float((freq - pm_t).abs().mean()) < 0.01
