@@ -224,11 +224,12 @@ int fjsp_a2c_layout(int32_t* out);
 int64_t fjsp_snapshot_bytes(const fjsp_handle* h);
 
 /* ---- fused A2C policy step (a2c.py:168-252 predict for all agents and envs; networks.py) ----
- * feats f32 [38][N] (fjsp_out.feats layout), masks int8 [29][N]; weights pre-packed:
- *   actor_w: 8 agents x FJSP_POLICY_ACTOR_FLOATS: W1 [256][16] (inputs zero-padded) | b1 [256] |
- *            W2 MFMA-packed [8 row tiles][128 k-steps][64 lanes], element (t, s, l) =
- *            W2[32 t + (l & 31)][2 s + (l >> 5)] | b2 [256] | W3 [8][256] (rows >= n_a zero) | b3 [16]
- *   critic_w: W1 [256][40] | b1 [256] | W2 packed [8][128][64] | b2 [256] | W3 packed [4][128][64] |
+ * feats f32 [38][N] (fjsp_out.feats layout), masks int8 [29][N]; weights pre-packed, every
+ * K >= 16 matrix W [R][K] in MFMA order P(W) = [R/32][K/8][64 lanes][4], element (t, q, l, j) =
+ * W[32 t + (l & 31)][2 (4 q + j) + (l >> 5)]:
+ *   actor_w: 8 agents x FJSP_POLICY_ACTOR_FLOATS: P(W1 [256][16], inputs zero-padded) | b1 [256] |
+ *            P(W2 [256][256]) | b2 [256] | W3 [8][256] (rows >= n_a zero) | b3 [16]
+ *   critic_w: P(W1 [256][40]) | b1 [256] | P(W2 [256][256]) | b2 [256] | P(W3 [128][256]) |
  *            b3 [128] | W4 [128] | b4 [16]
  * Out: actions u8 [8][N] (argmax if deterministic, else an inverse-CDF draw from the masked
  * distribution keyed by (*seed, env, step, agent); `seed` is a DEVICE pointer so a captured

@@ -227,13 +227,14 @@ def clip_per_agent_(actors, max_norm):
 
 # ---------------------------------------------------------------- fused policy kernel weights
 def pack_mfma(W):
-    """[..., R, K] -> [..., R/32, K/2, 64] with (t, s, l) = W[32 t + (l & 31)][2 s + (l >> 5)]:
-    the lane order of the A operand of v_mfma_f32_32x32x2_f32 (csrc/fjsp_policy.hip)."""
+    """[..., R, K] -> [..., R/32, K/8, 64, 4] with (t, q, l, j) = W[32 t + (l & 31)][2 (4 q + j) + (l >> 5)]:
+    the A-operand lane order of v_mfma_f32_32x32x2_f32 in groups of 4 k-steps, one float4
+    load per lane per group (csrc/fjsp_policy.hip)."""
     *lead, R, K = W.shape
     nl = len(lead)
-    W = W.reshape(*lead, R // 32, 32, K // 2, 2)
-    W = W.permute(*range(nl), nl, nl + 2, nl + 3, nl + 1)
-    return W.reshape(*lead, R // 32, K // 2, 64)
+    W = W.reshape(*lead, R // 32, 32, K // 8, 4, 2)                  # t, i, q, j, kk
+    W = W.permute(*range(nl), nl, nl + 2, nl + 4, nl + 1, nl + 3)     # t, q, kk, i, j
+    return W.reshape(*lead, R // 32, K // 8, 64, 4)
 
 
 @torch.no_grad()
@@ -243,10 +244,10 @@ def pack_policy_weights(actors, critic, out_actor=None, out_critic=None):
     z = lambda *s: torch.zeros(*s, device=dev)  # noqa: E731
     w1 = torch.cat([actors.W1, z(NA, actors.hidden, 16 - DPAD)], dim=2)            # [8, 256, 16]
     b3 = torch.cat([actors.b3[:, :, 0], z(NA, 8)], dim=1)                             # [8, 16]
-    a = torch.cat([w1.reshape(NA, -1), actors.b1.reshape(NA, -1), pack_mfma(actors.W2).reshape(NA, -1),
+    a = torch.cat([pack_mfma(w1).reshape(NA, -1), actors.b1.reshape(NA, -1), pack_mfma(actors.W2).reshape(NA, -1),
                    actors.b2.reshape(NA, -1), actors.W3.reshape(NA, -1), b3], dim=1).reshape(-1)
     n = critic.net
-    c = torch.cat([torch.cat([n[0].weight, z(256, 2)], dim=1).reshape(-1), n[0].bias,
+    c = torch.cat([pack_mfma(torch.cat([n[0].weight, z(256, 2)], dim=1)).reshape(-1), n[0].bias,
                    pack_mfma(n[2].weight).reshape(-1), n[2].bias, pack_mfma(n[4].weight).reshape(-1), n[4].bias,
                    n[6].weight.reshape(-1), torch.cat([n[6].bias, z(15)])])
     assert a.numel() == NA * nat.POLICY_ACTOR_FLOATS and c.numel() == nat.POLICY_CRITIC_FLOATS

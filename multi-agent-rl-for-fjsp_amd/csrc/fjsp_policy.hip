@@ -9,10 +9,11 @@
 // Grid: blockIdx.y = role (0..7 actor of agent y, 8 critic), blockIdx.x = tile of 64 envs;
 // 256 threads = 4 wavefronts.  The hidden activations never leave LDS:
 //   x   [40][64]  inputs of the tile (feature rows of the kernel-written [38][N] slab)
-//   h1  [256][64] layer 1 (K <= 40: f32 VALU FMAs)
-//   h2  [256][64] layer 2 (K = 256: v_mfma_f32_32x32x2_f32, exact f32 fma chains; each wave
-//                 owns 64 output rows = 2 x 2 tiles of 32 x 32, 128 k-steps of 2)
-//   critic h3 [128][64] (MFMA again, one 32-row tile per wave), then the 128 -> 1 dot.
+//   h   [256][64] layer 1, then layer 2, then the critic's layer 3 (in place: results stay in
+//                 registers across a barrier), so two workgroups fit a CU (74 KB of LDS each)
+// Every layer with K >= 16 runs on v_mfma_f32_32x32x2_f32 (exact f32 fma chains): each wave
+// owns 64 output rows = 2 x 2 tiles of 32 x 32 (the critic's 128-row layer 3: one tile row).
+// The actor's 256 -> n_a logits and the critic's 128 -> 1 value are VALU dot products.
 // MFMA A operands (weights) are pre-packed on the host per (row tile, k-step) in lane order
 // (fjsp_pack_policy_weights layout below), so each k-step's A fragment is one coalesced
 // 256-byte load; B fragments (activations) are conflict-free LDS reads.
@@ -44,24 +45,57 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t z) {
     return z;
 }
 
-// acc += W (rows [32*rt0, 32*rt0 + 64), packed) . act (LDS [256][64], rows = k), 2 x 2 tiles.
-__device__ __forceinline__ void mfma_rows64(const float* __restrict__ wp, int rt0, const float* act, int lane,
-                                            f32x16 acc[2][2]) {
-    const float* a0 = wp + ((size_t)(rt0 + 0) * KS2) * 64 + lane;
-    const float* a1 = wp + ((size_t)(rt0 + 1) * KS2) * 64 + lane;
+// MFMA A operands are packed per row tile t in groups of 4 k-steps: element (t, q, l, j) =
+// W[32 t + (l & 31)][2 (4 q + j) + (l >> 5)], so one 16-byte load per lane fetches the A
+// fragments of 4 consecutive k-steps (a coalesced 1 KB per wave instruction).
+// acc[i][j] += W(row tile rt0 + i) . act(col tile j); act = LDS [K][64] (rows = k), KS = K / 2.
+template <int NT, int KS>
+__device__ __forceinline__ void mfma_rows(const float* __restrict__ wp, int rt0, const float* act, int lane,
+                                          f32x16 acc[NT][2]) {
+    static_assert(KS % 4 == 0, "k-steps come in groups of 4");
+    constexpr int NQ = KS / 4;
+    const float4* a[NT];
+#pragma unroll
+    for (int i = 0; i < NT; i++) a[i] = reinterpret_cast<const float4*>(wp) + (size_t)(rt0 + i) * NQ * 64 + lane;
     const int kr = lane >> 5, cl = lane & 31;
-    float na0 = a0[0], na1 = a1[0];
-#pragma unroll 4
-    for (int ks = 0; ks < KS2; ks++) {
-        const float fa0 = na0, fa1 = na1;
-        if (ks + 1 < KS2) { na0 = a0[(ks + 1) * 64]; na1 = a1[(ks + 1) * 64]; }
-        const float b0 = act[(2 * ks + kr) * TILE + cl];
-        const float b1 = act[(2 * ks + kr) * TILE + 32 + cl];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1, b1, acc[1][1], 0, 0, 0);
+    constexpr int PF = NQ < 2 ? NQ : 2;   // groups in flight
+    float4 buf[PF][NT];
+#pragma unroll
+    for (int p = 0; p < PF; p++)
+#pragma unroll
+        for (int i = 0; i < NT; i++) buf[p][i] = a[i][p * 64];
+#pragma unroll 2
+    for (int q = 0; q < NQ; q++) {
+        float4 cur[NT];
+#pragma unroll
+        for (int i = 0; i < NT; i++) cur[i] = buf[q % PF][i];
+        if (q + PF < NQ) {
+#pragma unroll
+            for (int i = 0; i < NT; i++) buf[q % PF][i] = a[i][(q + PF) * 64];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int k = 2 * (4 * q + j) + kr;
+            const float b0 = act[k * TILE + cl];
+            const float b1 = act[k * TILE + 32 + cl];
+#pragma unroll
+            for (int i = 0; i < NT; i++) {
+                const float fa = j == 0 ? cur[i].x : j == 1 ? cur[i].y : j == 2 ? cur[i].z : cur[i].w;
+                acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, b0, acc[i][0], 0, 0, 0);
+                acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, b1, acc[i][1], 0, 0, 0);
+            }
+        }
     }
+}
+
+template <int NT>
+__device__ __forceinline__ void zero_acc(f32x16 acc[NT][2]) {
+#pragma unroll
+    for (int i = 0; i < NT; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.0f;
 }
 
 // relu(acc + bias) -> out LDS [rows][64]; C/D layout of the 32x32 f32 MFMA: col = lane & 31,
@@ -75,103 +109,84 @@ __device__ __forceinline__ void store_tile(const f32x16& acc, int row0, int col0
         out[row * TILE + col0 + (lane & 31)] = v > 0.0f ? v : 0.0f;
     }
 }
+template <int NT>
+__device__ __forceinline__ void store_rows(const f32x16 acc[NT][2], int row0, const float* __restrict__ bias, float* out,
+                                           int lane) {
+#pragma unroll
+    for (int i = 0; i < NT; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) store_tile(acc[i][j], row0 + 32 * i, 32 * j, bias, out, lane);
+}
 
-__global__ void __launch_bounds__(256) k_policy(const float* __restrict__ feats, const int8_t* __restrict__ masks, int n,
-                                                const float* __restrict__ actor_w, const float* __restrict__ critic_w,
-                                                const uint64_t* __restrict__ seedp, uint32_t step, int deterministic,
-                                                uint8_t* __restrict__ actions, float* __restrict__ values,
-                                                float* __restrict__ probs_out) {
-    __shared__ float s_x[40 * TILE];
-    __shared__ float s_h1[HID * TILE];
-    __shared__ float s_h2[HID * TILE];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// Hidden layers 1 and 2 of a 256-wide MLP on the tile (x in s_x [DPAD][64]) -> s_h [256][64].
+template <int DPAD>
+__device__ __forceinline__ void hidden256(const float* __restrict__ W, const float* s_x, float* s_h, int wave, int lane) {
+    const float* W1 = W;                         // packed [8][DPAD/8][64][4]
+    const float* B1 = W1 + 256 * DPAD;           // [256]
+    const float* W2 = B1 + 256;                  // packed [8][32][64][4]
+    const float* B2 = W2 + 256 * 256;            // [256]
+    f32x16 acc[2][2];
+    zero_acc<2>(acc);
+    mfma_rows<2, DPAD / 2>(W1, 2 * wave, s_x, lane, acc);
+    store_rows<2>(acc, 64 * wave, B1, s_h, lane);
+    __syncthreads();
+    zero_acc<2>(acc);
+    mfma_rows<2, 128>(W2, 2 * wave, s_h, lane, acc);
+    __syncthreads();                             // every wave has read h1
+    store_rows<2>(acc, 64 * wave, B2, s_h, lane);
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256, 2) k_policy(const float* __restrict__ feats, const int8_t* __restrict__ masks,
+                                                   int n, const float* __restrict__ actor_w,
+                                                   const float* __restrict__ critic_w, const uint64_t* __restrict__ seedp,
+                                                   uint32_t step, int deterministic, uint8_t* __restrict__ actions,
+                                                   float* __restrict__ values, float* __restrict__ probs_out) {
+    __shared__ float s_x[FJSP_POLICY_CRITIC_DPAD * TILE];   // inputs; later the logits [8][64]
+    __shared__ float s_h[HID * TILE];                        // h1, then h2 (then critic h3)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int role = blockIdx.y;
     const int e0 = blockIdx.x * TILE;
     const bool critic = role == NAG;
     const int din = critic ? 38 : c_obs_dim[role];
     const int off = critic ? 0 : c_obs_off[role];
     const int dpad = critic ? FJSP_POLICY_CRITIC_DPAD : FJSP_POLICY_ACTOR_DPAD;
-    // inputs
     for (int i = tid; i < dpad * TILE; i += 256) {
         const int k = i / TILE, c = i % TILE;
         s_x[i] = (k < din && e0 + c < n) ? feats[(size_t)(off + k) * n + e0 + c] : 0.0f;
     }
     __syncthreads();
-    const float* W = critic ? critic_w : actor_w + (size_t)role * FJSP_POLICY_ACTOR_FLOATS;
-    const float* W1 = W;                                   // [256][dpad]
-    const float* B1 = W1 + HID * dpad;                     // [256]
-    const float* W2 = B1 + HID;                            // packed [8][128][64]
-    const float* B2 = W2 + HID * HID;                      // [256]
-    // layer 1 (VALU): lane -> env column c, wave -> rows r = wave + 4 i (weights wave-uniform)
-    {
-        const int c = lane;
-        const int wv = __builtin_amdgcn_readfirstlane(wave);
-        float x[40];
-#pragma unroll
-        for (int k = 0; k < 40; k++) x[k] = k < dpad ? s_x[k * TILE + c] : 0.0f;
-        for (int i = 0; i < HID / 4; i++) {
-            const int r = wv + 4 * i;
-            float acc = B1[r];
-#pragma unroll
-            for (int k = 0; k < 40; k++)
-                if (k < dpad) acc = fmaf(W1[r * dpad + k], x[k], acc);
-            s_h1[r * TILE + c] = acc > 0.0f ? acc : 0.0f;
-        }
-    }
-    __syncthreads();
-    // layer 2 (MFMA): wave w -> rows [64w, 64w + 64)
-    {
-        f32x16 acc[2][2];
-#pragma unroll
-        for (int i = 0; i < 2; i++)
-#pragma unroll
-            for (int j = 0; j < 2; j++)
-#pragma unroll
-                for (int r = 0; r < 16; r++) acc[i][j][r] = 0.0f;
-        mfma_rows64(W2, 2 * wave, s_h1, lane, acc);
-#pragma unroll
-        for (int i = 0; i < 2; i++)
-#pragma unroll
-            for (int j = 0; j < 2; j++) store_tile(acc[i][j], 64 * wave + 32 * i, 32 * j, B2, s_h2, lane);
-    }
-    __syncthreads();
     if (critic) {
-        const float* W3 = B2 + HID;                        // packed [4][128][64]
+        hidden256<FJSP_POLICY_CRITIC_DPAD>(critic_w, s_x, s_h, wave, lane);
+        const float* W3 = critic_w + 256 * FJSP_POLICY_CRITIC_DPAD + 256 + 256 * 256 + 256;   // packed [4][32][64][4]
         const float* B3 = W3 + 128 * HID;                  // [128]
         const float* W4 = B3 + 128;                        // [128]
         const float* B4 = W4 + 128;                        // [1]
-        f32x16 acc[2];
-#pragma unroll
-        for (int j = 0; j < 2; j++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) acc[j][r] = 0.0f;
-        const float* a0 = W3 + ((size_t)wave * KS2) * 64 + lane;
-        const int kr = lane >> 5, cl = lane & 31;
-        for (int ks = 0; ks < KS2; ks++) {
-            const float fa = a0[ks * 64];
-            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, s_h2[(2 * ks + kr) * TILE + cl], acc[0], 0, 0, 0);
-            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, s_h2[(2 * ks + kr) * TILE + 32 + cl], acc[1], 0, 0, 0);
-        }
-        // h3 [128][64] reuses s_h1
-        store_tile(acc[0], 32 * wave, 0, B3, s_h1, lane);
-        store_tile(acc[1], 32 * wave, 32, B3, s_h1, lane);
+        f32x16 acc[1][2];
+        zero_acc<1>(acc);
+        mfma_rows<1, 128>(W3, wave, s_h, lane, acc);
+        __syncthreads();
+        store_rows<1>(acc, 32 * wave, B3, s_h, lane);      // h3 [128][64]
         __syncthreads();
         if (tid < TILE && e0 + tid < n) {
             float v = B4[0];
-            for (int k = 0; k < 128; k++) v = fmaf(W4[k], s_h1[k * TILE + tid], v);
+            for (int k = 0; k < 128; k++) v = fmaf(W4[k], s_h[k * TILE + tid], v);
             values[e0 + tid] = v;
         }
         return;
     }
-    // actor layer 3: logits [8][64]; thread -> (action pair, env)
-    const float* W3 = B2 + HID;                            // [8][256]
-    const float* B3 = W3 + 8 * HID;                        // [8]
-    float* s_logit = s_x;                                  // [8][64]
+    const float* W = actor_w + (size_t)role * FJSP_POLICY_ACTOR_FLOATS;
+    hidden256<FJSP_POLICY_ACTOR_DPAD>(W, s_x, s_h, wave, lane);
+    // layer 3: logits [8][64]; thread -> (action pair, env); weights wave-uniform
+    const float* W3 = W + 256 * FJSP_POLICY_ACTOR_DPAD + 256 + 256 * 256 + 256;   // [8][256]
+    const float* B3 = W3 + 8 * HID;                                                // [8]
+    float* s_logit = s_x;
     {
-        const int c = tid & 63, r0 = (tid >> 6) * 2;
+        const int c = lane, r0 = 2 * wave;
         float l0 = B3[r0], l1 = B3[r0 + 1];
         for (int k = 0; k < HID; k++) {
-            const float h = s_h2[k * TILE + c];
+            const float h = s_h[k * TILE + c];
             l0 = fmaf(W3[r0 * HID + k], h, l0);
             l1 = fmaf(W3[(r0 + 1) * HID + k], h, l1);
         }
@@ -201,7 +216,8 @@ __global__ void __launch_bounds__(256) k_policy(const float* __restrict__ feats,
             for (int j = 1; j < na; j++) if (p[j] > best) { best = p[j]; act = j; }
         } else {
             const uint64_t seed = *seedp;
-            const uint64_t h = fmix64(seed ^ fmix64(((uint64_t)(uint32_t)e << 32) | step) ^ (uint64_t)(role + 1) * 0x9E3779B97F4A7C15ull);
+            const uint64_t h = fmix64(seed ^ fmix64(((uint64_t)(uint32_t)e << 32) | step) ^
+                                      (uint64_t)(role + 1) * 0x9E3779B97F4A7C15ull);
             const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
             float cdf[8], tot = 0.0f;
             for (int j = 0; j < na; j++) { tot += p[j]; cdf[j] = tot; }
