@@ -161,8 +161,15 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        # one GPU per rank; FJSP_BENCH_BACKEND=gloo rehearses the multi-rank logic with several
+        # ranks on fewer GPUs (timing collectives only; stepping has no data-path collective)
+        backend = os.environ.get("FJSP_BENCH_BACKEND", "nccl")
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", local % torch.cuda.device_count()))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
