@@ -53,6 +53,7 @@ def parse():
                          "training loop (BASELINE configs 4/5; one bench step = one A2C batch)")
     ap.add_argument("--batch-size", type=int, default=256, help="A2C batch (vector steps per update)")
     ap.add_argument("--no-a2c", action="store_true", help="skip the A2C training-loop leg of the step workload")
+    ap.add_argument("--no-scale", action="store_true", help="skip the 16x-envs leg of the step workload")
     a = ap.parse_args()
     if a.steps is None:
         a.steps = 2000 if a.workload == "step" else 4
@@ -269,6 +270,34 @@ def main():
                     "achieved_GBs": ALGO_BYTES_STEP * N / (kms * 1e-3) / 1e9,
                     "note": "one launch per step, actions u8[8][N] resident in HBM (rank 0)"}
 
+    # the same kernel at 16x the envs (65 536 on this GPU): how far the env-step approaches the
+    # HBM roofline once occupancy allows (the headline stays the 4 096-env workload)
+    scale = None
+    if world == 1 and not args.no_scale:
+        try:
+            NS = 16 * N
+            senv = vec_env.FJSPVecEnv(NS, device=dev)
+            senv.reset(seeds=torch.arange(NS), num_orders=args.num_orders)
+            sbuf = vec_env.Buffers(chunk, NS, dev, infos=False)
+            senv.rollout(chunk, action_seed=1234, masked=args.masked, buffers=sbuf)
+            torch.cuda.synchronize()
+            sms = []
+            for r in range(3):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                senv.rollout(chunk, action_seed=1234, step0=(r + 1) * chunk, masked=args.masked, buffers=sbuf)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                sms.append(e0.elapsed_time(e1))
+            sm = float(np.mean(sms))
+            sach = ALGO_BYTES_FUSED * NS * chunk / (sm * 1e-3) / 1e9
+            scale = {"envs": NS, "value": NS * chunk / (sm * 1e-3), "unit": "env-steps/s",
+                     "avg_launch_ms": sm, "kernel": senv.last_kernel(), "achieved_GBs": sach,
+                     "frac": sach / HBM_PEAK_GBS, "steps_per_launch": chunk}
+            del senv, sbuf
+        except Exception as e:
+            scale = {"error": f"{type(e).__name__}: {e}"}
+
     a2c = None
     if world == 1 and not args.no_a2c:
         try:
@@ -319,6 +348,7 @@ def main():
             "cpu_baseline": cpu,
             "per_step_launch": per_step,
             "a2c_training": a2c,
+            "scale_16x_envs": scale,
             "state_bytes_per_env": env.state_bytes_per_env(),
         }
         print(json.dumps(out), flush=True)
