@@ -874,6 +874,14 @@ FJSP_DEV void flag_obs_overflow(Env& E) {
     if (ov) E.flag(ST_OBS_OVERFLOW | ST_DIVERGED);
 }
 
+// calculate_global_reward (utils/RewardModel.py:34-44) / len(self.agents), Python op order.
+FJSP_DEV double global_reward8(const Cfg& C, int orders_done, int packaged) {
+    double g = C.lut[80] * (double)orders_done;
+    g += C.lut[81] * (double)packaged;
+    g += C.lut[82];
+    return g / 8.0;
+}
+
 // Actions in dict order, then env.run in closed form.  actions[a] for agent a (canonical order);
 // order = execution order (CANON -> 0..7).  Fills res[8]; returns the shared global reward / 8.
 template <bool CANON>
@@ -917,10 +925,7 @@ FJSP_DEV double env_advance(Env& E, const Tables& T, const Cfg& C, const int* ac
     E.set_ncompleted(E.ncompleted() + orders_done);
     FJSP_STAMP(E, 2);
     // 3. calculate_global_reward; combine_rewards divides it by len(self.agents)
-    double g = C.lut[80] * (double)orders_done;
-    g += C.lut[81] * (double)(E.total_packaged() - products_before);
-    g += C.lut[82];
-    return g / 8.0;
+    return global_reward8(C, orders_done, E.total_packaged() - products_before);
 }
 
 // One step with rewards (host harness / tests): r_a = g / 8 + local_a (combine_rewards).

@@ -522,29 +522,42 @@ __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, u
 #endif
 }
 
-// K fused steps, pipelined over two wavefronts per 64-env workgroup (lean outputs only).
+// K fused steps, pipelined over 2 or 3 wavefronts per 64-env workgroup (lean outputs only).
 // Wave 0 ("sim") advances the env state: actions, action phase, SimPy run, auto-reset; after
-// each step it leaves a snapshot of the pre-reset state (30 words), the 8 reward-table indices
-// and g/8 in LDS.  Wave 1 ("emit"), on another SIMD of the same CU, turns snapshot k into the
-// outputs of step k (rewards, observation, masks, term, trunc, status) while wave 0 already
-// computes step k+1, and precomputes the next step's actions when they do not depend on the
-// state (uniform random mode).  Snapshots and action slots are double-buffered; one
-// workgroup barrier per step orders them.
+// each step it leaves a snapshot of the pre-reset state (the 22 words the observation reads),
+// the 8 action-result words and the step's completed orders / packaged products in LDS.  The
+// emit wave(s), on other SIMDs of the same CU, turn snapshot k into the outputs of step k
+// (rewards, observation, masks, term, trunc, status) while wave 0 already computes step k+1,
+// and precompute the next step's actions when they do not depend on the state (uniform
+// random mode).  Snapshots and action slots are double-buffered; one workgroup barrier per
+// step orders them.
+// Output sink of one emit wave: part 0 stores the int32 and float32 observation fields, part 1
+// the int8 fields and the masks (the other part's values are dead code and never computed);
+// part -1 stores everything.
+template <int PART>
+struct PartSink {
+    StoreSink s;
+    __device__ __forceinline__ void i32(int f, int v) { if (PART <= 0) s.i32(f, v); }
+    __device__ __forceinline__ void f32(int f, float v) { if (PART <= 0) s.f32(f, v); }
+    __device__ __forceinline__ void i8(int f, int v) { if (PART != 0) s.i8(f, v); }
+    __device__ __forceinline__ void mask(int f, int v) { if (PART != 0) s.mask(f, v); }
+};
+
 // State words the observation / masks / term / trunc / status read (observe, compute_masks):
 // all but the MT cursor (W3), the packaging run lists (W13-16), the machines' next-event steps
 // (W19) and the packaging completion counters (W24-25).
 constexpr uint32_t SNAP_WORDS = ((1u << NSTATE) - 1u) & ~((1u << 3) | (0xFu << 13) | (1u << 19) | (3u << 24));
 struct alignas(16) PipeSnap {
-    double g8[BLOCK];
     uint32_t w[NSTATE][BLOCK];
-    uint32_t ridx[2][BLOCK];   // reward_index of agents 0..3 / 4..7, one byte each
+    uint32_t res[NA][BLOCK];   // action-result words, the agent's action in bits 8..11
+    uint32_t gstat[BLOCK];     // orders completed | products packaged << 16 this step
 };
 __device__ __forceinline__ uint32_t pack_actions(const int* act, int lo) {
     return (uint32_t)act[lo] | ((uint32_t)act[lo + 1] << 8) | ((uint32_t)act[lo + 2] << 16) | ((uint32_t)act[lo + 3] << 24);
 }
 
-template <bool LDS>
-__global__ void __launch_bounds__(2 * BLOCK) k_step_pipe(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0,
+template <bool LDS, int NEMIT>
+__global__ void __launch_bounds__((1 + NEMIT) * BLOCK) k_step_pipe(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0,
                                                          uint32_t step0, int mode, int autoreset, fjsp_out out) {
     __shared__ uint32_t s_orders[LDS ? MAX_ORDERS * BLOCK : 1];
     __shared__ uint16_t s_code[LDS ? MAX_SLOTS * BLOCK : 1];
@@ -554,7 +567,7 @@ __global__ void __launch_bounds__(2 * BLOCK) k_step_pipe(DevState S, Cfg C, int 
     __shared__ uint32_t s_act[2][2][BLOCK];
     __shared__ uint32_t s_mtbuf[MTB * BLOCK];
     __shared__ double s_lut[RLUT_SIZE];
-    for (int i = threadIdx.x; i < RLUT_SIZE; i += 2 * BLOCK) s_lut[i] = C.lut[i];
+    for (int i = threadIdx.x; i < RLUT_SIZE; i += (1 + NEMIT) * BLOCK) s_lut[i] = C.lut[i];
     C.lut = s_lut;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / BLOCK);
     const int lane = threadIdx.x % BLOCK;
@@ -604,21 +617,16 @@ __global__ void __launch_bounds__(2 * BLOCK) k_step_pipe(DevState S, Cfg C, int 
                 }
                 FJSP_STAMP(E, 0);
                 uint32_t res[NA];
-                const double g8 = env_advance<true>(E, T, C, act, nullptr, res);
+                const int nc0 = E.ncompleted(), tp0 = E.total_packaged();
+                (void)env_advance<true>(E, T, C, act, nullptr, res);   // g/8: the emit wave
                 flag_obs_overflow(E);
                 PipeSnap& sp = snap[k & 1];
-                sp.g8[lane] = g8;
 #pragma unroll
                 for (int i = 0; i < NSTATE; i++)
                     if ((SNAP_WORDS >> i) & 1u) sp.w[i][lane] = E.w[i];
-                uint32_t r0 = 0, r1 = 0;
 #pragma unroll
-                for (int a = 0; a < 4; a++) {
-                    r0 |= reward_index(a, res[a], act[a]) << (8 * a);
-                    r1 |= reward_index(4 + a, res[4 + a], act[4 + a]) << (8 * a);
-                }
-                sp.ridx[0][lane] = r0;
-                sp.ridx[1][lane] = r1;
+                for (int a = 0; a < NA; a++) sp.res[a][lane] = res[a] | ((uint32_t)act[a] << 8);
+                sp.gstat[lane] = (uint32_t)(E.ncompleted() - nc0) | ((uint32_t)(E.total_packaged() - tp0) << 16);
                 const int nord = E.norders();
                 const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
                 const int truncated = E.step() >= C.max_steps;
@@ -646,6 +654,10 @@ __global__ void __launch_bounds__(2 * BLOCK) k_step_pipe(DevState S, Cfg C, int 
             for (int i = 0; i < 8; i++) atomicAdd((unsigned long long*)&g_stamps[i], (unsigned long long)E.st_acc[i]);
 #endif
     } else {
+        // NEMIT == 2: two emit waves split the outputs: wave 1 rewards + int32 / float32
+        // observation fields (+ the next step's uniform actions), wave 2 int8 fields, masks,
+        // term, trunc, status.  NEMIT == 1 (many envs: the CUs are already full): one wave.
+        const int part = wave - 1;
         for (int k = 0; k <= K; k++) {
             if (k > 0 && valid) {
                 const uint32_t t = (uint32_t)(k - 1);
@@ -653,25 +665,35 @@ __global__ void __launch_bounds__(2 * BLOCK) k_step_pipe(DevState S, Cfg C, int 
                 Env E;
 #pragma unroll
                 for (int i = 0; i < NSTATE; i++) E.w[i] = ((SNAP_WORDS >> i) & 1u) ? sp.w[i][lane] : 0u;
-                const double g8 = sp.g8[lane];
-                if (out.rewards) {
-                    const uint32_t r0 = sp.ridx[0][lane], r1 = sp.ridx[1][lane];
+                const StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, ue};
+                if (part == 0) {   // rewards (+ everything when NEMIT == 1)
+                    if (out.rewards) {
+                        const uint32_t gs = sp.gstat[lane];
+                        const double g8 = global_reward8(C, (int)(gs & 0xFFFFu), (int)(gs >> 16));
 #pragma unroll
-                    for (int a = 0; a < NA; a++) {
-                        const uint32_t idx = ((a < 4 ? r0 : r1) >> (8 * (a & 3))) & 0xFFu;
-                        st32(out.rewards, (t * NA + (uint32_t)a) * n + ue, g8 + C.lut[idx]);
+                        for (int a = 0; a < NA; a++) {
+                            const uint32_t r = sp.res[a][lane];
+                            st32(out.rewards, (t * NA + (uint32_t)a) * n + ue,
+                                 g8 + C.lut[reward_index(a, r & 0xFFFF00FFu, (int)((r >> 8) & 0xFu))]);
+                        }
                     }
+                    PartSink<NEMIT == 1 ? -1 : 0> ps{sink};
+                    observe(E, C, ps);
                 }
-                StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, ue};
-                observe(E, C, sink);
-                const int nord = E.norders();
-                const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
-                const int truncated = E.step() >= C.max_steps;
-                if (out.term) st32(out.term, t * n + ue, (uint8_t)all_done);
-                if (out.trunc) st32(out.trunc, t * n + ue, (uint8_t)truncated);
-                if (out.status) st32(out.status, t * n + ue, E.status());
+                if (part == NEMIT - 1) {   // int8 fields, masks, term, trunc, status
+                    if (NEMIT == 2) {
+                        PartSink<1> ps{sink};
+                        observe(E, C, ps);
+                    }
+                    const int nord = E.norders();
+                    const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
+                    const int truncated = E.step() >= C.max_steps;
+                    if (out.term) st32(out.term, t * n + ue, (uint8_t)all_done);
+                    if (out.trunc) st32(out.trunc, t * n + ue, (uint8_t)truncated);
+                    if (out.status) st32(out.status, t * n + ue, E.status());
+                }
             }
-            if (pre && k + 1 < K) {
+            if (part == 0 && pre && k + 1 < K) {
                 int act[NA];
                 synth_uniform(seed, gid0 + (uint32_t)e, step0 + (uint32_t)(k + 1), act);
                 s_act[(k + 1) & 1][0][lane] = pack_actions(act, 0);
@@ -999,17 +1021,22 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
                         al16(o.status);
     // LDS tables (97.5 KB per 64-env workgroup) pay while every workgroup has a CU of its own
     const bool lds = h->use_lds < 0 ? h->n <= 256 * BLOCK : h->use_lds != 0;
-    h->last_kernel = (h->use_pipe && !full && !staged) ? (lds ? "k_step_pipe<lds>" : "k_step_pipe")
+    const bool two_emit = h->n <= 256 * BLOCK;
+    h->last_kernel = (h->use_pipe && !full && !staged)
+                         ? (lds ? (two_emit ? "k_step_pipe<lds,2emit>" : "k_step_pipe<lds,1emit>")
+                                : (two_emit ? "k_step_pipe<2emit>" : "k_step_pipe<1emit>"))
                    : full ? (lds ? "k_step_many<lds,full>" : "k_step_many<full>")
                    : staged ? (lds ? "k_step_many<lds,staged>" : "k_step_many<staged>")
                    : (lds ? "k_step_many<lds>" : "k_step_many");
     if (h->use_pipe && !full && !staged) {
-        if (lds)
-            hipLaunchKernelGGL(k_step_pipe<true>, grid, dim3(2 * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed,
-                               env_gid0, step0, action_mode, autoreset, o);
-        else
-            hipLaunchKernelGGL(k_step_pipe<false>, grid, dim3(2 * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed,
-                               env_gid0, step0, action_mode, autoreset, o);
+        // a second emit wave pays while the CUs are not full (N <= 16384 at 64 envs per CU)
+        const bool two = two_emit;
+        auto launch_pipe = [&](auto kern, int waves) {
+            hipLaunchKernelGGL(kern, grid, dim3(waves * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0,
+                               step0, action_mode, autoreset, o);
+        };
+        if (lds) two ? launch_pipe(k_step_pipe<true, 2>, 3) : launch_pipe(k_step_pipe<true, 1>, 2);
+        else two ? launch_pipe(k_step_pipe<false, 2>, 3) : launch_pipe(k_step_pipe<false, 1>, 2);
     } else if (lds) {
         if (full) launch(k_step_many<true, true>);
         else if (staged) launch(k_step_many<true, false, true>);

@@ -291,3 +291,19 @@ def test_pipelined_matches_single_wave(G, policy):
             assert P.bits_equal(outs[0][0][k], o[0][k]), k
         for k in outs[0][1]:
             assert P.bits_equal(outs[0][1][k], o[1][k]), k
+
+
+def test_pipelined_single_emit_wave_large_n(G):
+    """N > 16384 takes the one-emit-wave pipelined variant (global tables): same bytes as the
+    single-wave kernel."""
+    n, steps = 16448, 60
+    outs = []
+    for pipe in (1, 0):
+        env = G.make_env(n)
+        G.native.check(G.native.lib().fjsp_set_option(env.handle, b"pipeline", pipe))
+        env.reset(seeds=torch.arange(n), num_orders=10)
+        outs.append(G.to_np(env.rollout(steps, action_seed=8, masked=True)))
+        if pipe:
+            assert env.last_kernel() == "k_step_pipe<1emit>"
+    for k in outs[0]:
+        assert P.bits_equal(outs[0][k], outs[1][k]), k
