@@ -21,7 +21,7 @@ def per_kernel(path, kernel, grid):
     vals = []
     with open(path) as f:
         for row in csv.DictReader(f):
-            if row["Kernel_Name"].startswith(kernel) and int(row["Grid_Size"]) in (grid, 2 * grid):
+            if row["Kernel_Name"].startswith(kernel) and int(row["Grid_Size"]) in (grid, 2 * grid, 3 * grid):
                 vals.append(float(row["Counter_Value"]))
     return vals
 
