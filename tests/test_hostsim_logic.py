@@ -136,3 +136,36 @@ def test_heuristic_vs_oracle_rollout(L):
             assert mine.tobytes() == np.ascontiguousarray(rec[t][name]).tobytes(), (t, name)
         done += int(hs.term.sum())
     assert done > 0   # the heuristic finishes small episodes
+
+
+def test_property_random_configs_and_actions(L):
+    """Property test (hypothesis): the kernel's state machine equals the oracle's event heap on
+    random valid configurations and arbitrary action streams, including out-of-range actions."""
+    hyp = pytest.importorskip("hypothesis")
+    st = hyp.strategies
+
+    @hyp.settings(max_examples=25, deadline=None, derandomize=True)
+    @hyp.given(seed=st.integers(0, 2**31 - 1), norders=st.integers(0, 12),
+               tray_cap=st.integers(1, 7), storage=st.integers(0, 6), trays=st.integers(1, 60),
+               step=st.sampled_from([10, 20]), acts=st.lists(st.lists(st.integers(0, 9), min_size=8, max_size=8),
+                                                             min_size=40, max_size=120))
+    def run(seed, norders, tray_cap, storage, trays, step, acts):
+        cfg = {"tray_capacity": tray_cap, "mask_tray_capacity": tray_cap, "storage_capacity": storage,
+               "num_trays": trays, "step_size": step, "pt_small": 6 * step, "pt_big": 12 * step,
+               "pt_packaging": 3 * step}
+        hs = HS(L, 1, cfg)
+        hs.reset([seed], norders)
+        o = O.OracleEnv(**cfg)
+        o.reset(seed=seed, num_orders=norders)
+        for a in acts:
+            a = np.array(a, np.uint8)
+            hs.step(a[None])
+            r = o.step(a)
+            if r["status"] & (O.ST_EXCEPTION | O.ST_PKG_WAIT | O.ST_OBS_OVERFLOW):
+                break
+            for name, mine in (("obs_i32", hs.i32), ("obs_i8", hs.i8), ("masks", hs.mk), ("rewards", hs.rew),
+                               ("results", hs.res)):
+                assert np.ascontiguousarray(mine[0]).tobytes() == np.ascontiguousarray(r[name]).tobytes(), name
+            if r["term"] or r["trunc"]:
+                o.reset(num_orders=norders)
+    run()
