@@ -583,6 +583,7 @@ __global__ void __launch_bounds__((1 + NEMIT) * BLOCK) k_step_pipe(DevState S, C
     }
     __syncthreads();
     if (wave == 0) {
+        __builtin_amdgcn_s_setprio(3);   // the sim wave is the critical path: win shared issue slots
         Env E;
         if (valid) env_load(E, S.words, S.n, e);
         Tables T = tables_of(S, valid ? e : 0);
