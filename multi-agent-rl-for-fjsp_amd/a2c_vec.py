@@ -395,8 +395,7 @@ class VecMultiAgentA2C:
         rc = nat.lib().fjsp_a2c_policy(P(feats), P(masks), int(feats.shape[-1]), P(self._pw_actor),
                                        P(self._pw_critic), P(self._rng), int(t), int(bool(deterministic)),
                                        P(act_out), P(val_out), P(probs_out), ctypes.c_void_p(stream))
-        if rc != 0:
-            raise nat.FjspNativeError(f"fjsp_a2c_policy failed ({rc})")
+        nat.check(rc)
 
     def repack(self):
         """Refresh the fused kernel's packed weights (after an update / load)."""

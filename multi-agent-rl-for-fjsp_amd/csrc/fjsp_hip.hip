@@ -547,11 +547,28 @@ struct PartSink {
 // all but the MT cursor (W3), the packaging run lists (W13-16), the machines' next-event steps
 // (W19) and the packaging completion counters (W24-25).
 constexpr uint32_t SNAP_WORDS = ((1u << NSTATE) - 1u) & ~((1u << 3) | (0xFu << 13) | (1u << 19) | (3u << 24));
+// Snapshot slot: 32 words per lane = the 22 observed state words (SNAP_WORDS, in word order),
+// the 8 action-result words (action in bits 8..11) and the step's completed orders | packaged
+// products << 16, stored lane-major as 8 uint4 per lane (16-byte LDS accesses, conflict-free:
+// consecutive lanes 16 bytes apart within each 1 KB row).
+constexpr int SNAP_N = 32;
+static_assert(__builtin_popcount(SNAP_WORDS) + NA + 1 <= SNAP_N, "snapshot slot");
 struct alignas(16) PipeSnap {
-    uint32_t w[NSTATE][BLOCK];
-    uint32_t res[NA][BLOCK];   // action-result words, the agent's action in bits 8..11
-    uint32_t gstat[BLOCK];     // orders completed | products packaged << 16 this step
+    uint4 q[SNAP_N / 4][BLOCK];
 };
+__device__ __forceinline__ void snap_put(PipeSnap& sp, int lane, const uint32_t* v) {
+#pragma unroll
+    for (int g = 0; g < SNAP_N / 4; g++) sp.q[g][lane] = make_uint4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+}
+__device__ __forceinline__ void snap_get(const PipeSnap& sp, int lane, uint32_t* v) {
+#pragma unroll
+    for (int g = 0; g < SNAP_N / 4; g++) {
+        const uint4 x = sp.q[g][lane];
+        v[4 * g] = x.x; v[4 * g + 1] = x.y; v[4 * g + 2] = x.z; v[4 * g + 3] = x.w;
+    }
+}
+constexpr int SNAP_RES = __builtin_popcount(SNAP_WORDS), SNAP_GSTAT = SNAP_RES + NA;
+
 __device__ __forceinline__ uint32_t pack_actions(const int* act, int lo) {
     return (uint32_t)act[lo] | ((uint32_t)act[lo + 1] << 8) | ((uint32_t)act[lo + 2] << 16) | ((uint32_t)act[lo + 3] << 24);
 }
@@ -621,13 +638,17 @@ __global__ void __launch_bounds__((1 + NEMIT) * BLOCK) k_step_pipe(DevState S, C
                 const int nc0 = E.ncompleted(), tp0 = E.total_packaged();
                 (void)env_advance<true>(E, T, C, act, nullptr, res);   // g/8: the emit wave
                 flag_obs_overflow(E);
-                PipeSnap& sp = snap[k & 1];
+                uint32_t v[SNAP_N];
+                int j = 0;
 #pragma unroll
                 for (int i = 0; i < NSTATE; i++)
-                    if ((SNAP_WORDS >> i) & 1u) sp.w[i][lane] = E.w[i];
+                    if ((SNAP_WORDS >> i) & 1u) v[j++] = E.w[i];
 #pragma unroll
-                for (int a = 0; a < NA; a++) sp.res[a][lane] = res[a] | ((uint32_t)act[a] << 8);
-                sp.gstat[lane] = (uint32_t)(E.ncompleted() - nc0) | ((uint32_t)(E.total_packaged() - tp0) << 16);
+                for (int a = 0; a < NA; a++) v[SNAP_RES + a] = res[a] | ((uint32_t)act[a] << 8);
+                v[SNAP_GSTAT] = (uint32_t)(E.ncompleted() - nc0) | ((uint32_t)(E.total_packaged() - tp0) << 16);
+#pragma unroll
+                for (int i = SNAP_GSTAT + 1; i < SNAP_N; i++) v[i] = 0u;
+                snap_put(snap[k & 1], lane, v);
                 const int nord = E.norders();
                 const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
                 const int truncated = E.step() >= C.max_steps;
@@ -662,18 +683,20 @@ __global__ void __launch_bounds__((1 + NEMIT) * BLOCK) k_step_pipe(DevState S, C
         for (int k = 0; k <= K; k++) {
             if (k > 0 && valid) {
                 const uint32_t t = (uint32_t)(k - 1);
-                const PipeSnap& sp = snap[(k - 1) & 1];
+                uint32_t v[SNAP_N];
+                snap_get(snap[(k - 1) & 1], lane, v);
                 Env E;
+                int j = 0;
 #pragma unroll
-                for (int i = 0; i < NSTATE; i++) E.w[i] = ((SNAP_WORDS >> i) & 1u) ? sp.w[i][lane] : 0u;
+                for (int i = 0; i < NSTATE; i++) E.w[i] = ((SNAP_WORDS >> i) & 1u) ? v[j++] : 0u;
                 const StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, ue};
                 if (part == 0) {   // rewards (+ everything when NEMIT == 1)
                     if (out.rewards) {
-                        const uint32_t gs = sp.gstat[lane];
+                        const uint32_t gs = v[SNAP_GSTAT];
                         const double g8 = global_reward8(C, (int)(gs & 0xFFFFu), (int)(gs >> 16));
 #pragma unroll
                         for (int a = 0; a < NA; a++) {
-                            const uint32_t r = sp.res[a][lane];
+                            const uint32_t r = v[SNAP_RES + a];
                             st32(out.rewards, (t * NA + (uint32_t)a) * n + ue,
                                  g8 + C.lut[reward_index(a, r & 0xFFFF00FFu, (int)((r >> 8) & 0xFu))]);
                         }
@@ -759,6 +782,12 @@ struct fjsp_handle {
 };
 
 static thread_local std::string g_err;
+
+// shared with the other translation unit of the library (fjsp_policy.hip)
+int fjsp_internal_fail(const char* msg) {
+    g_err = msg;
+    return -1;
+}
 
 static int fail(const char* msg) {
     g_err = msg;

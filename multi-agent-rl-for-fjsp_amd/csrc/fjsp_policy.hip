@@ -233,12 +233,21 @@ __global__ void __launch_bounds__(256, 2) k_policy(const float* __restrict__ fea
 
 }  // namespace
 
+int fjsp_internal_fail(const char* msg);   // fjsp_hip.hip: sets fjsp_last_error()
+
 extern "C" int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const float* actor_w,
                                const float* critic_w, const uint64_t* seed, uint32_t step, int32_t deterministic,
                                uint8_t* actions, float* values, float* probs, void* stream) {
-    if (n <= 0 || !feats || !masks || !actor_w || !critic_w || !seed || !actions || !values) return -1;
+    if (n <= 0) return fjsp_internal_fail("fjsp_a2c_policy: n must be > 0");
+    if (!feats || !masks || !actor_w || !critic_w || !seed || !actions || !values)
+        return fjsp_internal_fail("fjsp_a2c_policy: null buffer");
     dim3 grid((n + TILE - 1) / TILE, NAG + 1);
     hipLaunchKernelGGL(k_policy, grid, dim3(256), 0, (hipStream_t)stream, feats, masks, n, actor_w, critic_w, seed, step,
                        deterministic, actions, values, probs);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
 }
