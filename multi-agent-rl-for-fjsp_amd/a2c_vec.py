@@ -519,6 +519,56 @@ class VecMultiAgentA2C:
             steps += self.batch_size * self.N
         return self
 
+    @torch.no_grad()
+    def test(self, num_orders=5, max_steps=500, seeds=None, deterministic=True, trace=False, env=None,
+             use_heuristic=False):
+        """MultiAgentA2C.test (a2c.py:539-645) with the learned policy on every env: greedy
+        actions (deterministic) until each env's episode ends or max_steps.  Returns per-env
+        numpy arrays as the reference's test() dict (+ the actions [T, 8, N] with trace).
+        Runs on `env` (a separate FJSPVecEnv, as the reference builds a fresh test env) or,
+        by default, resets the training env (the next collect() starts new episodes)."""
+        import numpy as np
+        from .vec_env import Buffers
+        env = self.env if env is None else env
+        if use_heuristic:
+            return env.evaluate("heuristic", num_orders=num_orders, max_steps=max_steps, seeds=seeds)
+        N = env.num_envs
+        env.reset(seeds=seeds, num_orders=num_orders)
+        feats, masks = env.pack_a2c()
+        b = Buffers(1, N, self.device, infos=True, feats=True)
+        act = torch.zeros(NA, N, dtype=torch.uint8, device=self.device)
+        val = torch.zeros(N, dtype=torch.float32, device=self.device)
+        alive = torch.ones(N, dtype=torch.bool, device=self.device)
+        steps = torch.zeros(N, dtype=torch.int64, device=self.device)
+        by_agent = torch.zeros(NA, N, dtype=torch.float64, device=self.device)
+        oc = torch.zeros(N, dtype=torch.int64, device=self.device)
+        pk = torch.zeros(N, dtype=torch.int64, device=self.device)
+        acts = []
+        for t in range(int(max_steps)):
+            if self.fused_policy:
+                self.policy_fused(feats, masks, t, deterministic, act, val)
+            else:
+                act.copy_(self.policy(feats, masks, deterministic)[0])
+            if trace:
+                acts.append(act.cpu().numpy().copy())
+            env.step(act, autoreset=False, buffers=b)
+            by_agent += torch.where(alive, b.rewards[0], torch.zeros_like(by_agent))
+            steps += alive.long()
+            oc = torch.where(alive, b.orders_completed[0].long(), oc)
+            pk = torch.where(alive, b.packaged[0].long(), pk)
+            alive &= ~(b.term[0].bool() | b.trunc[0].bool())
+            feats.copy_(b.feats[0])
+            masks.copy_(b.masks[0])
+            if not bool(alive.any()):
+                break
+        by_agent = by_agent.cpu().numpy()
+        res = {"steps": steps.cpu().numpy(), "orders_completed": oc.cpu().numpy(),
+               "products_packaged": pk.cpu().numpy(), "total_orders": num_orders,
+               "rewards_by_agent": by_agent, "total_reward": np.cumsum(by_agent, axis=0)[-1]}
+        if trace:
+            res["actions"] = np.stack(acts) if acts else np.zeros((0, NA, N), np.uint8)
+        return res
+
     # ------------------------------------------------------------ checkpoints (a2c.py:733-775)
     def state_dicts(self):
         return {

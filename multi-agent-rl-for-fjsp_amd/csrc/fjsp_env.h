@@ -21,6 +21,13 @@
 #ifndef FJSP_DEV
 #define FJSP_DEV __device__ __forceinline__
 #endif
+#ifndef FJSP_HD   // small maps the host side of the library uses too
+#ifdef __HIP__
+#define FJSP_HD __host__ __device__ __forceinline__
+#else
+#define FJSP_HD FJSP_DEV
+#endif
+#endif
 
 namespace fjsp {
 
@@ -44,11 +51,11 @@ constexpr uint32_t nibs(int a0, int a1, int a2, int a3, int a4, int a5, int a6 =
     return (uint32_t)a0 | ((uint32_t)a1 << 4) | ((uint32_t)a2 << 8) | ((uint32_t)a3 << 12) | ((uint32_t)a4 << 16) |
            ((uint32_t)a5 << 20) | ((uint32_t)a6 << 24) | ((uint32_t)a7 << 28);
 }
-FJSP_DEV int nib(uint32_t table, int i) { return (int)((table >> (4 * i)) & 0xFu); }
+FJSP_HD int nib(uint32_t table, int i) { return (int)((table >> (4 * i)) & 0xFu); }
 constexpr uint32_t ROW_TAB = nibs(0, 0, 0, 2, 3, 3);   // location -> grid row
 constexpr uint32_t COL_TAB = nibs(0, 0, 3, 3, 0, 5);   // location -> grid column
-FJSP_DEV int loc_row(int l) { return nib(ROW_TAB, l); }
-FJSP_DEV int loc_col(int l) { return nib(COL_TAB, l); }
+FJSP_HD int loc_row(int l) { return nib(ROW_TAB, l); }
+FJSP_HD int loc_col(int l) { return nib(COL_TAB, l); }
 // AGV move action a (1..5) -> location (AGVAgent.py:218-224)
 constexpr uint32_t MOVE_TAB = nibs(0, LOC_PICKUP, LOC_SMALL, LOC_BIG, LOC_STORAGE, LOC_PACK);
 FJSP_DEV int move_loc(int a) { return nib(MOVE_TAB, a & 7); }

@@ -1215,10 +1215,9 @@ int fjsp_read_env(fjsp_handle* h, int32_t env, fjsp_env_view* v) {
     HIPCHK(hipStreamSynchronize(h->stream));
     uint32_t w[NWORDS];
     uint32_t orders[MAX_ORDERS];
-    for (int i = 0; i < NWORDS; i++)
-        HIPCHK(hipMemcpy(&w[i], h->S.words + (size_t)i * h->n + env, 4, hipMemcpyDeviceToHost));
-    for (int i = 0; i < MAX_ORDERS; i++)
-        HIPCHK(hipMemcpy(&orders[i], h->S.orders + (size_t)i * h->n + env, 4, hipMemcpyDeviceToHost));
+    // one strided copy per table (column `env` of the [rows][N] SoA arrays)
+    HIPCHK(hipMemcpy2D(w, 4, h->S.words + env, (size_t)h->n * 4, 4, NWORDS, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy2D(orders, 4, h->S.orders + env, (size_t)h->n * 4, 4, MAX_ORDERS, hipMemcpyDeviceToHost));
     memset(v, 0, sizeof(*v));
     v->current_step = (int32_t)(w[0] & 0xFFFF);
     v->num_orders = (int32_t)((w[0] >> 16) & 0xFF);
@@ -1227,8 +1226,8 @@ int fjsp_read_env(fjsp_handle* h, int32_t env, fjsp_env_view* v) {
     v->total_packaged = (int32_t)(w[1] >> 8);
     v->status = w[2];
     const int loc = (int)(w[6] & 7), carry = (int)((w[6] >> 3) & 0xFF), code = (int)((w[6] >> 11) & 0x1FFF);
-    v->agv_row = loc == LOC_SMALL ? 2 : (loc >= LOC_STORAGE ? 3 : 0);
-    v->agv_col = (loc == LOC_PICKUP || loc == LOC_STORAGE) ? 0 : (loc == LOC_PACK ? 5 : 3);
+    v->agv_row = loc_row(loc);
+    v->agv_col = loc_col(loc);
     v->agv_carrying = carry != NIL;
     v->agv_tray_count = carry != NIL ? (code >> 10) & 7 : 0;
     for (int i = 0; i < v->num_orders && i < MAX_ORDERS; i++) {

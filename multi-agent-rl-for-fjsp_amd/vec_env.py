@@ -174,6 +174,28 @@ class FJSPVecEnv:
                                            int(step0), mode, int(bool(autoreset)), ctypes.byref(out)))
         return b
 
+    def evaluate(self, policy="heuristic", num_orders=5, max_steps=500, seeds=None, action_seed=0):
+        """MultiAgentA2C.test (a2c.py:539-645) for every env at once: each env runs from a reset
+        until its episode ends (term or trunc: the reference's `while env.agents`) or max_steps.
+        Returns the reference's test() dict with one entry per env: steps, orders_completed,
+        products_packaged, rewards_by_agent [8, N] (each agent's rewards summed in step order,
+        as episode_rewards) and total_reward (their sum in agent order, a2c.py:626)."""
+        import numpy as np
+        self.reset(seeds=seeds, num_orders=num_orders)
+        b = self.rollout(int(max_steps), action_seed=action_seed, policy=policy, autoreset=False, infos=True)
+        done = (b.term | b.trunc).cpu().numpy().astype(bool)                  # [T, N]
+        T = done.shape[0]
+        first = np.where(done.any(0), done.argmax(0) + 1, T)                  # steps run per env
+        live = np.arange(T)[:, None] < first[None, :]
+        rew = np.where(live[:, None, :], b.rewards.cpu().numpy(), 0.0)        # [T, 8, N]
+        by_agent = np.cumsum(rew, axis=0)[-1] if T else np.zeros((NA, self.num_envs))   # sequential
+        idx = np.maximum(first - 1, 0)
+        cols = np.arange(self.num_envs)
+        pick = lambda x: x.cpu().numpy()[idx, cols] if T else np.zeros(self.num_envs, np.int32)  # noqa: E731
+        return {"steps": first, "orders_completed": pick(b.orders_completed),
+                "products_packaged": pick(b.packaged), "total_orders": num_orders,
+                "rewards_by_agent": by_agent, "total_reward": np.cumsum(by_agent, axis=0)[-1]}
+
     def pack_a2c(self, feats=None, masks=None):
         """a2c features f32 [38, N] and masks int8 [29, N] of the current observations
         (MultiAgentA2C._get_global_state, a2c.py:153-166)."""
