@@ -32,6 +32,7 @@ constexpr int BLOCK = 64;
 constexpr int MT_N = 624;
 #ifdef FJSP_STAMPS
 __device__ unsigned long long g_stamps[8];
+__device__ unsigned long long g_pgstamps[4];   // pre-draw wave: busy cycles, active steps, busy in active steps, steps
 #endif
 
 struct DevState {
@@ -40,7 +41,8 @@ struct DevState {
     uint16_t* scode;
     uint8_t* snext;
     uint16_t* scstep;
-    uint32_t* mt;
+    uint32_t* mt;       // [2][n][624] MT rows (live one selected by W3 bit 31)
+    uint32_t* nxt;      // [MAX_ORDERS][n] pre-drawn next order tables (W[PGW])
     int n;
 };
 
@@ -81,99 +83,128 @@ __device__ void mt_seed(uint32_t* __restrict__ mt, int e, uint32_t seed) {
     }
 }
 
-// Batched reader of the lazily twisted stream for resets.  A refill starts at the 16-byte
-// aligned word pa = pos & ~3 and loads the words it needs as two runs of nine uint4 (words
-// [pa, pa+36) and [pa+396, pa+432), wrapped into the row; 624 is a multiple of 4 so no uint4
-// straddles the wrap), regenerates and tempers MTB words into the lane's LDS buffer `buf`
-// (stride BLOCK) and writes the regenerated words back; the pos - pa words already consumed
-// are skipped (bi starts at pos - pa).  Consumption (the rejection loops, divergent across
-// lanes) only reads LDS; refills happen at one wave-uniform point.
+// Batched reader of the lazily twisted stream for resets.  A refill of B words starts at the
+// 16-byte aligned word pa = pos & ~3 and loads the words it needs as two runs of B/4 + 1 uint4
+// (words [pa, pa+B+4) and [pa+396, pa+B+400), wrapped into the row; 624 is a multiple of 4
+// so no uint4 straddles the wrap), regenerates the words at or past g, writes the batch back
+// as uint4 (words before g are written back unchanged) and returns the B tempered words in
+// registers; the pos - pa words before pos are skipped by the consumer.  cnt = words of the
+// batch inside the row (a multiple of 4; a batch never crosses the wrap).
 constexpr int MTB = 32;
-struct MtReader {
-    uint32_t* mt;
-    uint32_t* buf;   // LDS, element j at buf[j * BLOCK]
-    int n, e;
-    int pos, g;      // next word to consume, regenerated prefix of the current block
-    int bi, bcnt;    // consumption index / end of the staged batch
 
-    __device__ __forceinline__ void fill() {
-        const uint4* row = reinterpret_cast<const uint4*>(mt + (size_t)e * MT_N);
-        uint32_t* roww = mt + (size_t)e * MT_N;
-        const int pa = pos & ~3;
-        const int cnt = (MT_N - pa) < MTB ? (MT_N - pa) : MTB;
-        uint32_t a[MTB + 4], c[MTB + 4];
+template <int B>
+__device__ __forceinline__ void mt_batch(uint32_t* __restrict__ roww, int pos, int& g, uint32_t (&v)[B], int& pa,
+                                         int& cnt) {
+    uint4* row = reinterpret_cast<uint4*>(roww);
+    pa = pos & ~3;
+    cnt = (MT_N - pa) < B ? (MT_N - pa) : B;
+    uint32_t a[B + 4], c[B + 4];
 #pragma unroll
-        for (int q = 0; q < (MTB + 4) / 4; q++) {
-            int ia = pa + 4 * q;
-            ia = ia >= MT_N ? ia - MT_N : ia;
-            int ic = pa + 396 + 4 * q;
-            ic = ic >= MT_N ? ic - MT_N : ic;
-            ic = ic >= MT_N ? ic - MT_N : ic;
-            const uint4 va = row[ia >> 2], vc = row[ic >> 2];
-            a[4 * q] = va.x; a[4 * q + 1] = va.y; a[4 * q + 2] = va.z; a[4 * q + 3] = va.w;
-            c[4 * q] = vc.x; c[4 * q + 1] = vc.y; c[4 * q + 2] = vc.z; c[4 * q + 3] = vc.w;
-        }
+    for (int q = 0; q < (B + 4) / 4; q++) {
+        int ia = pa + 4 * q;
+        ia = ia >= MT_N ? ia - MT_N : ia;
+        int ic = pa + 396 + 4 * q;
+        ic = ic >= MT_N ? ic - MT_N : ic;
+        ic = ic >= MT_N ? ic - MT_N : ic;
+        const uint4 va = row[ia >> 2], vc = row[ic >> 2];
+        a[4 * q] = va.x; a[4 * q + 1] = va.y; a[4 * q + 2] = va.z; a[4 * q + 3] = va.w;
+        c[4 * q] = vc.x; c[4 * q + 1] = vc.y; c[4 * q + 2] = vc.z; c[4 * q + 3] = vc.w;
+    }
+    uint32_t w[B];
 #pragma unroll
-        for (int j = 0; j < MTB; j++) {
-            const int idx = pa + j;
-            const uint32_t y = (a[j] & 0x80000000u) | (a[j + 1] & 0x7fffffffu);   // a[cnt] = word 0 at the wrap
-            const uint32_t regen = c[j + 1] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);   // word idx + 397
-            const bool fresh = idx >= g;
-            uint32_t v = fresh ? regen : a[j];
-            if (fresh && j < cnt) roww[idx] = v;
-            v ^= v >> 11;
-            v ^= (v << 7) & 0x9d2c5680u;
-            v ^= (v << 15) & 0xefc60000u;
-            v ^= v >> 18;
-            buf[j * BLOCK] = v;
-        }
-        if (pa + cnt > g) g = pa + cnt;
-        bi = pos - pa;
-        bcnt = cnt;
+    for (int j = 0; j < B; j++) {
+        const uint32_t y = (a[j] & 0x80000000u) | (a[j + 1] & 0x7fffffffu);   // a[cnt] = word 0 at the wrap
+        const uint32_t regen = c[j + 1] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);   // word pa + j + 397
+        const uint32_t stale = (uint32_t)((pa + j - g) >> 31);   // all ones iff word pa + j < g (already current)
+        w[j] = (regen & ~stale) | (a[j] & stale);   // bitwise: no branch per word
+        uint32_t t = w[j];
+        t ^= t >> 11;
+        t ^= (t << 7) & 0x9d2c5680u;
+        t ^= (t << 15) & 0xefc60000u;
+        t ^= t >> 18;
+        v[j] = t;
     }
-    __device__ __forceinline__ uint32_t peek(int j) const { return buf[(bi + j) * BLOCK]; }   // bi + j < bcnt
-    __device__ __forceinline__ void consume() {
-        bi += 1;
-        pos += 1;
-        if (pos == MT_N) { pos = 0; g = 0; }
-    }
+#pragma unroll
+    for (int q = 0; q < B / 4; q++)
+        if (4 * q < cnt) row[(pa >> 2) + q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    if (pa + cnt > g) g = pa + cnt;
+}
+
+// generate_order (FJSPSimulation.py:101-131) as a state machine over the stream: per order
+// randint(1, 10) then choice(ProductType) then choice(PackagingColor) (:107,111-112) with
+// numpy's masked rejection: rng 8 / mask 15 for the product count (field k = 0), rng 2 /
+// mask 3 for type and colour (k = 1, 2).
+struct OrderDraw {
+    int o, k, np, ty;
+    uint32_t last;
 };
 
-// FJSPSimulation.reset body after the optional reseed (FJSPSimulation.py:301-320).
-// generate_order draws randint(1, 10) then choice(ProductType) then choice(PackagingColor)
-// per order (FJSPSimulation.py:107,111-112): field f = 3 * order + k with numpy's masked
-// rejection (rng 8 / mask 15 for k = 0, rng 2 / mask 3 otherwise).
-// mtbuf: this lane's LDS staging buffer for the MT reader (MTB words, stride BLOCK).
-__device__ __forceinline__ void env_reset(Env& E, const Tables& T, const Cfg& C, const DevState& S, int e, int num_orders,
-                                          uint32_t* mtbuf) {
+// Consume words [skip, cnt) of one batch (straight-line selects, no per-draw branch) until
+// `num_orders` orders are complete; returns the words consumed.  The order word is stored
+// every draw, to slot o (overwritten later by order o's own store) or, once the table is
+// complete, as the unchanged last order.
+template <int B>
+__device__ __forceinline__ int draw_orders(const uint32_t (&v)[B], int skip, int cnt, int num_orders, OrderDraw& d,
+                                           uint32_t* orders, int stride) {
+    int used = 0;
+#pragma unroll
+    for (int j = 0; j < B; j++) {
+        const bool act = j >= skip && j < cnt && d.o < num_orders;
+        const uint32_t x = v[j] & (d.k == 0 ? 15u : 3u);
+        const bool acc = act && x <= (d.k == 0 ? 8u : 2u);
+        const bool emit = acc && d.k == 2;
+        d.np = (acc && d.k == 0) ? 1 + (int)x : d.np;
+        d.ty = (acc && d.k == 1) ? 1 + (int)x : d.ty;
+        const uint32_t ow = ow_make(d.np, d.ty, 1 + (int)x);
+        d.last = emit ? ow : d.last;
+        orders[(d.o < num_orders ? d.o : num_orders - 1) * stride] = d.last;
+        d.o += emit ? 1 : 0;
+        d.k = acc ? (d.k == 2 ? 0 : d.k + 1) : d.k;
+        used += act ? 1 : 0;
+    }
+    return used;
+}
+
+// MT rows: two per env ([2][N][624]); bit 31 of the cursor word W3 selects the live one (the
+// other is the pre-draw wave's working copy, see k_step_pipe).  W[PGW] = the pre-draw record:
+// 0, or ready (bit 0) | cursor after the pre-drawn orders (mti bits 1..10, g bits 11..20) |
+// row (bit 21) | num_orders (bits 24..30), with the orders in S.nxt.
+constexpr int PGW = NSTATE;
+static_assert(NWORDS > PGW, "state buffer rows");
+__device__ __forceinline__ uint32_t* mt_row(const DevState& S, uint32_t w3, int e) {
+    return S.mt + ((size_t)(w3 >> 31) * S.n + e) * MT_N;
+}
+
+// FJSPSimulation.reset body after the optional reseed (FJSPSimulation.py:301-320): clear the
+// env and draw num_orders orders from the env's live MT row.  clear_pg: drop a pre-drawn
+// next table (it was drawn from the stream position this reset consumes).
+__device__ __forceinline__ void env_reset(Env& E, const Tables& T, const Cfg& C, const DevState& S, int e,
+                                          int num_orders, bool clear_pg = true) {
     env_clear(E, C);
     E.set_norders(num_orders);
-    MtReader R{S.mt, mtbuf, S.n, e, E.mti() & 0x3FF, (E.mti() >> 16) & 0x3FF, 0, 0};
-    int o = 0, k = 0, np = 0, ty = 0;   // order index, field within the order (n, type, colour)
-    // One draw: numpy's masked rejection (rng 8 / mask 15 for n, rng 2 / mask 3 otherwise).
-    auto take = [&](uint32_t v) {
-        R.consume();
-        const uint32_t x = v & (k == 0 ? 15u : 3u);
-        if (x > (k == 0 ? 8u : 2u)) return;   // rejected draw
-        if (k == 0) { np = 1 + (int)x; k = 1; }
-        else if (k == 1) { ty = 1 + (int)x; k = 2; }
-        else { T.orders[o * T.stride] = ow_make(np, ty, 1 + (int)x); k = 0; o += 1; }
-    };
-    for (;;) {
-        // four staged draws per LDS round trip (their reads are independent of the rejections)
-        while (o < num_orders && R.bi + 4 <= R.bcnt) {
-            const uint32_t v0 = R.peek(0), v1 = R.peek(1), v2 = R.peek(2), v3 = R.peek(3);
-            take(v0);
-            if (o < num_orders) take(v1);
-            if (o < num_orders) take(v2);
-            if (o < num_orders) take(v3);
-        }
-        while (o < num_orders && R.bi < R.bcnt) take(R.peek(0));
-        const bool need = o < num_orders;
-        if (!__any(need)) break;   // wave-uniform refill point
-        if (need) R.fill();
+    const uint32_t w3 = (uint32_t)E.mti();
+    uint32_t* roww = mt_row(S, w3, e);
+    int pos = (int)(w3 & 0x3FF), g = (int)((w3 >> 16) & 0x3FF);
+    OrderDraw d{0, 0, 0, 0, 0u};
+    while (d.o < num_orders) {
+        uint32_t v[MTB];
+        int pa, cnt;
+        mt_batch<MTB>(roww, pos, g, v, pa, cnt);
+        pos += draw_orders<MTB>(v, pos - pa, cnt, num_orders, d, T.orders, T.stride);
+        if (pos == MT_N) { pos = 0; g = 0; }
     }
-    E.set_mti(R.pos | (R.g << 16));
+    E.set_mti((int)((uint32_t)pos | ((uint32_t)g << 16) | (w3 & 0x80000000u)));
+    if (clear_pg) S.words[(size_t)PGW * S.n + e] = 0u;
+}
+
+// reset(seed=None) from a pre-drawn table (lane's slots nxt[o * BLOCK]): the same state as
+// env_reset, the stream position and live row taken from the pre-draw.
+__device__ __forceinline__ void env_reset_predrawn(Env& E, const Tables& T, const Cfg& C, int num_orders,
+                                                   uint32_t w3, const uint32_t* nxt) {
+    env_clear(E, C);
+    E.set_norders(num_orders);
+    for (int o = 0; o < num_orders; o++) T.orders[o * T.stride] = nxt[o * BLOCK];
+    E.set_mti((int)w3);
 }
 
 // Auto-reset inside the step kernels is a cold path (once per ~200 steps): a non-inlined call
@@ -184,9 +215,8 @@ __device__ __forceinline__
 #else
 __device__ __attribute__((noinline))
 #endif
-Env env_reset_cold(Env E, Tables T, Cfg C, DevState S, int e, int num_orders,
-                                                        uint32_t* mtbuf) {
-    env_reset(E, T, C, S, e, num_orders, mtbuf);
+Env env_reset_cold(Env E, Tables T, Cfg C, DevState S, int e, int num_orders, bool clear_pg = true) {
+    env_reset(E, T, C, S, e, num_orders, clear_pg);
     return E;
 }
 
@@ -240,11 +270,11 @@ __global__ void __launch_bounds__(BLOCK) k_seed(DevState S, const uint32_t* __re
     if (e >= S.n) return;
     mt_seed(S.mt, e, seeds ? seeds[e] : seed_base + (uint32_t)e);
     S.words[3 * S.n + e] = 0;
+    S.words[(size_t)PGW * S.n + e] = 0;
 }
 
 __global__ void __launch_bounds__(BLOCK) k_reset(DevState S, Cfg C, const uint32_t* __restrict__ seeds,
                                                  const uint8_t* __restrict__ env_mask, int num_orders, fjsp_out out) {
-    __shared__ uint32_t s_mtbuf[MTB * BLOCK];
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     if (e >= S.n) return;
     if (env_mask && !env_mask[e]) return;
@@ -253,7 +283,7 @@ __global__ void __launch_bounds__(BLOCK) k_reset(DevState S, Cfg C, const uint32
     int mti = (int)S.words[3 * S.n + e];
     if (seeds) { mt_seed(S.mt, e, seeds[e]); mti = 0; }
     E.set_mti(mti);
-    env_reset(E, T, C, S, e, num_orders, s_mtbuf + threadIdx.x);
+    env_reset(E, T, C, S, e, num_orders);
     StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, 0u, (uint32_t)S.n, (uint32_t)e, out.feats};
     observe(E, C, sink);
     env_store(E, S.words, S.n, e);
@@ -366,7 +396,7 @@ __device__ __forceinline__ void copy_out(const StageTile& tl, const fjsp_out& ou
 // Lean + LDS-staged variant of step_and_emit (obs, masks, rewards, term, trunc, status).
 __device__ __forceinline__ void step_and_emit_staged(Env& E, const Tables& T, const Cfg& C, const DevState& S, int e,
                                                      const int* act, int autoreset, const fjsp_out& out, uint32_t t,
-                                                     uint32_t* mtbuf, StageTile* tl, int lane) {
+                                                     StageTile* tl, int lane) {
     uint32_t res[NA];
     const double g8 = env_advance<true>(E, T, C, act, nullptr, res);
 #pragma unroll
@@ -387,7 +417,7 @@ __device__ __forceinline__ void step_and_emit_staged(Env& E, const Tables& T, co
     FJSP_STAMP(E, 5);
     E.set_step(E.step() + 1);
     if (autoreset && (all_done || truncated))
-        E = env_reset_cold(E, T, C, S, e, nord, mtbuf);   // reset(seed=None) continues the MT stream
+        E = env_reset_cold(E, T, C, S, e, nord);   // reset(seed=None) continues the MT stream
     FJSP_STAMP(E, 6);
 }
 
@@ -396,7 +426,7 @@ __device__ __forceinline__ void step_and_emit_staged(Env& E, const Tables& T, co
 template <bool CANON, bool FULL = true>
 __device__ __forceinline__ void step_and_emit(Env& E, const Tables& T, const Cfg& C, const DevState& S, int e,
                                               const int* act, const uint8_t* order, int autoreset, const fjsp_out& out,
-                                              uint32_t t, uint32_t* mtbuf) {
+                                              uint32_t t) {
     const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
     uint32_t res[NA];
     const double g8 = env_advance<CANON>(E, T, C, act, order, res);
@@ -424,7 +454,7 @@ __device__ __forceinline__ void step_and_emit(Env& E, const Tables& T, const Cfg
     FJSP_STAMP(E, 5);
     E.set_step(E.step() + 1);
     if (autoreset && (all_done || truncated))
-        E = env_reset_cold(E, T, C, S, e, nord, mtbuf);   // reset(seed=None) continues the MT stream
+        E = env_reset_cold(E, T, C, S, e, nord);   // reset(seed=None) continues the MT stream
     if (FULL && (out.next_i32 || out.next_i8 || out.next_f32 || out.next_masks || out.feats)) {
         StoreSink nsink{out.next_i32, out.next_i8, out.next_f32, out.next_masks, t, n, ue, out.feats};
         observe(E, C, nsink);
@@ -435,7 +465,6 @@ __device__ __forceinline__ void step_and_emit(Env& E, const Tables& T, const Cfg
 template <bool CANON>
 __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t* __restrict__ actions, uint64_t order_packed,
                                                 int autoreset, fjsp_out out) {
-    __shared__ uint32_t s_mtbuf[MTB * BLOCK];
     __shared__ double s_lut[RLUT_SIZE];
     for (int i = threadIdx.x; i < RLUT_SIZE; i += BLOCK) s_lut[i] = C.lut[i];
     __syncthreads();
@@ -451,7 +480,7 @@ __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t
     uint8_t order[NA];
 #pragma unroll
     for (int i = 0; i < NA; i++) order[i] = (uint8_t)(order_packed >> (8 * i));
-    step_and_emit<CANON>(E, T, C, S, e, act, order, autoreset, out, 0, s_mtbuf + threadIdx.x);
+    step_and_emit<CANON>(E, T, C, S, e, act, order, autoreset, out, 0);
     env_store(E, S.words, S.n, e);
 }
 
@@ -468,7 +497,6 @@ __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, u
     __shared__ uint16_t s_code[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint8_t s_next[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint16_t s_cstep[LDS ? MAX_SLOTS * BLOCK : 1];
-    __shared__ uint32_t s_mtbuf[MTB * BLOCK];
     __shared__ double s_lut[RLUT_SIZE];
     const int lane = threadIdx.x;
     for (int i = lane; i < RLUT_SIZE; i += BLOCK) s_lut[i] = C.lut[i];
@@ -503,9 +531,9 @@ __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, u
         synth_actions(seed, gid0 + (uint32_t)e, step0 + (uint32_t)k, mode, E, T, C, act);
         FJSP_STAMP(E, 0);
         if constexpr (STAGED)
-            step_and_emit_staged(E, T, C, S, e, act, autoreset, out, (uint32_t)k, s_mtbuf + lane, &s_tile, lane);
+            step_and_emit_staged(E, T, C, S, e, act, autoreset, out, (uint32_t)k, &s_tile, lane);
         else
-            step_and_emit<true, FULL>(E, T, C, S, e, act, nullptr, autoreset, out, (uint32_t)k, s_mtbuf + lane);
+            step_and_emit<true, FULL>(E, T, C, S, e, act, nullptr, autoreset, out, (uint32_t)k);
     }
     if constexpr (LDS) {
         for (int o = 0; o < E.norders(); o++) S.orders[(size_t)o * S.n + e] = T.orders[o * BLOCK];
@@ -573,18 +601,42 @@ __device__ __forceinline__ uint32_t pack_actions(const int* act, int lo) {
     return (uint32_t)act[lo] | ((uint32_t)act[lo + 1] << 8) | ((uint32_t)act[lo + 2] << 16) | ((uint32_t)act[lo + 3] << 24);
 }
 
-template <bool LDS, int NEMIT>
-__global__ void __launch_bounds__((1 + NEMIT) * BLOCK) k_step_pipe(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0,
-                                                         uint32_t step0, int mode, int autoreset, fjsp_out out) {
+// PG: a pre-draw wave (wave 1 + NEMIT, a SIMD of its own) draws each env's next order table
+// while the episode runs, so an auto-reset is a table copy instead of ~130 MT draws on the
+// sim wave's critical path.  It copies the live MT row to the env's other row (CQ uint4 per
+// step), then draws from the copy (PB words per step) into LDS; the sim wave consumes a
+// finished table at reset (the other row becomes live) or, if it is not finished, resets
+// inline from the live row.  Copies are cooperative (the wave copies one env's row with
+// contiguous 1 KB loads); the draw is per lane.  The two waves exchange per-lane mailboxes double-buffered by
+// step parity (written in step k, read in step k + 1, the barrier between): the sim wave
+// posts its episode counter, num_orders and cursor word, the pre-draw wave whether its table
+// is ready for that episode counter and the cursor word after it.  A finished table outlives
+// the launch (W[PGW], S.nxt); every other reset path clears it.
+#ifndef FJSP_PG_CR
+#define FJSP_PG_CR 1   // pre-draw work per step: MT rows copied (whole wave) ...
+#endif
+#ifndef FJSP_PG_PB
+#define FJSP_PG_PB 8   // ... and words drawn per env
+#endif
+template <bool LDS, int NEMIT, bool PG = false>
+__global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2))) k_step_pipe(DevState S, Cfg C, int K, uint64_t seed,
+                                                              uint32_t gid0, uint32_t step0, int mode, int autoreset,
+                                                              fjsp_out out) {
+    static_assert(!PG || LDS, "the pre-drawn tables live in LDS");
+    // pre-draw work per step (sized so the wave stays off the critical path): rows copied by
+    // the whole wave (CR envs, 1 KB per load), words drawn per env
+    constexpr int CR = FJSP_PG_CR, PB = FJSP_PG_PB;
     __shared__ uint32_t s_orders[LDS ? MAX_ORDERS * BLOCK : 1];
+    __shared__ uint32_t s_nxt[PG ? MAX_ORDERS * BLOCK : 1];
+    __shared__ uint32_t s_mb[PG ? 4 : 1][2][BLOCK];   // sim: epi | nord << 8, cursor word; pre-draw: ready, cursor
+    __shared__ uint4 s_cp[PG ? FJSP_PG_CR : 1][3][BLOCK];   // MT rows in flight (pre-draw copies)
     __shared__ uint16_t s_code[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint8_t s_next[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint16_t s_cstep[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ PipeSnap snap[2];
     __shared__ uint32_t s_act[2][2][BLOCK];
-    __shared__ uint32_t s_mtbuf[MTB * BLOCK];
     __shared__ double s_lut[RLUT_SIZE];
-    for (int i = threadIdx.x; i < RLUT_SIZE; i += (1 + NEMIT) * BLOCK) s_lut[i] = C.lut[i];
+    for (int i = threadIdx.x; i < RLUT_SIZE; i += (1 + NEMIT + PG) * BLOCK) s_lut[i] = C.lut[i];
     C.lut = s_lut;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / BLOCK);
     const int lane = threadIdx.x % BLOCK;
@@ -597,6 +649,24 @@ __global__ void __launch_bounds__((1 + NEMIT) * BLOCK) k_step_pipe(DevState S, C
         synth_uniform(seed, gid0 + (uint32_t)e, step0, act);
         s_act[0][0][lane] = pack_actions(act, 0);
         s_act[0][1][lane] = pack_actions(act, 4);
+    }
+    if constexpr (PG) {   // step-0 mailboxes
+        if (wave == 0 && valid) {
+            s_mb[0][0][lane] = ((S.words[e] >> 16) & 0xFFu) << 8;   // episode counter 0 | num_orders
+            s_mb[1][0][lane] = S.words[3 * n + e];
+        }
+        if (wave == 1 + NEMIT && valid) {
+            const uint32_t pg = S.words[(size_t)PGW * n + e];
+            uint32_t r = 0, c = 0;
+            if (pg & 1u) {   // a table finished in an earlier launch
+                const int no = (int)((pg >> 24) & 0x7Fu);
+                for (int o = 0; o < no; o++) s_nxt[o * BLOCK + lane] = S.nxt[(size_t)o * n + e];
+                r = 1u | ((uint32_t)no << 9);
+                c = ((pg >> 1) & 0x3FFu) | (((pg >> 11) & 0x3FFu) << 16) | (((pg >> 21) & 1u) << 31);
+            }
+            s_mb[2][0][lane] = r;
+            s_mb[3][0][lane] = c;
+        }
     }
     __syncthreads();
     if (wave == 0) {
@@ -623,6 +693,7 @@ __global__ void __launch_bounds__((1 + NEMIT) * BLOCK) k_step_pipe(DevState S, C
         for (int i = 0; i < 8; i++) E.st_acc[i] = 0;
         E.st_t0 = __builtin_amdgcn_s_memtime();
 #endif
+        int epi = 0;   // episodes started in this launch (mod 256), the pre-draw tag
         for (int k = 0; k <= K; k++) {
             if (k < K && valid) {
                 int act[NA];
@@ -654,8 +725,22 @@ __global__ void __launch_bounds__((1 + NEMIT) * BLOCK) k_step_pipe(DevState S, C
                 const int truncated = E.step() >= C.max_steps;
                 FJSP_STAMP(E, 3);
                 E.set_step(E.step() + 1);
-                if (autoreset && (all_done || truncated))
-                    E = env_reset_cold(E, T, C, S, e, nord, s_mtbuf + lane);   // reset(seed=None)
+                if (autoreset && (all_done || truncated)) {   // reset(seed=None)
+                    if constexpr (PG) {
+                        const uint32_t pr = s_mb[2][k & 1][lane];
+                        if ((pr & 1u) && ((pr >> 1) & 0xFFu) == (uint32_t)epi && (int)((pr >> 9) & 0x7Fu) == nord)
+                            env_reset_predrawn(E, T, C, nord, s_mb[3][k & 1][lane], s_nxt + lane);
+                        else
+                            E = env_reset_cold(E, T, C, S, e, nord, false);
+                        epi = (epi + 1) & 0xFF;
+                    } else {
+                        E = env_reset_cold(E, T, C, S, e, nord);
+                    }
+                }
+                if constexpr (PG) {
+                    s_mb[0][(k + 1) & 1][lane] = (uint32_t)epi | ((uint32_t)E.norders() << 8);
+                    s_mb[1][(k + 1) & 1][lane] = E.w[3];
+                }
                 FJSP_STAMP(E, 6);
             }
             __syncthreads();
@@ -675,6 +760,129 @@ __global__ void __launch_bounds__((1 + NEMIT) * BLOCK) k_step_pipe(DevState S, C
         if (lane == 0)
             for (int i = 0; i < 8; i++) atomicAdd((unsigned long long*)&g_stamps[i], (unsigned long long)E.st_acc[i]);
 #endif
+    } else if (PG && wave == 1 + NEMIT) {
+        // the pre-draw wave: 0 idle, 1 copying the live row, 2 drawing, 3 table ready
+        int ph = 0, nord = 0, pos = 0, g = 0;
+        uint32_t src = 0, my = 0x100u;   // live row at the start of the pre-draw; episode it is for
+        OrderDraw d{0, 0, 0, 0, 0u};
+        if (valid) {
+            const uint32_t pg = S.words[(size_t)PGW * n + e];
+            if (pg & 1u) {
+                ph = 3;
+                my = 0;
+                nord = (int)((pg >> 24) & 0x7Fu);
+                pos = (int)((pg >> 1) & 0x3FFu);
+                g = (int)((pg >> 11) & 0x3FFu);
+                src = ((pg >> 21) & 1u) ^ (nord > 0 ? 1u : 0u);
+            }
+        }
+#ifdef FJSP_STAMPS
+        uint64_t pg_busy = 0, pg_act = 0, pg_busy_act = 0;
+#endif
+        for (int k = 0; k <= K; k++) {
+#ifdef FJSP_STAMPS
+            const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+            bool pg_active = false;
+#endif
+            if (valid) {
+                const uint32_t si = s_mb[0][k & 1][lane];
+                if ((si & 0xFFu) != my) {   // a new episode: start over from its stream position
+                    const uint32_t sw = s_mb[1][k & 1][lane];
+                    my = si & 0xFFu;
+                    nord = (int)((si >> 8) & 0x7Fu);
+                    src = sw >> 31;
+                    pos = (int)(sw & 0x3FFu);
+                    g = (int)((sw >> 16) & 0x3FFu);
+                    d = OrderDraw{0, 0, 0, 0, 0u};
+#ifdef FJSP_PG_IDLE
+                    ph = 0;   // diagnostic: the pre-draw wave only keeps the mailboxes
+#else
+                    ph = nord > 0 ? 1 : 3;
+#endif
+                }
+            }
+            // Copy the live rows of up to CR envs that start a pre-draw (the whole wave, one
+            // env at a time: contiguous 1 KB loads): loads first, the per-lane draw in the shadow
+            // of their latency, then the stores.  Rows copied in step k are first read in k + 1.
+            auto draw_step = [&]() {
+                if (valid && ph == 2) {
+                    uint32_t* work = S.mt + ((size_t)(src ^ 1u) * n + e) * MT_N;
+                    uint32_t v[PB];
+                    int pa, cnt;
+                    mt_batch<PB>(work, pos, g, v, pa, cnt);
+                    pos += draw_orders<PB>(v, pos - pa, cnt, nord, d, s_nxt + lane, BLOCK);
+                    if (pos == MT_N) { pos = 0; g = 0; }
+                    if (d.o >= nord) ph = 3;
+                }
+            };
+            uint64_t need = __ballot(valid && ph == 1);
+#ifdef FJSP_STAMPS
+            pg_active = need != 0 || __ballot(valid && ph == 2) != 0;
+#endif
+            if (need) {
+                // rows go through LDS by DMA (global_load_lds: no VGPRs held across the draw);
+                // slots beyond the envs waiting re-copy the first env's row (identical stores)
+                const int first = __builtin_ctzll(need);
+                int ls[CR];
+#pragma unroll
+                for (int r = 0; r < CR; r++) {
+                    ls[r] = need ? __builtin_ctzll(need) : first;
+                    need &= need - 1;
+                    const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)src, ls[r]);
+                    const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls[r];
+                    const uint4* rs = reinterpret_cast<const uint4*>(S.mt + ((size_t)sl * n + el) * MT_N);
+#pragma unroll
+                    for (int i = 0; i < 3; i++)
+                        __builtin_amdgcn_global_load_lds(
+                            (__attribute__((address_space(1))) void*)(rs + min(lane + 64 * i, MT_N / 4 - 1)),
+                            (__attribute__((address_space(3))) void*)&s_cp[r][i][0], 16, 0, 0);
+                }
+                draw_step();
+                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the row DMAs have landed
+#pragma unroll
+                for (int r = 0; r < CR; r++) {
+                    const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)src, ls[r]);
+                    const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls[r];
+                    uint4* rd = reinterpret_cast<uint4*>(S.mt + ((size_t)(sl ^ 1u) * n + el) * MT_N);
+                    rd[lane] = s_cp[r][0][lane];
+                    rd[lane + 64] = s_cp[r][1][lane];
+                    if (lane + 128 < MT_N / 4) rd[lane + 128] = s_cp[r][2][lane];
+                    if (lane == ls[r]) ph = 2;
+                }
+            } else {
+                draw_step();
+            }
+            if (valid) {
+                const uint32_t wrow = nord > 0 ? (src ^ 1u) : src;
+                s_mb[2][(k + 1) & 1][lane] = (ph == 3 ? 1u : 0u) | (my << 1) | ((uint32_t)nord << 9);
+                s_mb[3][(k + 1) & 1][lane] = (uint32_t)pos | ((uint32_t)g << 16) | (wrow << 31);
+            }
+#ifdef FJSP_STAMPS
+            {
+                const uint64_t dt = __builtin_amdgcn_s_memtime() - pt0;
+                pg_busy += dt;
+                if (pg_active) { pg_act += 1; pg_busy_act += dt; }
+            }
+#endif
+            __syncthreads();
+        }
+#ifdef FJSP_STAMPS
+        if (lane == 0) {
+            atomicAdd(&g_pgstamps[0], (unsigned long long)pg_busy);
+            atomicAdd(&g_pgstamps[1], (unsigned long long)pg_act);
+            atomicAdd(&g_pgstamps[2], (unsigned long long)pg_busy_act);
+            atomicAdd(&g_pgstamps[3], (unsigned long long)(K + 1));
+        }
+#endif
+        if (valid) {
+            uint32_t pg = 0;
+            if (ph == 3) {
+                const uint32_t wrow = nord > 0 ? (src ^ 1u) : src;
+                pg = 1u | ((uint32_t)pos << 1) | ((uint32_t)g << 11) | (wrow << 21) | ((uint32_t)nord << 24);
+                for (int o = 0; o < nord; o++) S.nxt[(size_t)o * n + e] = s_nxt[o * BLOCK + lane];
+            }
+            S.words[(size_t)PGW * n + e] = pg;
+        }
     } else {
         // NEMIT == 2: two emit waves split the outputs: wave 1 rewards + int32 / float32
         // observation fields (+ the next step's uniform actions), wave 2 int8 fields, masks,
@@ -778,6 +986,7 @@ struct fjsp_handle {
     int use_staged;  // LDS-staged wide output stores (FJSP_STAGED env var / fjsp_set_option)
     int timing;      // hipEvent bracketing of step launches (off while graph-capturing)
     int use_pipe;    // two-wave pipelined k_step_many for lean outputs (FJSP_PIPE / fjsp_set_option)
+    int use_pg;      // pre-draw wave in the pipelined kernel (FJSP_PREDRAW / fjsp_set_option "predraw")
     const char* last_kernel;   // name of the last step kernel launched (fjsp_last_kernel)
 };
 
@@ -895,6 +1104,8 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
         h->timing = 1;
         const char* pp = getenv("FJSP_PIPE");
         h->use_pipe = pp ? atoi(pp) : 1;
+        const char* pd = getenv("FJSP_PREDRAW");
+        h->use_pg = pd ? atoi(pd) : 1;
     }
     h->dcfg.step_size = c.step_size;
     h->dcfg.max_steps = c.max_episode_steps;
@@ -910,9 +1121,9 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     const size_t n = (size_t)num_envs;
     const size_t b_words = (size_t)NWORDS * n * 4, b_orders = (size_t)MAX_ORDERS * n * 4;
     const size_t b_scode = (size_t)MAX_SLOTS * n * 2, b_snext = (size_t)MAX_SLOTS * n, b_scstep = (size_t)MAX_SLOTS * n * 2;
-    const size_t b_mt = (size_t)MT_N * n * 4;
+    const size_t b_mt = (size_t)2 * MT_N * n * 4, b_nxt = (size_t)MAX_ORDERS * n * 4;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    h->bytes = al(b_words) + al(b_orders) + al(b_scode) + al(b_snext) + al(b_scstep) + al(b_mt);
+    h->bytes = al(b_words) + al(b_orders) + al(b_scode) + al(b_snext) + al(b_scstep) + al(b_nxt) + al(b_mt);
     hipError_t e = hipMalloc(&h->base, h->bytes);
     if (e != hipSuccess) { delete h; return hip_fail("hipMalloc(state)", e); }
     char* p = (char*)h->base;
@@ -921,6 +1132,7 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     h->S.scode = (uint16_t*)p; p += al(b_scode);
     h->S.snext = (uint8_t*)p; p += al(b_snext);
     h->S.scstep = (uint16_t*)p; p += al(b_scstep);
+    h->S.nxt = (uint32_t*)p; p += al(b_nxt);
     h->S.mt = (uint32_t*)p;
     h->S.n = num_envs;
     e = hipMemsetAsync(h->base, 0, h->bytes, h->stream);
@@ -963,6 +1175,7 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
     if (!strcmp(name, "fused_lds")) { h->use_lds = value < 0 ? -1 : value != 0; return 0; }
     if (!strcmp(name, "staged_stores")) { h->use_staged = value != 0; return 0; }
     if (!strcmp(name, "pipeline")) { h->use_pipe = value != 0; return 0; }
+    if (!strcmp(name, "predraw")) { h->use_pg = value != 0; return 0; }
     if (!strcmp(name, "timing")) { h->timing = value != 0; if (!h->timing) h->timed = 0; return 0; }
     return fail("unknown option");
 }
@@ -1052,8 +1265,11 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
     // LDS tables (97.5 KB per 64-env workgroup) pay while every workgroup has a CU of its own
     const bool lds = h->use_lds < 0 ? h->n <= 256 * BLOCK : h->use_lds != 0;
     const bool two_emit = h->n <= 256 * BLOCK;
+    // the pre-draw wave pays while the CUs have a free SIMD (and only with auto-reset)
+    const bool pg = h->use_pg && lds && two_emit && autoreset;
     h->last_kernel = (h->use_pipe && !full && !staged)
-                         ? (lds ? (two_emit ? "k_step_pipe<lds,2emit>" : "k_step_pipe<lds,1emit>")
+                         ? (lds ? (two_emit ? (pg ? "k_step_pipe<lds,2emit,predraw>" : "k_step_pipe<lds,2emit>")
+                                            : "k_step_pipe<lds,1emit>")
                                 : (two_emit ? "k_step_pipe<2emit>" : "k_step_pipe<1emit>"))
                    : full ? (lds ? "k_step_many<lds,full>" : "k_step_many<full>")
                    : staged ? (lds ? "k_step_many<lds,staged>" : "k_step_many<staged>")
@@ -1065,7 +1281,8 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
             hipLaunchKernelGGL(kern, grid, dim3(waves * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0,
                                step0, action_mode, autoreset, o);
         };
-        if (lds) two ? launch_pipe(k_step_pipe<true, 2>, 3) : launch_pipe(k_step_pipe<true, 1>, 2);
+        if (lds && two && pg) launch_pipe(k_step_pipe<true, 2, true>, 4);
+        else if (lds) two ? launch_pipe(k_step_pipe<true, 2>, 3) : launch_pipe(k_step_pipe<true, 1>, 2);
         else two ? launch_pipe(k_step_pipe<false, 2>, 3) : launch_pipe(k_step_pipe<false, 1>, 2);
     } else if (lds) {
         if (full) launch(k_step_many<true, true>);
@@ -1113,6 +1330,13 @@ extern "C" int fjsp_debug_stamps(unsigned long long* out) {
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8));
     unsigned long long z[8] = {0};
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)));
+    return 0;
+}
+extern "C" int fjsp_debug_pgstamps(unsigned long long* out) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pgstamps), sizeof(unsigned long long) * 4));
+    unsigned long long z[4] = {0};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_pgstamps), z, sizeof(z)));
     return 0;
 }
 #endif
@@ -1183,7 +1407,7 @@ int fjsp_mt_get(fjsp_handle* h, int32_t env, uint32_t* key, int32_t* pos) {
     HIPCHK(hipStreamSynchronize(h->stream));
     uint32_t st = 0;
     HIPCHK(hipMemcpy(&st, h->S.words + (size_t)3 * h->n + env, 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(key, h->S.mt + (size_t)env * MT_N, 4 * MT_N, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(key, h->S.mt + ((size_t)(st >> 31) * h->n + env) * MT_N, 4 * MT_N, hipMemcpyDeviceToHost));
     int mti = (int)(st & 0x3FF), gg = (int)((st >> 16) & 0x3FF);
     if (gg == 0) { *pos = MT_N; return 0; }
     for (int i = gg; i < MT_N; i++) {   // finish the in-place twist of the current block
@@ -1205,6 +1429,8 @@ int fjsp_mt_set(fjsp_handle* h, int32_t env, const uint32_t* key, int32_t pos) {
     const uint32_t st = pos >= MT_N ? 0u : ((uint32_t)pos | ((uint32_t)MT_N << 16));
     HIPCHK(hipMemcpy(h->S.mt + (size_t)env * MT_N, key, 4 * MT_N, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->S.words + (size_t)3 * h->n + env, &st, 4, hipMemcpyHostToDevice));
+    const uint32_t zero = 0;   // a pre-drawn table belongs to the replaced stream
+    HIPCHK(hipMemcpy(h->S.words + (size_t)PGW * h->n + env, &zero, 4, hipMemcpyHostToDevice));
     return 0;
 }
 
