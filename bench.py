@@ -266,7 +266,7 @@ def main():
         wall = time.perf_counter() - t1
         kms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
         per_step = {"value": K * N / wall, "unit": "env-steps/s", "n_gpus": 1, "avg_kernel_ms": kms,
-                    "kernel": "k_step<true>", "algo_bytes_per_env_step": ALGO_BYTES_STEP,
+                    "kernel": env.last_kernel(), "algo_bytes_per_env_step": ALGO_BYTES_STEP,
                     "achieved_GBs": ALGO_BYTES_STEP * N / (kms * 1e-3) / 1e9,
                     "note": "one launch per step, actions u8[8][N] resident in HBM (rank 0)"}
 
