@@ -159,7 +159,10 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
  * step's obs / masks / rewards / term / trunc / status in LDS and writes them as 16-byte
  * chunks; used when only those outputs are requested, N % 64 == 0 and rows are aligned);
  * "timing" (0/1, default 1: bracket fjsp_step / fjsp_step_many launches with hipEvents for
- * fjsp_last_kernel_ms; set 0 while capturing the calls into a hipGraph). */
+ * fjsp_last_kernel_ms; set 0 while capturing the calls into a hipGraph); "predraw" (0/1,
+ * default 1: the pipelined kernel with LDS tables and auto-reset draws every env's next order
+ * table ahead on a fourth wave, so auto-resets need no MT draws on the critical path; the
+ * results are identical either way). */
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value);
 int fjsp_num_envs(const fjsp_handle* h);
 /* Bytes of device state per env (HBM footprint of the SoA state). */
