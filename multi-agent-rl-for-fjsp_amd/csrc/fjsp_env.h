@@ -891,9 +891,15 @@ FJSP_DEV double global_reward8(const Cfg& C, int orders_done, int packaged) {
 
 // Actions in dict order, then env.run in closed form.  actions[a] for agent a (canonical order);
 // order = execution order (CANON -> 0..7).  Fills res[8]; returns the shared global reward / 8.
-template <bool CANON>
+struct NoMid {
+    FJSP_DEV void operator()(const Env&) const {}
+};
+// mid(E) runs right after the AGV's action (the pipelined kernel hands the pickup station's
+// state to another wave there); pick_done: res[0] already holds the pickup's result, applied
+// to E by the caller (the pickup ran ahead on that wave).
+template <bool CANON, class Mid = NoMid>
 FJSP_DEV double env_advance(Env& E, const Tables& T, const Cfg& C, const int* act, const uint8_t* order,
-                            uint32_t* res) {
+                            uint32_t* res, Mid mid = Mid(), bool pick_done = false) {
     int move_to = 0, m_start[2] = {-1, -1}, p_started[4] = {0, 0, 0, 0};
     const int products_before = E.total_packaged();
     // 1. actions in dict order (FJSPSimulation.py:172-174)
@@ -904,7 +910,7 @@ FJSP_DEV double env_advance(Env& E, const Tables& T, const Cfg& C, const int* ac
         uint32_t r = 0;
         if (ac != 255) {
             switch (a) {
-            case 0: r = pickup_execute(E, T, C, ac); break;
+            case 0: r = pick_done ? res[0] : pickup_execute(E, T, C, ac); break;
             case 1: r = agv_execute(E, T, C, ac, &move_to); break;
             case 2: r = machine_execute<0>(E, T, ac, &m_start[0]); break;
             case 3: r = machine_execute<1>(E, T, ac, &m_start[1]); break;
@@ -916,6 +922,7 @@ FJSP_DEV double env_advance(Env& E, const Tables& T, const Cfg& C, const int* ac
         }
         res[a] = r;
         if (CANON) FJSP_STAMP_AGENT(E, i);
+        if (CANON && i == 1) mid(E);
     }
     FJSP_STAMP(E, 1);
     // 2. env.run(until=now+step_size) in closed form

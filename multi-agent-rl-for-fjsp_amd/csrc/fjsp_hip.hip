@@ -33,6 +33,7 @@ constexpr int MT_N = 624;
 #ifdef FJSP_STAMPS
 __device__ unsigned long long g_stamps[8];
 __device__ unsigned long long g_pgstamps[4];   // pre-draw wave: busy cycles, active steps, busy in active steps, steps
+__device__ unsigned long long g_emitstamps[4];   // emit waves 1, 2: busy cycles, steps
 #endif
 
 struct DevState {
@@ -630,6 +631,13 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
     __shared__ uint32_t s_nxt[PG ? MAX_ORDERS * BLOCK : 1];
     __shared__ uint32_t s_mb[PG ? 4 : 1][2][BLOCK];   // sim: epi | nord << 8, cursor word; pre-draw: ready, cursor
     __shared__ uint4 s_cp[PG ? FJSP_PG_CR : 1][3][BLOCK];   // MT rows in flight (pre-draw copies)
+    // pickup ahead (PG, uniform-random actions): the sim wave posts the pickup station's state
+    // after the AGV's action of step k (s_pk_in, then s_pkflag = k + 1); emit wave 1 runs step
+    // k + 1's pickup on it while the sim wave finishes step k and posts the new state words and
+    // the result (s_pk_out / s_pk_res), which the sim wave applies at the top of step k + 1.
+    __shared__ uint4 s_pk_in[PG ? BLOCK : 1], s_pk_out[PG ? BLOCK : 1];
+    __shared__ uint2 s_pk_res[PG ? BLOCK : 1];
+    __shared__ uint32_t s_pkflag;
     __shared__ uint16_t s_code[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint8_t s_next[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint16_t s_cstep[LDS ? MAX_SLOTS * BLOCK : 1];
@@ -651,6 +659,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
         s_act[0][1][lane] = pack_actions(act, 4);
     }
     if constexpr (PG) {   // step-0 mailboxes
+        if (threadIdx.x == 0) s_pkflag = 0;
         if (wave == 0 && valid) {
             s_mb[0][0][lane] = ((S.words[e] >> 16) & 0xFFu) << 8;   // episode counter 0 | num_orders
             s_mb[1][0][lane] = S.words[3 * n + e];
@@ -694,6 +703,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
         E.st_t0 = __builtin_amdgcn_s_memtime();
 #endif
         int epi = 0;   // episodes started in this launch (mod 256), the pre-draw tag
+        bool fresh = true;   // this step's pickup runs here (first step of the launch / after a reset)
         for (int k = 0; k <= K; k++) {
             if (k < K && valid) {
                 int act[NA];
@@ -706,8 +716,30 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
                 }
                 FJSP_STAMP(E, 0);
                 uint32_t res[NA];
+                bool pick_done = false;
+                if constexpr (PG) {
+                    if (pre && !fresh) {   // step k's pickup ran ahead on emit wave 1
+                        const uint4 po = s_pk_out[lane];
+                        const uint2 pr = s_pk_res[lane];
+                        E.w[0] = (E.w[0] & 0x00FFFFFFu) | (po.x << 24);
+                        E.w[4] = po.y;
+                        E.w[5] = po.z;
+                        E.w[7 + L_PREADY] = po.w;
+                        E.w[2] |= pr.y;
+                        res[0] = pr.x;
+                        pick_done = true;
+                    }
+                }
+                auto mid = [&](const Env& Em) {
+                    if constexpr (PG) {
+                        if (pre) {
+                            s_pk_in[lane] = make_uint4(Em.w[0], Em.w[4], Em.w[5], Em.w[7 + L_PREADY]);
+                            __hip_atomic_store(&s_pkflag, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                    }
+                };
                 const int nc0 = E.ncompleted(), tp0 = E.total_packaged();
-                (void)env_advance<true>(E, T, C, act, nullptr, res);   // g/8: the emit wave
+                (void)env_advance<true>(E, T, C, act, nullptr, res, mid, pick_done);   // g/8: the emit wave
                 flag_obs_overflow(E);
                 uint32_t v[SNAP_N];
                 int j = 0;
@@ -725,7 +757,9 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
                 const int truncated = E.step() >= C.max_steps;
                 FJSP_STAMP(E, 3);
                 E.set_step(E.step() + 1);
+                fresh = false;
                 if (autoreset && (all_done || truncated)) {   // reset(seed=None)
+                    fresh = true;
                     if constexpr (PG) {
                         const uint32_t pr = s_mb[2][k & 1][lane];
                         if ((pr & 1u) && ((pr >> 1) & 0xFFu) == (uint32_t)epi && (int)((pr >> 9) & 0x7Fu) == nord)
@@ -888,7 +922,13 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
         // observation fields (+ the next step's uniform actions), wave 2 int8 fields, masks,
         // term, trunc, status.  NEMIT == 1 (many envs: the CUs are already full): one wave.
         const int part = wave - 1;
+#ifdef FJSP_STAMPS
+        uint64_t em_busy = 0;
+#endif
         for (int k = 0; k <= K; k++) {
+#ifdef FJSP_STAMPS
+            const uint64_t et0 = __builtin_amdgcn_s_memtime();
+#endif
             if (k > 0 && valid) {
                 const uint32_t t = (uint32_t)(k - 1);
                 uint32_t v[SNAP_N];
@@ -930,9 +970,36 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
                 synth_uniform(seed, gid0 + (uint32_t)e, step0 + (uint32_t)(k + 1), act);
                 s_act[(k + 1) & 1][0][lane] = pack_actions(act, 0);
                 s_act[(k + 1) & 1][1][lane] = pack_actions(act, 4);
+                if constexpr (PG) {   // step k + 1's pickup, once the sim wave has posted its state
+                    while (__hip_atomic_load(&s_pkflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (uint32_t)(k + 1))
+                        __builtin_amdgcn_s_sleep(1);
+                    if (valid) {
+                        const uint4 pi = s_pk_in[lane];
+                        Env Ep;
+#pragma unroll
+                        for (int i = 0; i < NSTATE; i++) Ep.w[i] = 0u;
+                        Ep.w[0] = pi.x;
+                        Ep.w[4] = pi.y;
+                        Ep.w[5] = pi.z;
+                        Ep.w[7 + L_PREADY] = pi.w;
+                        const Tables Tp{s_orders + lane, s_code + lane, s_next + lane, s_cstep + lane, BLOCK};
+                        const uint32_t r = pickup_execute(Ep, Tp, C, act[0]);
+                        s_pk_out[lane] = make_uint4(Ep.w[0] >> 24, Ep.w[4], Ep.w[5], Ep.w[7 + L_PREADY]);
+                        s_pk_res[lane] = make_uint2(r, Ep.w[2]);
+                    }
+                }
             }
+#ifdef FJSP_STAMPS
+            em_busy += __builtin_amdgcn_s_memtime() - et0;
+#endif
             __syncthreads();
         }
+#ifdef FJSP_STAMPS
+        if (lane == 0 && part < 2) {
+            atomicAdd(&g_emitstamps[2 * part], (unsigned long long)em_busy);
+            atomicAdd(&g_emitstamps[2 * part + 1], (unsigned long long)(K + 1));
+        }
+#endif
     }
 }
 
@@ -1332,11 +1399,13 @@ extern "C" int fjsp_debug_stamps(unsigned long long* out) {
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)));
     return 0;
 }
-extern "C" int fjsp_debug_pgstamps(unsigned long long* out) {
+extern "C" int fjsp_debug_pgstamps(unsigned long long* out) {   // out[8]: pre-draw [4], emit [4]
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pgstamps), sizeof(unsigned long long) * 4));
+    HIPCHK(hipMemcpyFromSymbol(out + 4, HIP_SYMBOL(g_emitstamps), sizeof(unsigned long long) * 4));
     unsigned long long z[4] = {0};
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_pgstamps), z, sizeof(z)));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_emitstamps), z, sizeof(z)));
     return 0;
 }
 #endif

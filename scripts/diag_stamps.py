@@ -23,7 +23,7 @@ for N in (4096,):
         env.rollout(200, buffers=b); torch.cuda.synchronize()
         buf = (ctypes.c_ulonglong * 8)()
         L.fjsp_debug_stamps(buf)
-        pgb = (ctypes.c_ulonglong * 4)()
+        pgb = (ctypes.c_ulonglong * 8)()
         L.fjsp_debug_pgstamps(pgb)
         env.rollout(200, step0=200, buffers=b); torch.cuda.synchronize()
         L.fjsp_debug_stamps(buf)
@@ -34,4 +34,5 @@ for N in (4096,):
                           "phases": {names[i]: round(buf[i] / waves / steps, 1) for i in range(8)},
                           "predraw_wave": {"busy_cycles_per_step": pgb[0] / max(1, pgb[3]),
                                            "active_step_frac": pgb[1] / max(1, pgb[3]),
-                                           "busy_cycles_per_active_step": pgb[2] / max(1, pgb[1])}}))
+                                           "busy_cycles_per_active_step": pgb[2] / max(1, pgb[1])},
+                          "emit_waves_busy_cycles_per_step": [pgb[4] / max(1, pgb[5]), pgb[6] / max(1, pgb[7])]}))
