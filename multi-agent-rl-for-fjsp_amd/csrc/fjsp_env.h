@@ -434,7 +434,12 @@ constexpr uint32_t DROP_LISTS = (1u << L_STORAGE) | (1u << L_M0Q) | (1u << L_M1Q
 // state words are updated with selects, so a wavefront whose lanes take all 8 actions executes
 // one path instead of the union of 8 branchy ones.  Only the memory operations sit in (two)
 // small guarded blocks: the PICKUP pop's loads and the DROP push's stores.
-FJSP_DEV uint32_t agv_execute(Env& E, const Tables& T, const Cfg& C, int action, int* move_to) {
+// DEFER (the pipelined kernel's AGV-ahead wave): a drop at packaging is not routed here — the
+// station choice needs the Resource counts after the current run phase — but returned in
+// *pend (1 | slot << 1 | code << 9 | colour << 22) for agv_pack_drop.
+template <bool DEFER = false>
+FJSP_DEV uint32_t agv_execute(Env& E, const Tables& T, const Cfg& C, int action, int* move_to,
+                              uint32_t* pend = nullptr) {
     const int loc = E.loc();
     const int carry = E.carry();
     const bool has = carry != NIL;
@@ -456,9 +461,9 @@ FJSP_DEV uint32_t agv_execute(Env& E, const Tables& T, const Cfg& C, int action,
     const bool ok7 = action == 7 && has && ((cond >> loc) & 1u);
     const bool at_pick = loc == LOC_PICKUP, at_store = loc == LOC_STORAGE, at_pack = loc == LOC_PACK;
     const bool store_full = E.ll(L_STORAGE) >= C.storage_cap;
-    const int st = pkg_station(E, C, E.carry_color());
+    const int st = DEFER ? -1 : pkg_station(E, C, E.carry_color());
     const int base = nib(nibs(0xF, 0xF, L_M1Q, L_M0Q, L_STORAGE, L_PKG), loc);
-    const bool no_dst = base == 0xF || (at_store && store_full) || (at_pack && st < 0);
+    const bool no_dst = base == 0xF || (at_store && store_full) || (at_pack && (DEFER || st < 0));
     const int dst = no_dst ? -1 : base + (at_pack ? st : 0);
     // memory: pop (loads) / push (stores)
     uint32_t next = 0, scode = 0, ow = 0;
@@ -489,13 +494,17 @@ FJSP_DEV uint32_t agv_execute(Env& E, const Tables& T, const Cfg& C, int action,
         E.w[7 + i] = v;
     }
     // packaging station: the dropped tray's products join its queue (PackagingAgent.add_tray)
-    const bool to_st = push && at_pack;
+    if (!DEFER) {
+        const bool to_st = push && at_pack;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t wk = E.w[20 + k];
-        const uint32_t qf = ((wk >> 2) & 0xFFu) == (uint32_t)NIL ? (uint32_t)carry : ((wk >> 2) & 0xFFu);
-        const uint32_t nw = (wk & ~(0xFFu << 2) & 0x3FFFFu) | (qf << 2) | (((wk >> 18) + (uint32_t)tc_count(code)) << 18);
-        E.w[20 + k] = (to_st && st == k) ? nw : wk;
+        for (int k = 0; k < 4; k++) {
+            const uint32_t wk = E.w[20 + k];
+            const uint32_t qf = ((wk >> 2) & 0xFFu) == (uint32_t)NIL ? (uint32_t)carry : ((wk >> 2) & 0xFFu);
+            const uint32_t nw = (wk & ~(0xFFu << 2) & 0x3FFFFu) | (qf << 2) | (((wk >> 18) + (uint32_t)tc_count(code)) << 18);
+            E.w[20 + k] = (to_st && st == k) ? nw : wk;
+        }
+    } else {
+        *pend = (ok7 && at_pack) ? (1u | ((uint32_t)carry << 1) | ((uint32_t)code << 9) | ((uint32_t)E.carry_color() << 22)) : 0u;
     }
     // AGV word: carried tray (pickup) / empty hands (drop)
     const uint32_t rg = tc_range((int)scode);
@@ -509,7 +518,7 @@ FJSP_DEV uint32_t agv_execute(Env& E, const Tables& T, const Cfg& C, int action,
     // add_empty_tray at the pickup station; lost tray / products flags
     E.set_pool(E.pool() + ((ok7 && at_pick) ? 1 : 0));
     uint32_t fl = (ok7 && at_store && store_full) ? ST_TRAY_LOST : 0u;
-    fl |= (ok7 && at_pack && st < 0) ? ST_PROD_LOST : 0u;
+    fl |= (!DEFER && ok7 && at_pack && st < 0) ? ST_PROD_LOST : 0u;
     E.w[2] |= fl;
     if (moved) *move_to = ml;
     // result: 1 success, 2 invalid, 4 moved, 8 pickup, 16 drop, 32 to packaging; 16.. distance
@@ -519,6 +528,28 @@ FJSP_DEV uint32_t agv_execute(Env& E, const Tables& T, const Cfg& C, int action,
     r |= ok6 ? 8u : 0u;
     r |= ok7 ? (16u | (at_pack ? 32u : 0u)) : 0u;
     return r;
+}
+
+// The packaging half of a deferred AGV drop (agv_execute<true>): route the tray to its station
+// (FJSPSimulation.add_tray_to_packaging) with the Resource counts as they are now.
+FJSP_DEV void agv_pack_drop(Env& E, const Tables& T, const Cfg& C, uint32_t pend) {
+    const int carry = (int)((pend >> 1) & 0xFFu), code = (int)((pend >> 9) & 0x1FFFu);
+    const int st = pkg_station(E, C, (int)((pend >> 22) & 3u));
+    if (st < 0) { E.flag(ST_PROD_LOST); return; }
+    const uint32_t lwd = lword<(0xFu << L_PKG)>(E, L_PKG + st);
+    T.snext[carry * T.stride] = (uint8_t)NIL;
+    T.scstep[carry * T.stride] = PKG_CONT;
+    const uint32_t nd = lwd >> 16;
+    if (nd != 0) T.snext[((lwd >> 8) & 0xFFu) * T.stride] = (uint8_t)carry;
+    set_lword<(0xFu << L_PKG)>(E, L_PKG + st,
+                                (nd == 0 ? (uint32_t)carry : (lwd & 0xFFu)) | ((uint32_t)carry << 8) | ((nd + 1) << 16));
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t wk = E.w[20 + k];
+        const uint32_t qf = ((wk >> 2) & 0xFFu) == (uint32_t)NIL ? (uint32_t)carry : ((wk >> 2) & 0xFFu);
+        const uint32_t nw = (wk & ~(0xFFu << 2) & 0x3FFFFu) | (qf << 2) | (((wk >> 18) + (uint32_t)tc_count(code)) << 18);
+        E.w[20 + k] = (st == k) ? nw : wk;
+    }
 }
 
 // MachineAgent.execute_action (MachineAgent.py:99-139); grant happens in the run.
@@ -892,15 +923,16 @@ FJSP_DEV double global_reward8(const Cfg& C, int orders_done, int packaged) {
 // Actions in dict order, then env.run in closed form.  actions[a] for agent a (canonical order);
 // order = execution order (CANON -> 0..7).  Fills res[8]; returns the shared global reward / 8.
 struct NoMid {
-    FJSP_DEV void operator()(const Env&) const {}
+    FJSP_DEV void operator()(const Env&, int) const {}
 };
-// mid(E) runs right after the AGV's action (the pipelined kernel hands the pickup station's
-// state to another wave there); pick_done: res[0] already holds the pickup's result, applied
-// to E by the caller (the pickup ran ahead on that wave).
+// mid(E, move_to) runs right after the machines' actions (the pipelined kernel hands the
+// pickup / AGV state to other waves there).  ahead: the pickup station and the AGV already
+// acted (on those waves, from the previous step's hand-off); res[0], res[1] hold their results,
+// the caller applied their state words and ahead_move is the AGV's move target.
 template <bool CANON, class Mid = NoMid>
 FJSP_DEV double env_advance(Env& E, const Tables& T, const Cfg& C, const int* act, const uint8_t* order,
-                            uint32_t* res, Mid mid = Mid(), bool pick_done = false) {
-    int move_to = 0, m_start[2] = {-1, -1}, p_started[4] = {0, 0, 0, 0};
+                            uint32_t* res, Mid mid = Mid(), bool ahead = false, int ahead_move = 0) {
+    int move_to = ahead ? ahead_move : 0, m_start[2] = {-1, -1}, p_started[4] = {0, 0, 0, 0};
     const int products_before = E.total_packaged();
     // 1. actions in dict order (FJSPSimulation.py:172-174)
 #pragma unroll
@@ -910,8 +942,8 @@ FJSP_DEV double env_advance(Env& E, const Tables& T, const Cfg& C, const int* ac
         uint32_t r = 0;
         if (ac != 255) {
             switch (a) {
-            case 0: r = pick_done ? res[0] : pickup_execute(E, T, C, ac); break;
-            case 1: r = agv_execute(E, T, C, ac, &move_to); break;
+            case 0: r = ahead ? res[0] : pickup_execute(E, T, C, ac); break;
+            case 1: r = ahead ? res[1] : agv_execute(E, T, C, ac, &move_to); break;
             case 2: r = machine_execute<0>(E, T, ac, &m_start[0]); break;
             case 3: r = machine_execute<1>(E, T, ac, &m_start[1]); break;
             case 4: r = pack_execute<0>(E, ac, &p_started[0]); break;
@@ -922,7 +954,7 @@ FJSP_DEV double env_advance(Env& E, const Tables& T, const Cfg& C, const int* ac
         }
         res[a] = r;
         if (CANON) FJSP_STAMP_AGENT(E, i);
-        if (CANON && i == 1) mid(E);
+        if (CANON && i == 3) mid(E, move_to);
     }
     FJSP_STAMP(E, 1);
     // 2. env.run(until=now+step_size) in closed form

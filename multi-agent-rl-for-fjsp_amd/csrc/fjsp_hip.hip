@@ -631,13 +631,18 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
     __shared__ uint32_t s_nxt[PG ? MAX_ORDERS * BLOCK : 1];
     __shared__ uint32_t s_mb[PG ? 4 : 1][2][BLOCK];   // sim: epi | nord << 8, cursor word; pre-draw: ready, cursor
     __shared__ uint4 s_cp[PG ? FJSP_PG_CR : 1][3][BLOCK];   // MT rows in flight (pre-draw copies)
-    // pickup ahead (PG, uniform-random actions): the sim wave posts the pickup station's state
-    // after the AGV's action of step k (s_pk_in, then s_pkflag = k + 1); emit wave 1 runs step
-    // k + 1's pickup on it while the sim wave finishes step k and posts the new state words and
-    // the result (s_pk_out / s_pk_res), which the sim wave applies at the top of step k + 1.
-    __shared__ uint4 s_pk_in[PG ? BLOCK : 1], s_pk_out[PG ? BLOCK : 1];
-    __shared__ uint2 s_pk_res[PG ? BLOCK : 1];
-    __shared__ uint32_t s_pkflag;
+    // Pickup + AGV ahead (PG, uniform-random actions).  Neither agent's next action depends on
+    // anything the packaging agents or the run phase of the current step change, except where
+    // a drop at packaging routes the tray (deferred: agv_pack_drop).  So after the machines'
+    // actions of step k the sim wave posts the words they read (s_post, then s_postflag = k+1);
+    // emit wave 1 runs step k+1's pickup on them (s_pick, s_pickflag = k+1), emit wave 2 step
+    // k+1's AGV on both, while the sim wave finishes step k; at the top of step k+1 the sim
+    // wave applies both (lanes that just reset run the two agents themselves).
+    constexpr int NPOST = 10;   // W0, W4, W5, W6 (loc after the move), W7..W12 (lists 0..5)
+    __shared__ uint32_t s_post[PG ? NPOST : 1][BLOCK];
+    __shared__ uint32_t s_pick[PG ? 6 : 1][BLOCK];   // next_order, W4, W5, W7, result, flags
+    __shared__ uint32_t s_agv[PG ? 12 : 1][BLOCK];   // W5, W6, W7..W12, result, flags, move, pend
+    __shared__ uint32_t s_postflag, s_pickflag;
     __shared__ uint16_t s_code[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint8_t s_next[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint16_t s_cstep[LDS ? MAX_SLOTS * BLOCK : 1];
@@ -659,7 +664,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
         s_act[0][1][lane] = pack_actions(act, 4);
     }
     if constexpr (PG) {   // step-0 mailboxes
-        if (threadIdx.x == 0) s_pkflag = 0;
+        if (threadIdx.x == 0) { s_postflag = 0; s_pickflag = 0; }
         if (wave == 0 && valid) {
             s_mb[0][0][lane] = ((S.words[e] >> 16) & 0xFFu) << 8;   // episode counter 0 | num_orders
             s_mb[1][0][lane] = S.words[3 * n + e];
@@ -716,30 +721,39 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
                 }
                 FJSP_STAMP(E, 0);
                 uint32_t res[NA];
-                bool pick_done = false;
+                bool ahead = false;
+                int ahead_move = 0;
                 if constexpr (PG) {
-                    if (pre && !fresh) {   // step k's pickup ran ahead on emit wave 1
-                        const uint4 po = s_pk_out[lane];
-                        const uint2 pr = s_pk_res[lane];
-                        E.w[0] = (E.w[0] & 0x00FFFFFFu) | (po.x << 24);
-                        E.w[4] = po.y;
-                        E.w[5] = po.z;
-                        E.w[7 + L_PREADY] = po.w;
-                        E.w[2] |= pr.y;
-                        res[0] = pr.x;
-                        pick_done = true;
+                    if (pre && !fresh) {   // step k's pickup and AGV ran on the emit waves
+                        E.w[0] = (E.w[0] & 0x00FFFFFFu) | (s_pick[0][lane] << 24);
+                        E.w[4] = s_pick[1][lane];
+                        res[0] = s_pick[4][lane];
+#pragma unroll
+                        for (int i = 0; i < 8; i++) E.w[5 + i] = s_agv[i][lane];   // W5..W12
+                        res[1] = s_agv[8][lane];
+                        E.w[2] |= s_pick[5][lane] | s_agv[9][lane];
+                        ahead_move = (int)s_agv[10][lane];
+                        const uint32_t pend = s_agv[11][lane];
+                        if (pend) agv_pack_drop(E, T, C, pend);
+                        ahead = true;
                     }
                 }
-                auto mid = [&](const Env& Em) {
+                auto mid = [&](const Env& Em, int mv) {
                     if constexpr (PG) {
                         if (pre) {
-                            s_pk_in[lane] = make_uint4(Em.w[0], Em.w[4], Em.w[5], Em.w[7 + L_PREADY]);
-                            __hip_atomic_store(&s_pkflag, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            s_post[0][lane] = Em.w[0];
+                            s_post[1][lane] = Em.w[4];
+                            s_post[2][lane] = Em.w[5];
+                            s_post[3][lane] = mv ? ((Em.w[6] & ~7u) | (uint32_t)mv) : Em.w[6];
+#pragma unroll
+                            for (int i = 0; i < 6; i++) s_post[4 + i][lane] = Em.w[7 + i];
+                            __hip_atomic_store(&s_postflag, (uint32_t)(k + 1), __ATOMIC_RELEASE,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
                     }
                 };
                 const int nc0 = E.ncompleted(), tp0 = E.total_packaged();
-                (void)env_advance<true>(E, T, C, act, nullptr, res, mid, pick_done);   // g/8: the emit wave
+                (void)env_advance<true>(E, T, C, act, nullptr, res, mid, ahead, ahead_move);   // g/8: the emit wave
                 flag_obs_overflow(E);
                 uint32_t v[SNAP_N];
                 int j = 0;
@@ -929,26 +943,63 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
 #ifdef FJSP_STAMPS
             const uint64_t et0 = __builtin_amdgcn_s_memtime();
 #endif
-            if (k > 0 && valid) {
-                const uint32_t t = (uint32_t)(k - 1);
-                uint32_t v[SNAP_N];
+            // order within a step (PG): wave 1 first draws step k + 1's actions, writes step
+            // k - 1's rewards and runs step k + 1's pickup as soon as the sim wave posts (early
+            // in step k), then the observation fields; wave 2 writes its fields, then runs step
+            // k + 1's AGV (needs that pickup)
+            int act_next[NA];
+            if (part == 0 && pre && k + 1 < K) {
+                synth_uniform(seed, gid0 + (uint32_t)e, step0 + (uint32_t)(k + 1), act_next);
+                s_act[(k + 1) & 1][0][lane] = pack_actions(act_next, 0);
+                s_act[(k + 1) & 1][1][lane] = pack_actions(act_next, 4);
+            }
+            const bool have = k > 0 && valid;
+            const uint32_t t = (uint32_t)(k - 1);
+            uint32_t v[SNAP_N];
+            Env E;
+            if (have) {
                 snap_get(snap[(k - 1) & 1], lane, v);
-                Env E;
                 int j = 0;
 #pragma unroll
                 for (int i = 0; i < NSTATE; i++) E.w[i] = ((SNAP_WORDS >> i) & 1u) ? v[j++] : 0u;
-                const StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, ue};
-                if (part == 0) {   // rewards (+ everything when NEMIT == 1)
-                    if (out.rewards) {
-                        const uint32_t gs = v[SNAP_GSTAT];
-                        const double g8 = global_reward8(C, (int)(gs & 0xFFFFu), (int)(gs >> 16));
+            }
+            const StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, ue};
+            if (part == 0 && have && out.rewards) {
+                const uint32_t gs = v[SNAP_GSTAT];
+                const double g8 = global_reward8(C, (int)(gs & 0xFFFFu), (int)(gs >> 16));
 #pragma unroll
-                        for (int a = 0; a < NA; a++) {
-                            const uint32_t r = v[SNAP_RES + a];
-                            st32(out.rewards, (t * NA + (uint32_t)a) * n + ue,
-                                 g8 + C.lut[reward_index(a, r & 0xFFFF00FFu, (int)((r >> 8) & 0xFu))]);
-                        }
+                for (int a = 0; a < NA; a++) {
+                    const uint32_t r = v[SNAP_RES + a];
+                    st32(out.rewards, (t * NA + (uint32_t)a) * n + ue,
+                         g8 + C.lut[reward_index(a, r & 0xFFFF00FFu, (int)((r >> 8) & 0xFu))]);
+                }
+            }
+            if constexpr (PG) {   // step k + 1's pickup, once the sim wave has posted its state
+                if (part == 0 && pre && k + 1 < K) {
+                    while (__hip_atomic_load(&s_postflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (uint32_t)(k + 1))
+                        __builtin_amdgcn_s_sleep(1);
+                    if (valid) {
+                        Env Ep;
+#pragma unroll
+                        for (int i = 0; i < NSTATE; i++) Ep.w[i] = 0u;
+                        Ep.w[0] = s_post[0][lane];
+                        Ep.w[4] = s_post[1][lane];
+                        Ep.w[5] = s_post[2][lane];
+                        Ep.w[7 + L_PREADY] = s_post[4 + L_PREADY][lane];
+                        const Tables Tp{s_orders + lane, s_code + lane, s_next + lane, s_cstep + lane, BLOCK};
+                        const uint32_t r = pickup_execute(Ep, Tp, C, act_next[0]);
+                        s_pick[0][lane] = Ep.w[0] >> 24;
+                        s_pick[1][lane] = Ep.w[4];
+                        s_pick[2][lane] = Ep.w[5];
+                        s_pick[3][lane] = Ep.w[7 + L_PREADY];
+                        s_pick[4][lane] = r;
+                        s_pick[5][lane] = Ep.w[2];
                     }
+                    __hip_atomic_store(&s_pickflag, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            if (have) {
+                if (part == 0) {   // int32 / float32 fields (+ everything when NEMIT == 1)
                     PartSink<NEMIT == 1 ? -1 : 0> ps{sink};
                     observe(E, C, ps);
                 }
@@ -965,27 +1016,30 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
                     if (out.status) st32(out.status, t * n + ue, E.status());
                 }
             }
-            if (part == 0 && pre && k + 1 < K) {
-                int act[NA];
-                synth_uniform(seed, gid0 + (uint32_t)e, step0 + (uint32_t)(k + 1), act);
-                s_act[(k + 1) & 1][0][lane] = pack_actions(act, 0);
-                s_act[(k + 1) & 1][1][lane] = pack_actions(act, 4);
-                if constexpr (PG) {   // step k + 1's pickup, once the sim wave has posted its state
-                    while (__hip_atomic_load(&s_pkflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (uint32_t)(k + 1))
+            if constexpr (PG) {   // step k + 1's AGV, on the posted state and that step's pickup
+                if (part == 1 && pre && k + 1 < K) {
+                    while (__hip_atomic_load(&s_pickflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (uint32_t)(k + 1))
                         __builtin_amdgcn_s_sleep(1);
                     if (valid) {
-                        const uint4 pi = s_pk_in[lane];
-                        Env Ep;
+                        Env Ea;
 #pragma unroll
-                        for (int i = 0; i < NSTATE; i++) Ep.w[i] = 0u;
-                        Ep.w[0] = pi.x;
-                        Ep.w[4] = pi.y;
-                        Ep.w[5] = pi.z;
-                        Ep.w[7 + L_PREADY] = pi.w;
-                        const Tables Tp{s_orders + lane, s_code + lane, s_next + lane, s_cstep + lane, BLOCK};
-                        const uint32_t r = pickup_execute(Ep, Tp, C, act[0]);
-                        s_pk_out[lane] = make_uint4(Ep.w[0] >> 24, Ep.w[4], Ep.w[5], Ep.w[7 + L_PREADY]);
-                        s_pk_res[lane] = make_uint2(r, Ep.w[2]);
+                        for (int i = 0; i < NSTATE; i++) Ea.w[i] = 0u;
+                        Ea.w[5] = s_pick[2][lane];
+                        Ea.w[6] = s_post[3][lane];
+#pragma unroll
+                        for (int i = 0; i < 6; i++) Ea.w[7 + i] = s_post[4 + i][lane];
+                        Ea.w[7 + L_PREADY] = s_pick[3][lane];
+                        const Tables Ta{s_orders + lane, s_code + lane, s_next + lane, s_cstep + lane, BLOCK};
+                        const int a1 = (int)((s_act[(k + 1) & 1][0][lane] >> 8) & 0xFFu);
+                        int mv = 0;
+                        uint32_t pend = 0;
+                        const uint32_t r = agv_execute<true>(Ea, Ta, C, a1, &mv, &pend);
+#pragma unroll
+                        for (int i = 0; i < 8; i++) s_agv[i][lane] = Ea.w[5 + i];
+                        s_agv[8][lane] = r;
+                        s_agv[9][lane] = Ea.w[2];
+                        s_agv[10][lane] = (uint32_t)mv;
+                        s_agv[11][lane] = pend;
                     }
                 }
             }
