@@ -287,6 +287,16 @@ struct Env {
     FJSP_DEV int p_startn(int s) const { return (int)w[26 + s]; }
 };
 
+// OR into an order word shared by two waves (k_step_ag: the machines' processed bits and the
+// packaging completions update one word from different wavefronts); returns the old word.
+#ifdef __HIP__
+FJSP_DEV uint32_t order_or(uint32_t* p, uint32_t v) {
+    return __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+#else
+inline uint32_t order_or(uint32_t* p, uint32_t v) { const uint32_t o = *p; *p = o | v; return o; }
+#endif
+
 // ---- table accessors: element i of a per-env table = base[i * stride]
 struct Tables {
     uint32_t* orders;   // [MAX_ORDERS]
@@ -611,20 +621,27 @@ FJSP_DEV void machine_grant(Env& E, const Cfg& C, int slot, int code, int step) 
     if (busy) E.set_m_next(M, step + (M == 0 ? C.ptk_small : C.ptk_big));
     else E.set_m_prog(M, 1);
 }
+// AT: the order words are shared with another wave (k_step_ag) -> atomic OR, no read.
+template <bool AT = false>
 FJSP_DEV void machines_run(Env& E, const Tables& T, const Cfg& C, int s0, int s1) {
     const int step = E.step();
     const bool due0 = E.m_busy(0) && E.m_next(0) == step, due1 = E.m_busy(1) && E.m_next(1) == step;
     const int c0 = E.m_code(0), c1 = E.m_code(1);
     const int o0 = tc_order(c0), o1 = tc_order(c1);
-    // independent loads (addresses clamped to valid entries when unused)
-    const uint32_t w0 = T.orders[(due0 ? o0 : 0) * T.stride];
-    const uint32_t w1 = T.orders[(due1 ? o1 : 0) * T.stride];
     const int g0 = T.scode[(s0 >= 0 ? s0 : 0) * T.stride];
     const int g1 = T.scode[(s1 >= 0 ? s1 : 0) * T.stride];
     const uint32_t b0 = 1u << (tc_start(c0) + E.m_k(0)), b1 = 1u << (tc_start(c1) + E.m_k(1));
     // product.is_processed = True
-    if (due0) T.orders[o0 * T.stride] = w0 | b0;
-    if (due1) T.orders[o1 * T.stride] = ((due0 && o0 == o1) ? (w0 | b0) : w1) | b1;
+    if constexpr (AT) {
+        if (due0) order_or(&T.orders[o0 * T.stride], b0);
+        if (due1) order_or(&T.orders[o1 * T.stride], b1);
+    } else {
+        // independent loads (addresses clamped to valid entries when unused)
+        const uint32_t w0 = T.orders[(due0 ? o0 : 0) * T.stride];
+        const uint32_t w1 = T.orders[(due1 ? o1 : 0) * T.stride];
+        if (due0) T.orders[o0 * T.stride] = w0 | b0;
+        if (due1) T.orders[o1 * T.stride] = ((due0 && o0 == o1) ? (w0 | b0) : w1) | b1;
+    }
     if (due0) machine_done<0>(E, C, step);
     if (s0 >= 0) machine_grant<0>(E, C, s0, g0, step);
     if (due1) machine_done<1>(E, C, step);
@@ -646,7 +663,7 @@ FJSP_DEV bool pack_due(const Env& E, const Tables& T, int step) {
     const uint16_t cs = T.scstep[(inflight ? h : 0) * T.stride];   // slot 0 always exists
     return inflight && cs == (uint16_t)step;
 }
-template <int S>
+template <int S, bool AT = false>
 FJSP_DEV void pack_run(Env& E, const Tables& T, const Cfg& C, int started, bool due, int* orders_done) {
     constexpr int L = L_PKG + S;
     const int step = E.step();
@@ -659,13 +676,15 @@ FJSP_DEV void pack_run(Env& E, const Tables& T, const Cfg& C, int started, bool 
         const int s = list_pop<L>(E, T);
         const int code = T.scode[s * T.stride];
         const int o = tc_order(code);
-        uint32_t w = T.orders[o * T.stride] | (tc_range(code) << 9);
+        const uint32_t add = tc_range(code) << 9;
+        uint32_t w = (AT ? order_or(&T.orders[o * T.stride], add) : T.orders[o * T.stride]) | add;
         const uint32_t full = (1u << ow_n(w)) - 1u;
         if (!(w & (1u << 18)) && ((w >> 9) & full) == full) {   // _check_order_completions
             w |= 1u << 18;
             *orders_done += 1;
+            if (AT) order_or(&T.orders[o * T.stride], 1u << 18);   // only this wave writes the bit
         }
-        T.orders[o * T.stride] = w;
+        if (!AT) T.orders[o * T.stride] = w;
         done += tc_count(code);
         // the batch continues while the next run is granted (not qfirst) and not a batch start
         due = E.ll(L) > 0 && E.lh(L) != qfirst && T.scstep[E.lh(L) * T.stride] == PKG_CONT;
@@ -681,6 +700,51 @@ FJSP_DEV void pack_run(Env& E, const Tables& T, const Cfg& C, int started, bool 
         T.scstep[qfirst * T.stride] = (uint16_t)(step + C.ptk_pack);
         const int inflight = E.p_inflight(S) + E.p_queued(S);
         // busy = 1, hascur = 1, qfirst = NIL, inflight += queued, queued = 0
+        E.w[20 + S] = 3u | ((uint32_t)NIL << 2) | ((uint32_t)(inflight & 0xFF) << 10);
+    }
+}
+
+// k_step_ag splits pack_run around the action phase.  pack_complete: the completions of the
+// station's in-flight batch due at this step (NORMAL events older than the step's actions,
+// PackagingAgent.py:143-147) computed BEFORE the AGV's drop and the station's action: the
+// completed runs leave the head of the station's list (a drop joins its tail, and the batch
+// ends at the first run that is not PKG_CONT either way) and their products are ORed into the
+// order table; returns the products packaged.  The counters and the busy flag are left as the
+// action phase reads them (routing reads in-flight counts, the action reads busy) and applied
+// by pack_finish together with the grants.
+template <int S>
+FJSP_DEV int pack_complete(Env& E, const Tables& T, bool due, int* orders_done) {
+    constexpr int L = L_PKG + S;
+    const int qfirst = E.p_qfirst(S);
+    int done = 0;
+    while (due) {
+        const int s = list_pop<L>(E, T);
+        const int code = T.scode[s * T.stride];
+        const int o = tc_order(code);
+        const uint32_t add = tc_range(code) << 9;
+        const uint32_t w = order_or(&T.orders[o * T.stride], add) | add;
+        const uint32_t full = (1u << ow_n(w)) - 1u;
+        if (!(w & (1u << 18)) && ((w >> 9) & full) == full) {   // _check_order_completions
+            order_or(&T.orders[o * T.stride], 1u << 18);
+            *orders_done += 1;
+        }
+        done += tc_count(code);
+        due = E.ll(L) > 0 && E.lh(L) != qfirst && T.scstep[E.lh(L) * T.stride] == PKG_CONT;
+    }
+    return done;
+}
+template <int S>
+FJSP_DEV void pack_finish(Env& E, const Tables& T, const Cfg& C, int started, int done) {
+    if (started && E.p_inflight(S) + E.p_queued(S) > C.pkg_cap) E.flag(ST_PKG_WAIT | ST_DIVERGED);
+    if (done) {
+        E.set_p_completed(S, E.p_completed(S) + done);
+        E.set_total_packaged(E.total_packaged() + done);
+        E.set_p_inflight(S, E.p_inflight(S) - done);
+        E.set_p_busy(S, 0);
+    }
+    if (started) {
+        T.scstep[E.p_qfirst(S) * T.stride] = (uint16_t)(E.step() + C.ptk_pack);
+        const int inflight = E.p_inflight(S) + E.p_queued(S);
         E.w[20 + S] = 3u | ((uint32_t)NIL << 2) | ((uint32_t)(inflight & 0xFF) << 10);
     }
 }

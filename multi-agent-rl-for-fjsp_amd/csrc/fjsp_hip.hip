@@ -34,6 +34,18 @@ constexpr int MT_N = 624;
 __device__ unsigned long long g_stamps[8];
 __device__ unsigned long long g_pgstamps[4];   // pre-draw wave: busy cycles, active steps, busy in active steps, steps
 __device__ unsigned long long g_emitstamps[4];   // emit waves 1, 2: busy cycles, steps
+__device__ unsigned long long g_agstamps[16];   // k_step_ag: per wave [busy, wait] cycles, epochs
+#define AG_T0() const uint64_t _ag_t0 = __builtin_amdgcn_s_memtime()
+#define AG_ACC(v) ((v) += __builtin_amdgcn_s_memtime() - _ag_t0)
+#else
+#define AG_T0() ((void)0)
+#define AG_ACC(v) ((void)0)
+#endif
+#ifdef FJSP_X_DEBUG   // bring-up build only: per-lane values of workgroup 1, step 0
+__device__ uint32_t g_dbg[8][64];
+#define FJSP_DBG(i, v) do { if (blockIdx.x == 1) g_dbg[i][lane] = (v); } while (0)
+#else
+#define FJSP_DBG(i, v) ((void)0)
 #endif
 
 struct DevState {
@@ -619,6 +631,139 @@ __device__ __forceinline__ uint32_t pack_actions(const int* act, int lo) {
 #ifndef FJSP_PG_PB
 #define FJSP_PG_PB 8   // ... and words drawn per env
 #endif
+// The pre-draw wave (k_step_pipe<..., PG>, k_step_ag): see the comment above k_step_pipe.
+// s_mb / s_cp / s_nxt are the kernel's LDS mailboxes, row-copy staging and next tables.
+// FINAL_MB: the sim side also posts in the final epoch K (k_step_ag resets at the top of an
+// epoch), so a table it consumed or abandoned there must not be stored as ready.
+template <int CR, int PB, bool FINAL_MB = false>
+__device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane, int e, bool valid,
+                                             uint32_t (*s_mb)[2][BLOCK], uint4 (*s_cp)[3][BLOCK], uint32_t* s_nxt) {
+    const uint32_t n = (uint32_t)S.n;
+    // the pre-draw wave: 0 idle, 1 copying the live row, 2 drawing, 3 table ready
+    int ph = 0, nord = 0, pos = 0, g = 0;
+    uint32_t src = 0, my = 0x100u;   // live row at the start of the pre-draw; episode it is for
+    OrderDraw d{0, 0, 0, 0, 0u};
+    if (valid) {
+        const uint32_t pg = S.words[(size_t)PGW * n + e];
+        if (pg & 1u) {
+            ph = 3;
+            my = 0;
+            nord = (int)((pg >> 24) & 0x7Fu);
+            pos = (int)((pg >> 1) & 0x3FFu);
+            g = (int)((pg >> 11) & 0x3FFu);
+            src = ((pg >> 21) & 1u) ^ (nord > 0 ? 1u : 0u);
+        }
+    }
+#ifdef FJSP_STAMPS
+    uint64_t pg_busy = 0, pg_act = 0, pg_busy_act = 0;
+#endif
+    for (int k = 0; k <= K; k++) {
+#ifdef FJSP_STAMPS
+        const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+        bool pg_active = false;
+#endif
+        if (valid) {
+            const uint32_t si = s_mb[0][k & 1][lane];
+            if ((si & 0xFFu) != my) {   // a new episode: start over from its stream position
+                const uint32_t sw = s_mb[1][k & 1][lane];
+                my = si & 0xFFu;
+                nord = (int)((si >> 8) & 0x7Fu);
+                src = sw >> 31;
+                pos = (int)(sw & 0x3FFu);
+                g = (int)((sw >> 16) & 0x3FFu);
+                d = OrderDraw{0, 0, 0, 0, 0u};
+#ifdef FJSP_PG_IDLE
+                ph = 0;   // diagnostic: the pre-draw wave only keeps the mailboxes
+#else
+                ph = nord > 0 ? 1 : 3;
+#endif
+            }
+        }
+        // Copy the live rows of up to CR envs that start a pre-draw (the whole wave, one
+        // env at a time: contiguous 1 KB loads): loads first, the per-lane draw in the shadow
+        // of their latency, then the stores.  Rows copied in step k are first read in k + 1.
+        auto draw_step = [&]() {
+            if (valid && ph == 2) {
+                uint32_t* work = S.mt + ((size_t)(src ^ 1u) * n + e) * MT_N;
+                uint32_t v[PB];
+                int pa, cnt;
+                mt_batch<PB>(work, pos, g, v, pa, cnt);
+                pos += draw_orders<PB>(v, pos - pa, cnt, nord, d, s_nxt + lane, BLOCK);
+                if (pos == MT_N) { pos = 0; g = 0; }
+                if (d.o >= nord) ph = 3;
+            }
+        };
+        uint64_t need = __ballot(valid && ph == 1);
+#ifdef FJSP_STAMPS
+        pg_active = need != 0 || __ballot(valid && ph == 2) != 0;
+#endif
+        if (need) {
+            // rows go through LDS by DMA (global_load_lds: no VGPRs held across the draw);
+            // slots beyond the envs waiting re-copy the first env's row (identical stores)
+            const int first = __builtin_ctzll(need);
+            int ls[CR];
+#pragma unroll
+            for (int r = 0; r < CR; r++) {
+                ls[r] = need ? __builtin_ctzll(need) : first;
+                need &= need - 1;
+                const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)src, ls[r]);
+                const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls[r];
+                const uint4* rs = reinterpret_cast<const uint4*>(S.mt + ((size_t)sl * n + el) * MT_N);
+#pragma unroll
+                for (int i = 0; i < 3; i++)
+                    __builtin_amdgcn_global_load_lds(
+                        (__attribute__((address_space(1))) void*)(rs + min(lane + 64 * i, MT_N / 4 - 1)),
+                        (__attribute__((address_space(3))) void*)&s_cp[r][i][0], 16, 0, 0);
+            }
+            draw_step();
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the row DMAs have landed
+#pragma unroll
+            for (int r = 0; r < CR; r++) {
+                const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)src, ls[r]);
+                const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls[r];
+                uint4* rd = reinterpret_cast<uint4*>(S.mt + ((size_t)(sl ^ 1u) * n + el) * MT_N);
+                rd[lane] = s_cp[r][0][lane];
+                rd[lane + 64] = s_cp[r][1][lane];
+                if (lane + 128 < MT_N / 4) rd[lane + 128] = s_cp[r][2][lane];
+                if (lane == ls[r]) ph = 2;
+            }
+        } else {
+            draw_step();
+        }
+        if (valid) {
+            const uint32_t wrow = nord > 0 ? (src ^ 1u) : src;
+            s_mb[2][(k + 1) & 1][lane] = (ph == 3 ? 1u : 0u) | (my << 1) | ((uint32_t)nord << 9);
+            s_mb[3][(k + 1) & 1][lane] = (uint32_t)pos | ((uint32_t)g << 16) | (wrow << 31);
+        }
+#ifdef FJSP_STAMPS
+        {
+            const uint64_t dt = __builtin_amdgcn_s_memtime() - pt0;
+            pg_busy += dt;
+            if (pg_active) { pg_act += 1; pg_busy_act += dt; }
+        }
+#endif
+        __syncthreads();
+    }
+#ifdef FJSP_STAMPS
+    if (lane == 0) {
+        atomicAdd(&g_pgstamps[0], (unsigned long long)pg_busy);
+        atomicAdd(&g_pgstamps[1], (unsigned long long)pg_act);
+        atomicAdd(&g_pgstamps[2], (unsigned long long)pg_busy_act);
+        atomicAdd(&g_pgstamps[3], (unsigned long long)(K + 1));
+    }
+#endif
+    if (valid) {
+        uint32_t pg = 0;
+        if (FINAL_MB && (s_mb[0][(K + 1) & 1][lane] & 0xFFu) != my) ph = 0;   // reset in the final epoch
+        if (ph == 3) {
+            const uint32_t wrow = nord > 0 ? (src ^ 1u) : src;
+            pg = 1u | ((uint32_t)pos << 1) | ((uint32_t)g << 11) | (wrow << 21) | ((uint32_t)nord << 24);
+            for (int o = 0; o < nord; o++) S.nxt[(size_t)o * n + e] = s_nxt[o * BLOCK + lane];
+        }
+        S.words[(size_t)PGW * n + e] = pg;
+    }
+}
+
 template <bool LDS, int NEMIT, bool PG = false>
 __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2))) k_step_pipe(DevState S, Cfg C, int K, uint64_t seed,
                                                               uint32_t gid0, uint32_t step0, int mode, int autoreset,
@@ -809,128 +954,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
             for (int i = 0; i < 8; i++) atomicAdd((unsigned long long*)&g_stamps[i], (unsigned long long)E.st_acc[i]);
 #endif
     } else if (PG && wave == 1 + NEMIT) {
-        // the pre-draw wave: 0 idle, 1 copying the live row, 2 drawing, 3 table ready
-        int ph = 0, nord = 0, pos = 0, g = 0;
-        uint32_t src = 0, my = 0x100u;   // live row at the start of the pre-draw; episode it is for
-        OrderDraw d{0, 0, 0, 0, 0u};
-        if (valid) {
-            const uint32_t pg = S.words[(size_t)PGW * n + e];
-            if (pg & 1u) {
-                ph = 3;
-                my = 0;
-                nord = (int)((pg >> 24) & 0x7Fu);
-                pos = (int)((pg >> 1) & 0x3FFu);
-                g = (int)((pg >> 11) & 0x3FFu);
-                src = ((pg >> 21) & 1u) ^ (nord > 0 ? 1u : 0u);
-            }
-        }
-#ifdef FJSP_STAMPS
-        uint64_t pg_busy = 0, pg_act = 0, pg_busy_act = 0;
-#endif
-        for (int k = 0; k <= K; k++) {
-#ifdef FJSP_STAMPS
-            const uint64_t pt0 = __builtin_amdgcn_s_memtime();
-            bool pg_active = false;
-#endif
-            if (valid) {
-                const uint32_t si = s_mb[0][k & 1][lane];
-                if ((si & 0xFFu) != my) {   // a new episode: start over from its stream position
-                    const uint32_t sw = s_mb[1][k & 1][lane];
-                    my = si & 0xFFu;
-                    nord = (int)((si >> 8) & 0x7Fu);
-                    src = sw >> 31;
-                    pos = (int)(sw & 0x3FFu);
-                    g = (int)((sw >> 16) & 0x3FFu);
-                    d = OrderDraw{0, 0, 0, 0, 0u};
-#ifdef FJSP_PG_IDLE
-                    ph = 0;   // diagnostic: the pre-draw wave only keeps the mailboxes
-#else
-                    ph = nord > 0 ? 1 : 3;
-#endif
-                }
-            }
-            // Copy the live rows of up to CR envs that start a pre-draw (the whole wave, one
-            // env at a time: contiguous 1 KB loads): loads first, the per-lane draw in the shadow
-            // of their latency, then the stores.  Rows copied in step k are first read in k + 1.
-            auto draw_step = [&]() {
-                if (valid && ph == 2) {
-                    uint32_t* work = S.mt + ((size_t)(src ^ 1u) * n + e) * MT_N;
-                    uint32_t v[PB];
-                    int pa, cnt;
-                    mt_batch<PB>(work, pos, g, v, pa, cnt);
-                    pos += draw_orders<PB>(v, pos - pa, cnt, nord, d, s_nxt + lane, BLOCK);
-                    if (pos == MT_N) { pos = 0; g = 0; }
-                    if (d.o >= nord) ph = 3;
-                }
-            };
-            uint64_t need = __ballot(valid && ph == 1);
-#ifdef FJSP_STAMPS
-            pg_active = need != 0 || __ballot(valid && ph == 2) != 0;
-#endif
-            if (need) {
-                // rows go through LDS by DMA (global_load_lds: no VGPRs held across the draw);
-                // slots beyond the envs waiting re-copy the first env's row (identical stores)
-                const int first = __builtin_ctzll(need);
-                int ls[CR];
-#pragma unroll
-                for (int r = 0; r < CR; r++) {
-                    ls[r] = need ? __builtin_ctzll(need) : first;
-                    need &= need - 1;
-                    const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)src, ls[r]);
-                    const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls[r];
-                    const uint4* rs = reinterpret_cast<const uint4*>(S.mt + ((size_t)sl * n + el) * MT_N);
-#pragma unroll
-                    for (int i = 0; i < 3; i++)
-                        __builtin_amdgcn_global_load_lds(
-                            (__attribute__((address_space(1))) void*)(rs + min(lane + 64 * i, MT_N / 4 - 1)),
-                            (__attribute__((address_space(3))) void*)&s_cp[r][i][0], 16, 0, 0);
-                }
-                draw_step();
-                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the row DMAs have landed
-#pragma unroll
-                for (int r = 0; r < CR; r++) {
-                    const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)src, ls[r]);
-                    const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls[r];
-                    uint4* rd = reinterpret_cast<uint4*>(S.mt + ((size_t)(sl ^ 1u) * n + el) * MT_N);
-                    rd[lane] = s_cp[r][0][lane];
-                    rd[lane + 64] = s_cp[r][1][lane];
-                    if (lane + 128 < MT_N / 4) rd[lane + 128] = s_cp[r][2][lane];
-                    if (lane == ls[r]) ph = 2;
-                }
-            } else {
-                draw_step();
-            }
-            if (valid) {
-                const uint32_t wrow = nord > 0 ? (src ^ 1u) : src;
-                s_mb[2][(k + 1) & 1][lane] = (ph == 3 ? 1u : 0u) | (my << 1) | ((uint32_t)nord << 9);
-                s_mb[3][(k + 1) & 1][lane] = (uint32_t)pos | ((uint32_t)g << 16) | (wrow << 31);
-            }
-#ifdef FJSP_STAMPS
-            {
-                const uint64_t dt = __builtin_amdgcn_s_memtime() - pt0;
-                pg_busy += dt;
-                if (pg_active) { pg_act += 1; pg_busy_act += dt; }
-            }
-#endif
-            __syncthreads();
-        }
-#ifdef FJSP_STAMPS
-        if (lane == 0) {
-            atomicAdd(&g_pgstamps[0], (unsigned long long)pg_busy);
-            atomicAdd(&g_pgstamps[1], (unsigned long long)pg_act);
-            atomicAdd(&g_pgstamps[2], (unsigned long long)pg_busy_act);
-            atomicAdd(&g_pgstamps[3], (unsigned long long)(K + 1));
-        }
-#endif
-        if (valid) {
-            uint32_t pg = 0;
-            if (ph == 3) {
-                const uint32_t wrow = nord > 0 ? (src ^ 1u) : src;
-                pg = 1u | ((uint32_t)pos << 1) | ((uint32_t)g << 11) | (wrow << 21) | ((uint32_t)nord << 24);
-                for (int o = 0; o < nord; o++) S.nxt[(size_t)o * n + e] = s_nxt[o * BLOCK + lane];
-            }
-            S.words[(size_t)PGW * n + e] = pg;
-        }
+        predraw_wave<CR, PB>(S, K, lane, e, valid, s_mb, s_cp, s_nxt);
     } else {
         // NEMIT == 2: two emit waves split the outputs: wave 1 rewards + int32 / float32
         // observation fields (+ the next step's uniform actions), wave 2 int8 fields, masks,
@@ -953,7 +977,11 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
                 s_act[(k + 1) & 1][0][lane] = pack_actions(act_next, 0);
                 s_act[(k + 1) & 1][1][lane] = pack_actions(act_next, 4);
             }
+#ifdef FJSP_X_NOEMIT   // diagnostic timing build only: the emit waves write no outputs
+            const bool have = false;
+#else
             const bool have = k > 0 && valid;
+#endif
             const uint32_t t = (uint32_t)(k - 1);
             uint32_t v[SNAP_N];
             Env E;
@@ -1057,6 +1085,387 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
     }
 }
 
+// ---------------------------------------------------------------- agent-group pipeline
+// k_step_ag: K fused steps (uniform-random actions, LDS tables, auto-reset with pre-drawn
+// tables), the env's agents split over the wavefronts of its 64-env workgroup so that per step
+// only the AGV -> machines chain is sequential:
+//   AM (wave 0) owns every state word but the packaging ones: it applies the pickup result
+//      P computed during the previous step, runs the AGV (a drop at packaging is deferred,
+//      agv_execute<true>), posts the words P and K need, then runs the machines' actions and
+//      their run phase (MachineAgent.py:99-169), and resets the env (FJSPSimulation.reset,
+//      seed=None) at the top of the next step once K has counted the step's completions;
+//   K  (wave 1) owns the packaging words (W1, W13-16, W20-29): after AM's post it routes the
+//      AGV's drop (add_tray_to_packaging), runs the four stations' actions, completions and
+//      grants (PackagingAgent.py:91-153) and the order completions (FJSPSimulation.py:245-258);
+//   P  (wave 5) draws step k+1's actions and, on AM's post of step k, runs step k+1's pickup
+//      station (PickupStationAgent.py:146-248) — nothing after the AGV in step k changes what
+//      the pickup reads (SURVEY.md Appendix A agent order);
+//   E0, E1 (waves 2, 3) turn step k-1's snapshot into the outputs (as k_step_pipe's emit waves);
+//   PD (wave 4) pre-draws the next order tables (predraw_wave).
+// The order words are shared by AM (processed bits) and K (packaged / complete bits): both OR
+// atomically (order_or).  The tray-slot arena is shared without atomics: within a step every
+// slot is written by the one wave that owns the list it is joining.  A step the pickup ran on
+// P is exactly the reference's step; lanes that just reset (and the first step of a launch) run
+// the pickup on AM.  One workgroup barrier per step; intra-step hand-off: AM's post (release /
+// acquire flag) -> P, K.  Result words are 16 bits (result | action << 8) in the snapshot.
+// Wave w runs on SIMD w % 4: AM shares its SIMD with P (whose pickup overlaps AM's machines,
+// off the critical path), K has a SIMD of its own, PD shares one with E0.
+constexpr int AG_AM = 0, AG_E0 = 1, AG_K = 2, AG_E1 = 3, AG_P = 4, AG_PD = 5, AG_WAVES = 6;
+// packaging-owned state words (K): W1, W13..W16 (packaging run lists), W20..W29
+constexpr uint32_t K_WORDS = (1u << 1) | (0xFu << 13) | (0x3FFu << 20);
+// snapshot slot words (PipeSnap, 32 per lane): AM writes q[0..3], K q[4..7]
+enum : int { SA_W0 = 0, SA_ST, SA_W4, SA_W5, SA_W6, SA_L0, SA_M0 = SA_L0 + 6, SA_M1, SA_R01, SA_R23,
+             SK_W1 = 16, SK_P0, SK_N0 = SK_P0 + 4, SK_ST = SK_N0 + 4, SK_G, SK_R45, SK_R67 };
+static_assert(SA_R23 < 16 && SK_R67 < 32, "snapshot slot");
+
+__device__ __forceinline__ void snap_put4(PipeSnap& sp, int q0, int lane, const uint32_t* v) {
+#pragma unroll
+    for (int g = 0; g < 4; g++) sp.q[q0 + g][lane] = make_uint4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+}
+
+__global__ void __launch_bounds__(AG_WAVES * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2)))
+k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0, int autoreset, fjsp_out out) {
+    constexpr int CR = FJSP_PG_CR, PB = FJSP_PG_PB;
+    __shared__ uint32_t s_orders[MAX_ORDERS * BLOCK];
+    __shared__ uint32_t s_nxt[MAX_ORDERS * BLOCK];
+    __shared__ uint32_t s_mb[4][2][BLOCK];   // AM <-> PD mailboxes (predraw_wave)
+    __shared__ uint4 s_cp[CR][3][BLOCK];
+    __shared__ uint16_t s_code[MAX_SLOTS * BLOCK];
+    __shared__ uint8_t s_next[MAX_SLOTS * BLOCK];
+    __shared__ uint16_t s_cstep[MAX_SLOTS * BLOCK];
+    __shared__ PipeSnap snap[2];
+    __shared__ uint32_t s_act[2][2][BLOCK];
+    __shared__ uint32_t s_apost[5][BLOCK];   // AM after the AGV of step k: W0, W4, W5, W7, pending packaging drop
+    __shared__ uint32_t s_pick[6][BLOCK];    // P, step k+1's pickup: next_order, W4, W5, W7, result, flags
+    __shared__ uint32_t s_kpost[2][BLOCK];   // K after step k: W1 (completed orders), final status
+    __shared__ uint32_t s_aflag;
+    __shared__ double s_lut[RLUT_SIZE];
+    for (int i = threadIdx.x; i < RLUT_SIZE; i += AG_WAVES * BLOCK) s_lut[i] = C.lut[i];
+    C.lut = s_lut;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / BLOCK);
+    const int lane = threadIdx.x % BLOCK;
+    const int e = blockIdx.x * BLOCK + lane;
+    const bool valid = e < S.n;
+    const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
+    const Tables TL{s_orders + lane, s_code + lane, s_next + lane, s_cstep + lane, BLOCK};
+#ifdef FJSP_STAMPS
+    uint64_t ag_busy = 0, ag_wait = 0;   // per epoch: busy until the barrier; AM: until its post, K / P: spinning
+#define AG_SPIN_T0() const uint64_t _ag_w0 = __builtin_amdgcn_s_memtime()
+#define AG_SPIN_ACC() (ag_wait += __builtin_amdgcn_s_memtime() - _ag_w0)
+#else
+#define AG_SPIN_T0() ((void)0)
+#define AG_SPIN_ACC() ((void)0)
+#endif
+    if (wave == AG_P && K > 0) {
+        int act[NA];
+        synth_uniform(seed, gid0 + (uint32_t)e, step0, act);
+        s_act[0][0][lane] = pack_actions(act, 0);
+        s_act[0][1][lane] = pack_actions(act, 4);
+    }
+    if (threadIdx.x == 0) s_aflag = 0;
+    if (wave == AG_AM && valid) {
+        // the env's order table and used slot prefix live in LDS for the launch (copied in before
+        // the first barrier: K's first completions read them before AM's first post)
+        const uint32_t w0 = S.words[e], nslots = S.words[5 * n + e] >> 24;
+        for (uint32_t o = 0; o < ((w0 >> 16) & 0xFFu); o++) TL.orders[o * BLOCK] = S.orders[(size_t)o * S.n + e];
+        for (uint32_t q = 0; q < nslots; q++) {
+            TL.scode[q * BLOCK] = S.scode[(size_t)q * S.n + e];
+            TL.snext[q * BLOCK] = S.snext[(size_t)q * S.n + e];
+            TL.scstep[q * BLOCK] = S.scstep[(size_t)q * S.n + e];
+        }
+        s_mb[0][0][lane] = ((w0 >> 16) & 0xFFu) << 8;   // episode counter 0 | num_orders
+        s_mb[1][0][lane] = S.words[3 * n + e];
+    }
+    if (wave == AG_PD && valid) {
+        const uint32_t pg = S.words[(size_t)PGW * n + e];
+        uint32_t r = 0, c = 0;
+        if (pg & 1u) {   // a table finished in an earlier launch
+            const int no = (int)((pg >> 24) & 0x7Fu);
+            for (int o = 0; o < no; o++) s_nxt[o * BLOCK + lane] = S.nxt[(size_t)o * n + e];
+            r = 1u | ((uint32_t)no << 9);
+            c = ((pg >> 1) & 0x3FFu) | (((pg >> 11) & 0x3FFu) << 16) | (((pg >> 21) & 1u) << 31);
+        }
+        s_mb[2][0][lane] = r;
+        s_mb[3][0][lane] = c;
+    }
+    __syncthreads();
+    if (wave == AG_AM) {
+        __builtin_amdgcn_s_setprio(3);   // the AGV -> machines chain is the critical path
+        Env E;
+        if (valid) env_load(E, S.words, S.n, e);
+        int epi = 0;
+        bool fresh = true, trunc_prev = false;
+        for (int k = 0; k <= K; k++) {
+            AG_T0();
+            if (valid) {
+                if (k > 0) {   // end of step k - 1: auto-reset once K has counted the completions
+                    const int nord = E.norders();
+                    const int all_done = (int)(s_kpost[0][lane] & 0xFFu) == nord && nord > 0 && E.next_order() == nord;
+                    if (autoreset && (all_done || trunc_prev)) {
+                        fresh = true;
+                        const uint32_t pr = s_mb[2][k & 1][lane];
+                        if ((pr & 1u) && ((pr >> 1) & 0xFFu) == (uint32_t)epi && (int)((pr >> 9) & 0x7Fu) == nord)
+                            env_reset_predrawn(E, TL, C, nord, s_mb[3][k & 1][lane], s_nxt + lane);
+                        else
+                            E = env_reset_cold(E, TL, C, S, e, nord, false);
+                        epi = (epi + 1) & 0xFF;
+                    }
+                }
+                s_mb[0][(k + 1) & 1][lane] = (uint32_t)epi | ((uint32_t)E.norders() << 8);
+                s_mb[1][(k + 1) & 1][lane] = E.w[3];
+            }
+            if (k < K) {
+                int act[NA];
+                uint32_t r0 = 0, r1 = 0;
+                if (valid) {
+                    const uint32_t a0 = s_act[k & 1][0][lane], a1 = s_act[k & 1][1][lane];
+#pragma unroll
+                    for (int a = 0; a < 4; a++) { act[a] = (a0 >> (8 * a)) & 0xFF; act[4 + a] = (a1 >> (8 * a)) & 0xFF; }
+                    if (!fresh) {   // step k's pickup ran on P
+                        E.w[0] = (E.w[0] & 0x00FFFFFFu) | (s_pick[0][lane] << 24);
+                        E.w[4] = s_pick[1][lane];
+                        E.w[5] = s_pick[2][lane];
+                        E.w[7 + L_PREADY] = s_pick[3][lane];
+                        r0 = s_pick[4][lane];
+                        E.w[2] |= s_pick[5][lane];
+                    } else {
+                        r0 = pickup_execute(E, TL, C, act[0]) | ((uint32_t)act[0] << 8);
+                    }
+#ifdef FJSP_STAMPS
+                    if (lane == 0) atomicAdd(&g_agstamps[14], (unsigned long long)(__builtin_amdgcn_s_memtime() - _ag_t0));
+#endif
+                    int mv = 0;
+                    uint32_t pend = 0;
+                    r1 = (agv_execute<true>(E, TL, C, act[1], &mv, &pend) & 0xFFu) | ((uint32_t)act[1] << 8);
+#ifdef FJSP_STAMPS
+                    if (lane == 0) atomicAdd(&g_agstamps[15], (unsigned long long)(__builtin_amdgcn_s_memtime() - _ag_t0));
+#endif
+                    if (mv) E.set_loc(mv);   // the move always lands inside the run
+                    s_apost[0][lane] = E.w[0];
+                    s_apost[1][lane] = E.w[4];
+                    s_apost[2][lane] = E.w[5];
+                    s_apost[3][lane] = E.w[7 + L_PREADY];
+                    s_apost[4][lane] = pend;
+                    if (k == 0) { FJSP_DBG(0, pend); FJSP_DBG(1, r1); FJSP_DBG(2, E.w[6]); }
+                    // stored by the lanes that posted, in the same instruction stream after their
+                    // post (a store by the other lanes could be scheduled before it); every
+                    // workgroup has at least one valid lane
+                    __hip_atomic_store(&s_aflag, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    AG_ACC(ag_wait);
+                }
+                if (valid) {
+                    int s0 = -1, s1 = -1;
+                    const uint32_t r2 = (machine_execute<0>(E, TL, act[2], &s0) & 0xFFu) | ((uint32_t)act[2] << 8);
+                    const uint32_t r3 = (machine_execute<1>(E, TL, act[3], &s1) & 0xFFu) | ((uint32_t)act[3] << 8);
+                    machines_run<true>(E, TL, C, s0, s1);
+                    if (E.ll(L_M0Q) > 127 || E.ll(L_M1Q) > 127) E.flag(ST_OBS_OVERFLOW | ST_DIVERGED);
+                    const uint32_t v[16] = {E.w[0], E.w[2], E.w[4], E.w[5], E.w[6], E.w[7], E.w[8], E.w[9], E.w[10],
+                                            E.w[11], E.w[12], E.w[17], E.w[18], r0 | (r1 << 16), r2 | (r3 << 16), 0u};
+                    snap_put4(snap[k & 1], 0, lane, v);
+                    trunc_prev = E.step() >= C.max_steps;
+                    E.set_step(E.step() + 1);
+                    fresh = false;
+                }
+            }
+            AG_ACC(ag_busy);
+            __syncthreads();
+        }
+        if (valid) {
+            for (int o = 0; o < E.norders(); o++) S.orders[(size_t)o * S.n + e] = TL.orders[o * BLOCK];
+            for (int q = 0; q < E.slot_next(); q++) {
+                S.scode[(size_t)q * S.n + e] = TL.scode[q * BLOCK];
+                S.snext[(size_t)q * S.n + e] = TL.snext[q * BLOCK];
+                S.scstep[(size_t)q * S.n + e] = TL.scstep[q * BLOCK];
+            }
+            E.w[2] |= s_kpost[1][lane];
+#pragma unroll
+            for (int i = 0; i < NSTATE; i++)
+                if (!((K_WORDS >> i) & 1u)) S.words[i * n + e] = E.w[i];
+        }
+    } else if (wave == AG_K) {
+        __builtin_amdgcn_s_setprio(2);
+        Env E;
+#pragma unroll
+        for (int i = 0; i < NSTATE; i++) E.w[i] = 0u;
+        if (valid) {
+#pragma unroll
+            for (int i = 0; i < NSTATE; i++)
+                if ((K_WORDS >> i) & 1u) E.w[i] = S.words[i * n + e];
+            E.w[0] = S.words[e] & 0xFFFFu;   // the step counter (AM owns W0)
+        }
+        uint32_t w0a = 0;   // AM's W0 after the AGV of the previous step (next_order, num_orders)
+        bool trunc_prev = false;
+        for (int k = 0; k <= K; k++) {
+            AG_T0();
+            if (valid && k > 0) {
+                const int nord = (int)((w0a >> 16) & 0xFFu);
+                const int all_done = E.ncompleted() == nord && nord > 0 && (int)(w0a >> 24) == nord;
+                if (autoreset && (all_done || trunc_prev)) {   // env_clear of the packaging words
+                    E.w[0] = 0u; E.w[1] = 0u; E.w[2] = 0u;
+#pragma unroll
+                    for (int s = 0; s < 4; s++) {
+                        E.w[7 + L_PKG + s] = (uint32_t)NIL | ((uint32_t)NIL << 8);
+                        E.w[20 + s] = (uint32_t)NIL << 2;
+                        E.w[26 + s] = 0u;
+                    }
+                    E.w[24] = 0u; E.w[25] = 0u;
+                }
+            }
+            if (k < K) {
+                // completions due this step first (they do not depend on this step's AGV)
+                int done[4] = {0, 0, 0, 0}, orders_done = 0, tp0 = 0, step = 0;
+                if (valid) {
+                    step = E.step();
+                    tp0 = E.total_packaged();
+                    const bool due0 = pack_due<0>(E, TL, step), due1 = pack_due<1>(E, TL, step);
+                    const bool due2 = pack_due<2>(E, TL, step), due3 = pack_due<3>(E, TL, step);
+                    done[0] = pack_complete<0>(E, TL, due0, &orders_done);
+                    done[1] = pack_complete<1>(E, TL, due1, &orders_done);
+                    done[2] = pack_complete<2>(E, TL, due2, &orders_done);
+                    done[3] = pack_complete<3>(E, TL, due3, &orders_done);
+                }
+                AG_SPIN_T0();
+                while (__hip_atomic_load(&s_aflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (uint32_t)(k + 1))
+                    __builtin_amdgcn_s_sleep(1);
+                AG_SPIN_ACC();
+                if (valid) {
+                    w0a = s_apost[0][lane];
+                    const uint32_t pend = s_apost[4][lane];
+                    const uint32_t a1 = s_act[k & 1][1][lane];
+                    if (pend) agv_pack_drop(E, TL, C, pend);   // routing reads the in-flight counts before the run
+                    int st[4] = {0, 0, 0, 0};
+                    uint32_t r[4];
+                    r[0] = pack_execute<0>(E, (int)(a1 & 0xFFu), &st[0]);
+                    r[1] = pack_execute<1>(E, (int)((a1 >> 8) & 0xFFu), &st[1]);
+                    r[2] = pack_execute<2>(E, (int)((a1 >> 16) & 0xFFu), &st[2]);
+                    r[3] = pack_execute<3>(E, (int)(a1 >> 24), &st[3]);
+                    pack_finish<0>(E, TL, C, st[0], done[0]);
+                    pack_finish<1>(E, TL, C, st[1], done[1]);
+                    pack_finish<2>(E, TL, C, st[2], done[2]);
+                    pack_finish<3>(E, TL, C, st[3], done[3]);
+                    E.set_ncompleted(E.ncompleted() + orders_done);
+                    if (E.p_queued(0) > 127 || E.p_queued(1) > 127 || E.p_queued(2) > 127 || E.p_queued(3) > 127)
+                        E.flag(ST_OBS_OVERFLOW | ST_DIVERGED);
+                    s_kpost[0][lane] = E.w[1];
+#pragma unroll
+                    for (int s = 0; s < 4; s++) r[s] = (r[s] & 0xFFu) | (((a1 >> (8 * s)) & 0xFFu) << 8);
+                    const uint32_t v[16] = {E.w[1], E.w[20], E.w[21], E.w[22], E.w[23], E.w[26], E.w[27], E.w[28],
+                                            E.w[29], E.w[2],
+                                            (uint32_t)orders_done | ((uint32_t)(E.total_packaged() - tp0) << 16),
+                                            r[0] | (r[1] << 16), r[2] | (r[3] << 16), 0u, 0u, 0u};
+                    snap_put4(snap[k & 1], 4, lane, v);
+                    trunc_prev = step >= C.max_steps;
+                    E.set_step(step + 1);
+                }
+            } else if (valid) {
+                s_kpost[1][lane] = E.w[2];   // status bits for AM's final store of W2
+            }
+            AG_ACC(ag_busy);
+            __syncthreads();
+        }
+        if (valid) {
+#pragma unroll
+            for (int i = 0; i < NSTATE; i++)
+                if ((K_WORDS >> i) & 1u) S.words[i * n + e] = E.w[i];
+        }
+    } else if (wave == AG_P) {
+        __builtin_amdgcn_s_setprio(2);
+        for (int k = 0; k <= K; k++) {
+            AG_T0();
+            if (k + 1 < K) {   // step k + 1: actions, then the pickup station on AM's post of step k
+                int act[NA];
+                synth_uniform(seed, gid0 + (uint32_t)e, step0 + (uint32_t)(k + 1), act);
+                s_act[(k + 1) & 1][0][lane] = pack_actions(act, 0);
+                s_act[(k + 1) & 1][1][lane] = pack_actions(act, 4);
+                AG_SPIN_T0();
+                while (__hip_atomic_load(&s_aflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (uint32_t)(k + 1))
+                    __builtin_amdgcn_s_sleep(1);
+                AG_SPIN_ACC();
+                if (valid) {
+                    Env Ep;
+#pragma unroll
+                    for (int i = 0; i < NSTATE; i++) Ep.w[i] = 0u;
+                    Ep.w[0] = s_apost[0][lane];
+                    Ep.w[4] = s_apost[1][lane];
+                    Ep.w[5] = s_apost[2][lane];
+                    Ep.w[7 + L_PREADY] = s_apost[3][lane];
+                    const uint32_t r = pickup_execute(Ep, TL, C, act[0]);
+                    s_pick[0][lane] = Ep.w[0] >> 24;
+                    s_pick[1][lane] = Ep.w[4];
+                    s_pick[2][lane] = Ep.w[5];
+                    s_pick[3][lane] = Ep.w[7 + L_PREADY];
+                    s_pick[4][lane] = (r & 0xFFu) | ((uint32_t)act[0] << 8);
+                    s_pick[5][lane] = Ep.w[2];
+                }
+            }
+            AG_ACC(ag_busy);
+            __syncthreads();
+        }
+    } else if (wave == AG_PD) {
+        predraw_wave<CR, PB, true>(S, K, lane, e, valid, s_mb, s_cp, s_nxt);
+    } else {
+        // E0: rewards + int32 / float32 observation fields; E1: int8 fields, masks, term, trunc, status
+        const int part = wave == AG_E0 ? 0 : 1;
+        for (int k = 0; k <= K; k++) {
+            AG_T0();
+            if (k > 0 && valid) {
+                const uint32_t t = (uint32_t)(k - 1);
+                uint32_t v[SNAP_N];
+                snap_get(snap[(k - 1) & 1], lane, v);
+                Env E;
+#pragma unroll
+                for (int i = 0; i < NSTATE; i++) E.w[i] = 0u;
+                E.w[0] = v[SA_W0]; E.w[2] = v[SA_ST] | v[SK_ST]; E.w[4] = v[SA_W4]; E.w[5] = v[SA_W5];
+                E.w[6] = v[SA_W6];
+#pragma unroll
+                for (int l = 0; l < 6; l++) E.w[7 + l] = v[SA_L0 + l];
+                E.w[17] = v[SA_M0]; E.w[18] = v[SA_M1];
+                E.w[1] = v[SK_W1];
+#pragma unroll
+                for (int s = 0; s < 4; s++) { E.w[20 + s] = v[SK_P0 + s]; E.w[26 + s] = v[SK_N0 + s]; }
+                const StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, ue};
+                if (part == 0) {
+                    if (out.rewards) {
+                        const uint32_t gs = v[SK_G];
+                        const double g8 = global_reward8(C, (int)(gs & 0xFFFFu), (int)(gs >> 16));
+                        const uint32_t rw[4] = {v[SA_R01], v[SA_R23], v[SK_R45], v[SK_R67]};
+#pragma unroll
+                        for (int a = 0; a < NA; a++) {
+                            const uint32_t r = (rw[a >> 1] >> (16 * (a & 1))) & 0xFFFFu;
+                            st32(out.rewards, (t * NA + (uint32_t)a) * n + ue,
+                                 g8 + C.lut[reward_index(a, r & 0xFFu, (int)((r >> 8) & 0xFu))]);
+                        }
+                    }
+                    PartSink<0> ps{sink};
+                    observe(E, C, ps);
+                } else {
+                    PartSink<1> ps{sink};
+                    observe(E, C, ps);
+                    const int nord = E.norders();
+                    const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
+                    const int truncated = E.step() >= C.max_steps;
+                    if (out.term) st32(out.term, t * n + ue, (uint8_t)all_done);
+                    if (out.trunc) st32(out.trunc, t * n + ue, (uint8_t)truncated);
+                    if (out.status) st32(out.status, t * n + ue, E.status());
+                }
+            }
+            AG_ACC(ag_busy);
+            __syncthreads();
+        }
+    }
+#ifdef FJSP_STAMPS
+    if (lane == 0 && blockIdx.x == 0) {   // SIMD of each wave (HW_REG_HW_ID bits 5:4)
+        const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        atomicOr(&g_agstamps[13], (unsigned long long)((hw >> 4) & 3u) << (4 * wave));
+    }
+    if (lane == 0 && wave != AG_PD) {
+        atomicAdd(&g_agstamps[2 * wave], (unsigned long long)ag_busy);
+        atomicAdd(&g_agstamps[2 * wave + 1], (unsigned long long)ag_wait);
+        if (wave == AG_AM) atomicAdd(&g_agstamps[12], (unsigned long long)(K + 1));
+    }
+#endif
+}
+
 // transition_memory.py:83-105 over a [T][M] rollout buffer; column m = a*N + e
 template <class VT>
 __global__ void __launch_bounds__(256) k_gae(const double* __restrict__ r, const VT* __restrict__ v,
@@ -1108,6 +1517,7 @@ struct fjsp_handle {
     int timing;      // hipEvent bracketing of step launches (off while graph-capturing)
     int use_pipe;    // two-wave pipelined k_step_many for lean outputs (FJSP_PIPE / fjsp_set_option)
     int use_pg;      // pre-draw wave in the pipelined kernel (FJSP_PREDRAW / fjsp_set_option "predraw")
+    int use_ag;      // agent-group pipeline k_step_ag for uniform-random actions (FJSP_AGENTS / "agents")
     const char* last_kernel;   // name of the last step kernel launched (fjsp_last_kernel)
 };
 
@@ -1227,6 +1637,8 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
         h->use_pipe = pp ? atoi(pp) : 1;
         const char* pd = getenv("FJSP_PREDRAW");
         h->use_pg = pd ? atoi(pd) : 1;
+        const char* ag = getenv("FJSP_AGENTS");
+        h->use_ag = ag ? atoi(ag) : 1;
     }
     h->dcfg.step_size = c.step_size;
     h->dcfg.max_steps = c.max_episode_steps;
@@ -1297,6 +1709,7 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
     if (!strcmp(name, "staged_stores")) { h->use_staged = value != 0; return 0; }
     if (!strcmp(name, "pipeline")) { h->use_pipe = value != 0; return 0; }
     if (!strcmp(name, "predraw")) { h->use_pg = value != 0; return 0; }
+    if (!strcmp(name, "agents")) { h->use_ag = value != 0; return 0; }
     if (!strcmp(name, "timing")) { h->timing = value != 0; if (!h->timing) h->timed = 0; return 0; }
     return fail("unknown option");
 }
@@ -1388,14 +1801,20 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
     const bool two_emit = h->n <= 256 * BLOCK;
     // the pre-draw wave pays while the CUs have a free SIMD (and only with auto-reset)
     const bool pg = h->use_pg && lds && two_emit && autoreset;
-    h->last_kernel = (h->use_pipe && !full && !staged)
+    // the agent-group pipeline: state-independent (uniform-random) actions, LDS tables, pre-draw
+    const bool ag = h->use_ag && h->use_pipe && !full && !staged && pg && action_mode == FJSP_ACTIONS_UNMASKED;
+    h->last_kernel = ag ? "k_step_ag<lds,predraw>"
+                   : (h->use_pipe && !full && !staged)
                          ? (lds ? (two_emit ? (pg ? "k_step_pipe<lds,2emit,predraw>" : "k_step_pipe<lds,2emit>")
                                             : "k_step_pipe<lds,1emit>")
                                 : (two_emit ? "k_step_pipe<2emit>" : "k_step_pipe<1emit>"))
                    : full ? (lds ? "k_step_many<lds,full>" : "k_step_many<full>")
                    : staged ? (lds ? "k_step_many<lds,staged>" : "k_step_many<staged>")
                    : (lds ? "k_step_many<lds>" : "k_step_many");
-    if (h->use_pipe && !full && !staged) {
+    if (ag) {
+        hipLaunchKernelGGL(k_step_ag, grid, dim3(AG_WAVES * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0,
+                           step0, autoreset, o);
+    } else if (h->use_pipe && !full && !staged) {
         // a second emit wave pays while the CUs are not full (N <= 16384 at 64 envs per CU)
         const bool two = two_emit;
         auto launch_pipe = [&](auto kern, int waves) {
@@ -1451,6 +1870,20 @@ extern "C" int fjsp_debug_stamps(unsigned long long* out) {
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8));
     unsigned long long z[8] = {0};
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)));
+    return 0;
+}
+#ifdef FJSP_X_DEBUG
+extern "C" int fjsp_debug_dump(uint32_t* out) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(uint32_t) * 8 * 64));
+    return 0;
+}
+#endif
+extern "C" int fjsp_debug_agstamps(unsigned long long* out) {   // out[16]: k_step_ag per wave busy / wait, epochs
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_agstamps), sizeof(unsigned long long) * 16));
+    unsigned long long z[16] = {0};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_agstamps), z, sizeof(z)));
     return 0;
 }
 extern "C" int fjsp_debug_pgstamps(unsigned long long* out) {   // out[8]: pre-draw [4], emit [4]

@@ -1,0 +1,25 @@
+"""Per-wave cycles per epoch of k_step_ag (diagnostic build libfjsp_stamps.so)."""
+import ctypes, os, sys, json
+os.environ["FJSP_LIB"] = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                      "multi-agent-rl-for-fjsp_amd", sys.argv[1] if len(sys.argv) > 1 else "libfjsp_stamps.so")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from tests import gpu_util as G
+L = G.native.lib()
+L.fjsp_debug_agstamps.argtypes = [ctypes.c_void_p]
+L.fjsp_debug_pgstamps.argtypes = [ctypes.c_void_p]
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+env = G.make_env(N)
+env.reset(seeds=torch.arange(N))
+b = G.vec_env.Buffers(200, N, env.device, infos=False)
+env.rollout(200, buffers=b); torch.cuda.synchronize()
+ag = (ctypes.c_ulonglong * 16)(); pg = (ctypes.c_ulonglong * 8)()
+L.fjsp_debug_agstamps(ag); L.fjsp_debug_pgstamps(pg)
+env.rollout(200, step0=200, buffers=b); torch.cuda.synchronize()
+L.fjsp_debug_agstamps(ag); L.fjsp_debug_pgstamps(pg)
+ep = max(1, ag[12])
+names = ["AM", "E0", "K", "E1", "P", "PD"]
+print(json.dumps({"N": N, "kernel": env.last_kernel(), "per_epoch": {names[w]: {"busy": round(ag[2 * w] / ep), "wait_or_post": round(ag[2 * w + 1] / ep)} for w in range(6) if names[w] != "PD"},
+                  "AM_after_pickup": round(ag[14] / ep), "AM_after_agv": round(ag[15] / ep),
+                  "simd_of_wave": [(ag[13] >> (4 * w)) & 3 for w in range(6)],
+                  "predraw": {"busy_per_step": pg[0] / max(1, pg[3]), "active_frac": pg[1] / max(1, pg[3]), "busy_active": pg[2] / max(1, pg[1])}}))

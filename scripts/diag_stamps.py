@@ -13,7 +13,8 @@ names = ["synth_actions(+barrier)", "action_phase", "run_phase", "rewards|snapsh
 if "fine" in (sys.argv[1] if len(sys.argv) > 1 else ""):
     names = ["synth_actions(+barrier)", "pickup", "agv", "machines", "packaging", "run_phase", "rewards+observe+stores|snapshot", "autoreset"]
 for N in (4096,):
-    for pipe, lds, pg in ((1, 1, 1), (1, 1, 0), (1, 0, 0), (0, 0, 0)):   # pipelined: the sim wave's phases
+    cfgs = ((1, 1, 1), (1, 1, 0), (1, 0, 0), (0, 0, 0))
+    for pipe, lds, pg in cfgs[:int(os.environ.get("STAMP_CFGS", "4"))]:   # pipelined: the sim wave's phases
         env = ve.FJSPVecEnv(N)
         nat.check(L.fjsp_set_option(env.handle, b"pipeline", pipe))
         nat.check(L.fjsp_set_option(env.handle, b"fused_lds", lds))

@@ -143,6 +143,7 @@ def test_pickup_ahead_desynchronised_episodes(G):
     for pipe, predraw in ((1, 1), (0, 0)):
         env = _env(G, n, predraw, **cfg)
         G.native.check(G.native.lib().fjsp_set_option(env.handle, b"pipeline", pipe))
+        G.native.check(G.native.lib().fjsp_set_option(env.handle, b"agents", 0))   # k_step_ag: test_gpu_agents.py
         env.reset(seeds=torch.arange(n) + 11, num_orders=3)
         seq = []
         for i, k in enumerate((13, 29, 8, 50)):
