@@ -631,11 +631,16 @@ __device__ __forceinline__ uint32_t pack_actions(const int* act, int lo) {
 #ifndef FJSP_PG_PB
 #define FJSP_PG_PB 8   // ... and words drawn per env
 #endif
+#ifndef FJSP_AG_PB
+#define FJSP_AG_PB 4   // words drawn per env per step in k_step_ag
+#endif
 // The pre-draw wave (k_step_pipe<..., PG>, k_step_ag): see the comment above k_step_pipe.
 // s_mb / s_cp / s_nxt are the kernel's LDS mailboxes, row-copy staging and next tables.
 // FINAL_MB: the sim side also posts in the final epoch K (k_step_ag resets at the top of an
 // epoch), so a table it consumed or abandoned there must not be stored as ready.
-template <int CR, int PB, bool FINAL_MB = false>
+// ASYNC: a row DMA issued in step k is waited for and stored in step k + 1 (its latency hides
+// behind the barrier instead of the step); s_cp holds two sets of CR rows.
+template <int CR, int PB, bool FINAL_MB = false, bool ASYNC = false>
 __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane, int e, bool valid,
                                              uint32_t (*s_mb)[2][BLOCK], uint4 (*s_cp)[3][BLOCK], uint32_t* s_nxt) {
     const uint32_t n = (uint32_t)S.n;
@@ -643,6 +648,9 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
     int ph = 0, nord = 0, pos = 0, g = 0;
     uint32_t src = 0, my = 0x100u;   // live row at the start of the pre-draw; episode it is for
     OrderDraw d{0, 0, 0, 0, 0u};
+    int ls_prev[CR];       // ASYNC: lanes whose row DMA is in flight (ph == 4) and their source rows
+    uint32_t sl_prev[CR];
+    bool inflight = false;
     if (valid) {
         const uint32_t pg = S.words[(size_t)PGW * n + e];
         if (pg & 1u) {
@@ -693,11 +701,49 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
                 if (d.o >= nord) ph = 3;
             }
         };
+        if (ASYNC && inflight) {   // last step's row DMAs: store them, the lanes draw from the next step on
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+            const int pb = (k - 1) & 1;
+#pragma unroll
+            for (int r = 0; r < CR; r++) {
+                const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls_prev[r];
+                uint4* rd = reinterpret_cast<uint4*>(S.mt + ((size_t)(sl_prev[r] ^ 1u) * n + el) * MT_N);
+                rd[lane] = s_cp[pb * CR + r][0][lane];
+                rd[lane + 64] = s_cp[pb * CR + r][1][lane];
+                if (lane + 128 < MT_N / 4) rd[lane + 128] = s_cp[pb * CR + r][2][lane];
+            }
+            inflight = false;
+        }
+        const int promote = ph;   // ASYNC: ph == 4 lanes become drawable after this step's draw
         uint64_t need = __ballot(valid && ph == 1);
 #ifdef FJSP_STAMPS
         pg_active = need != 0 || __ballot(valid && ph == 2) != 0;
 #endif
-        if (need) {
+        if (ASYNC) {
+            draw_step();
+#pragma unroll
+            for (int r = 0; r < CR; r++)
+                if (promote == 4 && ph == 4 && lane == ls_prev[r]) ph = 2;
+            if (need) {
+                const int first = __builtin_ctzll(need);
+                const int cb = k & 1;
+#pragma unroll
+                for (int r = 0; r < CR; r++) {
+                    ls_prev[r] = need ? __builtin_ctzll(need) : first;
+                    need &= need - 1;
+                    sl_prev[r] = (uint32_t)__builtin_amdgcn_readlane((int)src, ls_prev[r]);
+                    const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls_prev[r];
+                    const uint4* rs = reinterpret_cast<const uint4*>(S.mt + ((size_t)sl_prev[r] * n + el) * MT_N);
+#pragma unroll
+                    for (int i = 0; i < 3; i++)
+                        __builtin_amdgcn_global_load_lds(
+                            (__attribute__((address_space(1))) void*)(rs + min(lane + 64 * i, MT_N / 4 - 1)),
+                            (__attribute__((address_space(3))) void*)&s_cp[cb * CR + r][i][0], 16, 0, 0);
+                    if (lane == ls_prev[r] && ph == 1) ph = 4;
+                }
+                inflight = true;
+            }
+        } else if (need) {
             // rows go through LDS by DMA (global_load_lds: no VGPRs held across the draw);
             // slots beyond the envs waiting re-copy the first env's row (identical stores)
             const int first = __builtin_ctzll(need);
@@ -744,6 +790,7 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
 #endif
         __syncthreads();
     }
+    if (ASYNC) __builtin_amdgcn_s_waitcnt(0x0F70);   // no LDS DMA outlives the workgroup
 #ifdef FJSP_STAMPS
     if (lane == 0) {
         atomicAdd(&g_pgstamps[0], (unsigned long long)pg_busy);
@@ -1125,11 +1172,13 @@ __device__ __forceinline__ void snap_put4(PipeSnap& sp, int q0, int lane, const 
 
 __global__ void __launch_bounds__(AG_WAVES * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2)))
 k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0, int autoreset, fjsp_out out) {
-    constexpr int CR = FJSP_PG_CR, PB = FJSP_PG_PB;
+    // pre-draw work per step: the draw costs more than its loads' latency here (PD shares its
+    // SIMD with E0), so four words per step (~33 steps for 30 orders) beat eight (measured)
+    constexpr int CR = FJSP_PG_CR, PB = FJSP_AG_PB;
     __shared__ uint32_t s_orders[MAX_ORDERS * BLOCK];
     __shared__ uint32_t s_nxt[MAX_ORDERS * BLOCK];
     __shared__ uint32_t s_mb[4][2][BLOCK];   // AM <-> PD mailboxes (predraw_wave)
-    __shared__ uint4 s_cp[CR][3][BLOCK];
+    __shared__ uint4 s_cp[2 * CR][3][BLOCK];   // two steps of row DMAs in flight (predraw_wave<ASYNC>)
     __shared__ uint16_t s_code[MAX_SLOTS * BLOCK];
     __shared__ uint8_t s_next[MAX_SLOTS * BLOCK];
     __shared__ uint16_t s_cstep[MAX_SLOTS * BLOCK];
@@ -1312,27 +1361,14 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 }
             }
             if (k < K) {
-                // completions due this step first (they do not depend on this step's AGV)
+                // Completions due this step first (they do not depend on this step's AGV), then the
+                // stations' actions, grants and the snapshot assuming the AGV drops nothing at
+                // packaging; lanes whose AGV did (rare) redo the actions after routing the drop from
+                // the saved words (the only table write of the first pass, a START's scstep of the
+                // queue front, is rewritten with the same value or superseded).
                 int done[4] = {0, 0, 0, 0}, orders_done = 0, tp0 = 0, step = 0;
-                if (valid) {
-                    step = E.step();
-                    tp0 = E.total_packaged();
-                    const bool due0 = pack_due<0>(E, TL, step), due1 = pack_due<1>(E, TL, step);
-                    const bool due2 = pack_due<2>(E, TL, step), due3 = pack_due<3>(E, TL, step);
-                    done[0] = pack_complete<0>(E, TL, due0, &orders_done);
-                    done[1] = pack_complete<1>(E, TL, due1, &orders_done);
-                    done[2] = pack_complete<2>(E, TL, due2, &orders_done);
-                    done[3] = pack_complete<3>(E, TL, due3, &orders_done);
-                }
-                AG_SPIN_T0();
-                while (__hip_atomic_load(&s_aflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (uint32_t)(k + 1))
-                    __builtin_amdgcn_s_sleep(1);
-                AG_SPIN_ACC();
-                if (valid) {
-                    w0a = s_apost[0][lane];
-                    const uint32_t pend = s_apost[4][lane];
-                    const uint32_t a1 = s_act[k & 1][1][lane];
-                    if (pend) agv_pack_drop(E, TL, C, pend);   // routing reads the in-flight counts before the run
+                uint32_t a1 = 0, sv[12];
+                auto act_and_grant = [&]() {
                     int st[4] = {0, 0, 0, 0};
                     uint32_t r[4];
                     r[0] = pack_execute<0>(E, (int)(a1 & 0xFFu), &st[0]);
@@ -1348,12 +1384,47 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                         E.flag(ST_OBS_OVERFLOW | ST_DIVERGED);
                     s_kpost[0][lane] = E.w[1];
 #pragma unroll
-                    for (int s = 0; s < 4; s++) r[s] = (r[s] & 0xFFu) | (((a1 >> (8 * s)) & 0xFFu) << 8);
+                    for (int q = 0; q < 4; q++) r[q] = (r[q] & 0xFFu) | (((a1 >> (8 * q)) & 0xFFu) << 8);
                     const uint32_t v[16] = {E.w[1], E.w[20], E.w[21], E.w[22], E.w[23], E.w[26], E.w[27], E.w[28],
                                             E.w[29], E.w[2],
                                             (uint32_t)orders_done | ((uint32_t)(E.total_packaged() - tp0) << 16),
                                             r[0] | (r[1] << 16), r[2] | (r[3] << 16), 0u, 0u, 0u};
                     snap_put4(snap[k & 1], 4, lane, v);
+                };
+                if (valid) {
+                    step = E.step();
+                    tp0 = E.total_packaged();
+                    const bool due0 = pack_due<0>(E, TL, step), due1 = pack_due<1>(E, TL, step);
+                    const bool due2 = pack_due<2>(E, TL, step), due3 = pack_due<3>(E, TL, step);
+                    done[0] = pack_complete<0>(E, TL, due0, &orders_done);
+                    done[1] = pack_complete<1>(E, TL, due1, &orders_done);
+                    done[2] = pack_complete<2>(E, TL, due2, &orders_done);
+                    done[3] = pack_complete<3>(E, TL, due3, &orders_done);
+                    sv[0] = E.w[1]; sv[1] = E.w[2];
+#pragma unroll
+                    for (int i = 0; i < 10; i++) sv[2 + i] = E.w[20 + i];
+                    a1 = s_act[k & 1][1][lane];
+                    act_and_grant();
+                }
+                AG_SPIN_T0();
+                while (__hip_atomic_load(&s_aflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (uint32_t)(k + 1))
+                    __builtin_amdgcn_s_sleep(1);
+                AG_SPIN_ACC();
+                uint32_t pend = 0;
+                if (valid) {
+                    w0a = s_apost[0][lane];
+                    pend = s_apost[4][lane];
+                }
+                if (__ballot(pend != 0)) {
+                    if (pend) {   // routing reads the in-flight counts before the run
+                        E.w[1] = sv[0]; E.w[2] = sv[1];
+#pragma unroll
+                        for (int i = 0; i < 10; i++) E.w[20 + i] = sv[2 + i];
+                        agv_pack_drop(E, TL, C, pend);
+                        act_and_grant();
+                    }
+                }
+                if (valid) {
                     trunc_prev = step >= C.max_steps;
                     E.set_step(step + 1);
                 }
@@ -1402,7 +1473,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             __syncthreads();
         }
     } else if (wave == AG_PD) {
-        predraw_wave<CR, PB, true>(S, K, lane, e, valid, s_mb, s_cp, s_nxt);
+        predraw_wave<CR, PB, true, true>(S, K, lane, e, valid, s_mb, s_cp, s_nxt);
     } else {
         // E0: rewards + int32 / float32 observation fields; E1: int8 fields, masks, term, trunc, status
         const int part = wave == AG_E0 ? 0 : 1;
