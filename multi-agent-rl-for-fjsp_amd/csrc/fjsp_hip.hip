@@ -34,7 +34,7 @@ constexpr int MT_N = 624;
 __device__ unsigned long long g_stamps[8];
 __device__ unsigned long long g_pgstamps[4];   // pre-draw wave: busy cycles, active steps, busy in active steps, steps
 __device__ unsigned long long g_emitstamps[4];   // emit waves 1, 2: busy cycles, steps
-__device__ unsigned long long g_agstamps[16];   // k_step_ag: per wave [busy, wait] cycles, epochs
+__device__ unsigned long long g_agstamps[40];   // k_step_ag (scripts/diag_ag_stamps.py)   // k_step_ag: per wave [busy, wait] cycles, epochs
 #define AG_T0() const uint64_t _ag_t0 = __builtin_amdgcn_s_memtime()
 #define AG_ACC(v) ((v) += __builtin_amdgcn_s_memtime() - _ag_t0)
 #else
@@ -582,6 +582,17 @@ struct PartSink {
     __device__ __forceinline__ void f32(int f, float v) { if (PART <= 0) s.f32(f, v); }
     __device__ __forceinline__ void i8(int f, int v) { if (PART != 0) s.i8(f, v); }
     __device__ __forceinline__ void mask(int f, int v) { if (PART != 0) s.mask(f, v); }
+};
+
+// Output sink of one of k_step_ag's four emit waves: only the fields in the compile-time masks
+// are computed and stored (observe()'s other values are dead code).
+template <uint32_t I32M, uint32_t I8M, uint32_t F32M, uint32_t MKM>
+struct FieldSink {
+    StoreSink s;
+    __device__ __forceinline__ void i32(int f, int v) { if ((I32M >> f) & 1u) s.i32(f, v); }
+    __device__ __forceinline__ void f32(int f, float v) { if ((F32M >> f) & 1u) s.f32(f, v); }
+    __device__ __forceinline__ void i8(int f, int v) { if ((I8M >> f) & 1u) s.i8(f, v); }
+    __device__ __forceinline__ void mask(int f, int v) { if ((MKM >> f) & 1u) s.mask(f, v); }
 };
 
 // State words the observation / masks / term / trunc / status read (observe, compute_masks):
@@ -1134,40 +1145,66 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
 
 // ---------------------------------------------------------------- agent-group pipeline
 // k_step_ag: K fused steps (uniform-random actions, LDS tables, auto-reset with pre-drawn
-// tables), the env's agents split over the wavefronts of its 64-env workgroup so that per step
-// only the AGV -> machines chain is sequential:
-//   AM (wave 0) owns every state word but the packaging ones: it applies the pickup result
-//      P computed during the previous step, runs the AGV (a drop at packaging is deferred,
-//      agv_execute<true>), posts the words P and K need, then runs the machines' actions and
-//      their run phase (MachineAgent.py:99-169), and resets the env (FJSPSimulation.reset,
-//      seed=None) at the top of the next step once K has counted the step's completions;
-//   K  (wave 1) owns the packaging words (W1, W13-16, W20-29): after AM's post it routes the
-//      AGV's drop (add_tray_to_packaging), runs the four stations' actions, completions and
-//      grants (PackagingAgent.py:91-153) and the order completions (FJSPSimulation.py:245-258);
-//   P  (wave 5) draws step k+1's actions and, on AM's post of step k, runs step k+1's pickup
-//      station (PickupStationAgent.py:146-248) — nothing after the AGV in step k changes what
-//      the pickup reads (SURVEY.md Appendix A agent order);
-//   E0, E1 (waves 2, 3) turn step k-1's snapshot into the outputs (as k_step_pipe's emit waves);
-//   PD (wave 4) pre-draws the next order tables (predraw_wave).
+// tables), the env's agents split over the wavefronts of its 64-env workgroup.  Per step k the
+// only sequential chain left is  machines' actions (k) -> AGV (k+1) -> machines' actions (k+1):
+//   AM owns every state word but the packaging ones.  At the top of step k it applies the
+//      pickup and AGV results P computed during step k-1 (on a lane that just reset, and on the
+//      first step of a launch, it runs those two agents itself), posts the pickup/AGV words
+//      (post 1), runs the machines' actions (MachineAgent.py:99-139), posts the machine lists
+//      (post 2), then the machines' run phase (:151-169) and its half of the step snapshot.  At
+//      the top of the next step it auto-resets the env (FJSPSimulation.reset(seed=None)) once K
+//      has counted the step's order completions.
+//   P  draws step k+1's actions, runs step k+1's pickup station (PickupStationAgent.py:146-248)
+//      on post 1 and step k+1's AGV (AGVAgent.py:180-368, a drop at packaging deferred) on post
+//      2: in the reference's agent order the pickup and the AGV read nothing that the packaging
+//      agents or the run phase of step k change.
+//   K  owns the packaging words (W1, W13-16, W20-29): at the top of step k the completions due
+//      (PackagingAgent.py:143-147, older events than the step's actions), the AGV's drop
+//      routed (FJSPSimulation.add_tray_to_packaging, with the in-flight counts before the run),
+//      the stations' actions and grants (:91-141) and the order completions
+//      (FJSPSimulation.py:245-258) — it needs only P's AGV result of the previous step.
+//   E0, E1 turn step k-1's snapshot into the outputs (as k_step_pipe's emit waves);
+//   PD pre-draws the next order tables (predraw_wave).
 // The order words are shared by AM (processed bits) and K (packaged / complete bits): both OR
-// atomically (order_or).  The tray-slot arena is shared without atomics: within a step every
-// slot is written by the one wave that owns the list it is joining.  A step the pickup ran on
-// P is exactly the reference's step; lanes that just reset (and the first step of a launch) run
-// the pickup on AM.  One workgroup barrier per step; intra-step hand-off: AM's post (release /
-// acquire flag) -> P, K.  Result words are 16 bits (result | action << 8) in the snapshot.
-// Wave w runs on SIMD w % 4: AM shares its SIMD with P (whose pickup overlaps AM's machines,
-// off the critical path), K has a SIMD of its own, PD shares one with E0.
-constexpr int AG_AM = 0, AG_E0 = 1, AG_K = 2, AG_E1 = 3, AG_P = 4, AG_PD = 5, AG_WAVES = 6;
+// atomically (order_or); P reads the static fields and the bits of the tray its AGV picks up,
+// which nothing else changes then.  The tray-slot arena needs no atomics: within a step every
+// slot is written by the one wave that owns the list it joins.  Hand-offs inside a step: AM's
+// posts (release / acquire flags) -> P; everything else crosses the one barrier per step.
+// Result words are 16 bits (result | action << 8).
+// Waves w and w + 4 share a SIMD (two waves per SIMD issue VALU at twice one wave's rate): K
+// shares AM's (both busy early in the step; AM has the higher priority), P (the critical path
+// after AM's post, higher priority) shares the lightest emit wave's, PD and E3 pair up.
+constexpr int AG_AM = 0, AG_P = 1, AG_E1 = 2, AG_E2 = 3, AG_K = 4, AG_E0 = 5, AG_PD = 6, AG_E3 = 7, AG_WAVES = 8;
 // packaging-owned state words (K): W1, W13..W16 (packaging run lists), W20..W29
 constexpr uint32_t K_WORDS = (1u << 1) | (0xFu << 13) | (0x3FFu << 20);
 // snapshot slot words (PipeSnap, 32 per lane): AM writes q[0..3], K q[4..7]
 enum : int { SA_W0 = 0, SA_ST, SA_W4, SA_W5, SA_W6, SA_L0, SA_M0 = SA_L0 + 6, SA_M1, SA_R01, SA_R23,
              SK_W1 = 16, SK_P0, SK_N0 = SK_P0 + 4, SK_ST = SK_N0 + 4, SK_G, SK_R45, SK_R67 };
 static_assert(SA_R23 < 16 && SK_R67 < 32, "snapshot slot");
+// P's results for a step (s_res): next_order, W4, W5..W12, pickup result, AGV result, status, drop
+enum : int { RS_NO = 0, RS_W4, RS_W5, RS_R0 = RS_W5 + 8, RS_R1, RS_ST, RS_PEND = 15, RS_N };
+static_assert(RS_N <= 16, "s_res slot");
+// AM's post 1 (s_p1): W0, W4, W5, W6, W7, W8 after the step's pickup and AGV, the AGV's drop
+enum : int { P1_W0 = 0, P1_W4, P1_W5, P1_W6, P1_W7, P1_W8, P1_PEND, P1_N };
+__device__ __forceinline__ void q_get(const uint4* q, int ng, uint32_t* v) {   // ng groups, stride BLOCK
+#pragma unroll
+    for (int g = 0; g < ng; g++) {
+        const uint4 x = q[g * BLOCK];
+        v[4 * g] = x.x; v[4 * g + 1] = x.y; v[4 * g + 2] = x.z; v[4 * g + 3] = x.w;
+    }
+}
+__device__ __forceinline__ void q_put(uint4* q, int ng, const uint32_t* v) {
+#pragma unroll
+    for (int g = 0; g < ng; g++) q[g * BLOCK] = make_uint4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+}
 
 __device__ __forceinline__ void snap_put4(PipeSnap& sp, int q0, int lane, const uint32_t* v) {
 #pragma unroll
     for (int g = 0; g < 4; g++) sp.q[q0 + g][lane] = make_uint4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+}
+
+__device__ __forceinline__ void ag_spin(uint32_t* flag, uint32_t v) {
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
 }
 
 __global__ void __launch_bounds__(AG_WAVES * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2)))
@@ -1184,10 +1221,12 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     __shared__ uint16_t s_cstep[MAX_SLOTS * BLOCK];
     __shared__ PipeSnap snap[2];
     __shared__ uint32_t s_act[2][2][BLOCK];
-    __shared__ uint32_t s_apost[5][BLOCK];   // AM after the AGV of step k: W0, W4, W5, W7, pending packaging drop
-    __shared__ uint32_t s_pick[6][BLOCK];    // P, step k+1's pickup: next_order, W4, W5, W7, result, flags
-    __shared__ uint32_t s_kpost[2][BLOCK];   // K after step k: W1 (completed orders), final status
-    __shared__ uint32_t s_aflag;
+    // hand-off slots are lane-major uint4 groups (one 16-byte LDS access per 4 words)
+    __shared__ uint4 s_p1[2][2][BLOCK];   // AM post 1 (P1_*), by step parity
+    __shared__ uint4 s_p2[BLOCK];         // AM post 2: W9..W12 (machine lists) after the machines' actions
+    __shared__ uint4 s_res[2][4][BLOCK];  // P: step k+1's pickup + AGV results (RS_*), by step parity
+    __shared__ uint32_t s_kpost[2][BLOCK];      // K after step k: W1 (completed orders), final status
+    __shared__ uint32_t s_flag1;   // AM posted step k's pickup / AGV words and machine lists (k + 1)
     __shared__ double s_lut[RLUT_SIZE];
     for (int i = threadIdx.x; i < RLUT_SIZE; i += AG_WAVES * BLOCK) s_lut[i] = C.lut[i];
     C.lut = s_lut;
@@ -1198,12 +1237,23 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
     const Tables TL{s_orders + lane, s_code + lane, s_next + lane, s_cstep + lane, BLOCK};
 #ifdef FJSP_STAMPS
-    uint64_t ag_busy = 0, ag_wait = 0;   // per epoch: busy until the barrier; AM: until its post, K / P: spinning
+    uint64_t ag_busy = 0, ag_wait = 0;   // per step: busy until the barrier; AM: until post 1, K / P: spinning
+    uint64_t amt[6] = {0, 0, 0, 0, 0, 0};   // AM: cycles into the step at its phase marks
+    uint64_t ag_last = 0;                    // steps this wave arrived last at the barrier
+#define AG_BARRIER()                                                        \
+    do {                                                                    \
+        const uint64_t _b0 = __builtin_amdgcn_s_memtime();                 \
+        __syncthreads();                                                    \
+        ag_last += (__builtin_amdgcn_s_memtime() - _b0) < 200 ? 1 : 0;     \
+    } while (0)
 #define AG_SPIN_T0() const uint64_t _ag_w0 = __builtin_amdgcn_s_memtime()
 #define AG_SPIN_ACC() (ag_wait += __builtin_amdgcn_s_memtime() - _ag_w0)
+#define AG_MARK(i) (amt[i] += __builtin_amdgcn_s_memtime() - _ag_t0)
 #else
+#define AG_BARRIER() __syncthreads()
 #define AG_SPIN_T0() ((void)0)
 #define AG_SPIN_ACC() ((void)0)
+#define AG_MARK(i) ((void)0)
 #endif
     if (wave == AG_P && K > 0) {
         int act[NA];
@@ -1211,10 +1261,10 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         s_act[0][0][lane] = pack_actions(act, 0);
         s_act[0][1][lane] = pack_actions(act, 4);
     }
-    if (threadIdx.x == 0) s_aflag = 0;
+    if (threadIdx.x == 0) s_flag1 = 0;
     if (wave == AG_AM && valid) {
         // the env's order table and used slot prefix live in LDS for the launch (copied in before
-        // the first barrier: K's first completions read them before AM's first post)
+        // the first barrier: K's first completions read them)
         const uint32_t w0 = S.words[e], nslots = S.words[5 * n + e] >> 24;
         for (uint32_t o = 0; o < ((w0 >> 16) & 0xFFu); o++) TL.orders[o * BLOCK] = S.orders[(size_t)o * S.n + e];
         for (uint32_t q = 0; q < nslots; q++) {
@@ -1239,17 +1289,31 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     }
     __syncthreads();
     if (wave == AG_AM) {
-        __builtin_amdgcn_s_setprio(3);   // the AGV -> machines chain is the critical path
+        __builtin_amdgcn_s_setprio(3);   // the machines -> AGV chain is the critical path
         Env E;
         if (valid) env_load(E, S.words, S.n, e);
         int epi = 0;
         bool fresh = true, trunc_prev = false;
+#ifdef FJSP_STAMPS
+        const uint64_t loop_t0 = __builtin_amdgcn_s_memtime();
+#endif
         for (int k = 0; k <= K; k++) {
             AG_T0();
+            AG_MARK(0);
+            // this step's inputs, read together: K's completion count, the actions, P's results
+            uint32_t kc = 0, a0 = 0, a1 = 0, rs[16];
+            if (valid) {
+                kc = s_kpost[0][lane];
+                if (k < K) {
+                    a0 = s_act[k & 1][0][lane];
+                    a1 = s_act[k & 1][1][lane];
+                    q_get(&s_res[k & 1][0][lane], 4, rs);
+                }
+            }
             if (valid) {
                 if (k > 0) {   // end of step k - 1: auto-reset once K has counted the completions
                     const int nord = E.norders();
-                    const int all_done = (int)(s_kpost[0][lane] & 0xFFu) == nord && nord > 0 && E.next_order() == nord;
+                    const int all_done = (int)(kc & 0xFFu) == nord && nord > 0 && E.next_order() == nord;
                     if (autoreset && (all_done || trunc_prev)) {
                         fresh = true;
                         const uint32_t pr = s_mb[2][k & 1][lane];
@@ -1263,62 +1327,58 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 s_mb[0][(k + 1) & 1][lane] = (uint32_t)epi | ((uint32_t)E.norders() << 8);
                 s_mb[1][(k + 1) & 1][lane] = E.w[3];
             }
-            if (k < K) {
+            AG_MARK(1);
+            if (k < K && valid) {
                 int act[NA];
-                uint32_t r0 = 0, r1 = 0;
-                if (valid) {
-                    const uint32_t a0 = s_act[k & 1][0][lane], a1 = s_act[k & 1][1][lane];
 #pragma unroll
-                    for (int a = 0; a < 4; a++) { act[a] = (a0 >> (8 * a)) & 0xFF; act[4 + a] = (a1 >> (8 * a)) & 0xFF; }
-                    if (!fresh) {   // step k's pickup ran on P
-                        E.w[0] = (E.w[0] & 0x00FFFFFFu) | (s_pick[0][lane] << 24);
-                        E.w[4] = s_pick[1][lane];
-                        E.w[5] = s_pick[2][lane];
-                        E.w[7 + L_PREADY] = s_pick[3][lane];
-                        r0 = s_pick[4][lane];
-                        E.w[2] |= s_pick[5][lane];
-                    } else {
-                        r0 = pickup_execute(E, TL, C, act[0]) | ((uint32_t)act[0] << 8);
-                    }
-#ifdef FJSP_STAMPS
-                    if (lane == 0) atomicAdd(&g_agstamps[14], (unsigned long long)(__builtin_amdgcn_s_memtime() - _ag_t0));
-#endif
+                for (int a = 0; a < 4; a++) { act[a] = (a0 >> (8 * a)) & 0xFF; act[4 + a] = (a1 >> (8 * a)) & 0xFF; }
+                uint32_t r0, r1, pend = 0;
+                if (!fresh) {   // step k's pickup and AGV ran on P during step k - 1
+                    E.w[0] = (E.w[0] & 0x00FFFFFFu) | (rs[RS_NO] << 24);
+                    E.w[4] = rs[RS_W4];
+#pragma unroll
+                    for (int i = 0; i < 8; i++) E.w[5 + i] = rs[RS_W5 + i];
+                    r0 = rs[RS_R0];
+                    r1 = rs[RS_R1];
+                    E.w[2] |= rs[RS_ST];
+                } else {
+                    r0 = (pickup_execute(E, TL, C, act[0]) & 0xFFu) | ((uint32_t)act[0] << 8);
                     int mv = 0;
-                    uint32_t pend = 0;
                     r1 = (agv_execute<true>(E, TL, C, act[1], &mv, &pend) & 0xFFu) | ((uint32_t)act[1] << 8);
-#ifdef FJSP_STAMPS
-                    if (lane == 0) atomicAdd(&g_agstamps[15], (unsigned long long)(__builtin_amdgcn_s_memtime() - _ag_t0));
-#endif
                     if (mv) E.set_loc(mv);   // the move always lands inside the run
-                    s_apost[0][lane] = E.w[0];
-                    s_apost[1][lane] = E.w[4];
-                    s_apost[2][lane] = E.w[5];
-                    s_apost[3][lane] = E.w[7 + L_PREADY];
-                    s_apost[4][lane] = pend;
-                    if (k == 0) { FJSP_DBG(0, pend); FJSP_DBG(1, r1); FJSP_DBG(2, E.w[6]); }
-                    // stored by the lanes that posted, in the same instruction stream after their
-                    // post (a store by the other lanes could be scheduled before it); every
-                    // workgroup has at least one valid lane
-                    __hip_atomic_store(&s_aflag, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    AG_ACC(ag_wait);
                 }
-                if (valid) {
-                    int s0 = -1, s1 = -1;
-                    const uint32_t r2 = (machine_execute<0>(E, TL, act[2], &s0) & 0xFFu) | ((uint32_t)act[2] << 8);
-                    const uint32_t r3 = (machine_execute<1>(E, TL, act[3], &s1) & 0xFFu) | ((uint32_t)act[3] << 8);
-                    machines_run<true>(E, TL, C, s0, s1);
-                    if (E.ll(L_M0Q) > 127 || E.ll(L_M1Q) > 127) E.flag(ST_OBS_OVERFLOW | ST_DIVERGED);
-                    const uint32_t v[16] = {E.w[0], E.w[2], E.w[4], E.w[5], E.w[6], E.w[7], E.w[8], E.w[9], E.w[10],
-                                            E.w[11], E.w[12], E.w[17], E.w[18], r0 | (r1 << 16), r2 | (r3 << 16), 0u};
-                    snap_put4(snap[k & 1], 0, lane, v);
-                    trunc_prev = E.step() >= C.max_steps;
-                    E.set_step(E.step() + 1);
-                    fresh = false;
+                AG_MARK(2);
+                int s0 = -1, s1 = -1;
+                const uint32_t r2 = (machine_execute<0>(E, TL, act[2], &s0) & 0xFFu) | ((uint32_t)act[2] << 8);
+                const uint32_t r3 = (machine_execute<1>(E, TL, act[3], &s1) & 0xFFu) | ((uint32_t)act[3] << 8);
+                AG_MARK(3);
+                {   // the post: pickup / AGV words (P1_*), machine lists
+                    const uint32_t p1[8] = {E.w[0], E.w[4], E.w[5], E.w[6], E.w[7], E.w[8], pend, 0u};
+                    q_put(&s_p1[k & 1][0][lane], 2, p1);
+                    s_p2[lane] = make_uint4(E.w[9], E.w[10], E.w[11], E.w[12]);
                 }
+                // stored by the lanes that posted, after their post in the same instruction
+                // stream (a store by the other lanes could be scheduled first); every workgroup
+                // has a valid lane
+                __hip_atomic_store(&s_flag1, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                AG_ACC(ag_wait);
+                AG_MARK(4);
+                machines_run<true>(E, TL, C, s0, s1);
+                AG_MARK(5);
+                if (E.ll(L_M0Q) > 127 || E.ll(L_M1Q) > 127) E.flag(ST_OBS_OVERFLOW | ST_DIVERGED);
+                const uint32_t v[16] = {E.w[0], E.w[2], E.w[4], E.w[5], E.w[6], E.w[7], E.w[8], E.w[9], E.w[10],
+                                        E.w[11], E.w[12], E.w[17], E.w[18], r0 | (r1 << 16), r2 | (r3 << 16), 0u};
+                snap_put4(snap[k & 1], 0, lane, v);
+                trunc_prev = E.step() >= C.max_steps;
+                E.set_step(E.step() + 1);
+                fresh = false;
             }
             AG_ACC(ag_busy);
-            __syncthreads();
+            AG_BARRIER();
         }
+#ifdef FJSP_STAMPS
+        if (lane == 0) atomicAdd(&g_agstamps[24], (unsigned long long)(__builtin_amdgcn_s_memtime() - loop_t0));
+#endif
         if (valid) {
             for (int o = 0; o < E.norders(); o++) S.orders[(size_t)o * S.n + e] = TL.orders[o * BLOCK];
             for (int q = 0; q < E.slot_next(); q++) {
@@ -1342,14 +1402,16 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 if ((K_WORDS >> i) & 1u) E.w[i] = S.words[i * n + e];
             E.w[0] = S.words[e] & 0xFFFFu;   // the step counter (AM owns W0)
         }
-        uint32_t w0a = 0;   // AM's W0 after the AGV of the previous step (next_order, num_orders)
         bool trunc_prev = false;
         for (int k = 0; k <= K; k++) {
             AG_T0();
-            if (valid && k > 0) {
+            bool fresh = k == 0;
+            if (valid && k > 0) {   // the reset AM makes at the top of this step, on the packaging words
+                const uint32_t w0a = s_p1[(k - 1) & 1][0][lane].x;   // AM's W0 after step k-1's pickup (P1_W0)
                 const int nord = (int)((w0a >> 16) & 0xFFu);
                 const int all_done = E.ncompleted() == nord && nord > 0 && (int)(w0a >> 24) == nord;
                 if (autoreset && (all_done || trunc_prev)) {   // env_clear of the packaging words
+                    fresh = true;
                     E.w[0] = 0u; E.w[1] = 0u; E.w[2] = 0u;
 #pragma unroll
                     for (int s = 0; s < 4; s++) {
@@ -1361,14 +1423,29 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 }
             }
             if (k < K) {
-                // Completions due this step first (they do not depend on this step's AGV), then the
-                // stations' actions, grants and the snapshot assuming the AGV drops nothing at
-                // packaging; lanes whose AGV did (rare) redo the actions after routing the drop from
-                // the saved words (the only table write of the first pass, a START's scstep of the
-                // queue front, is rewritten with the same value or superseded).
-                int done[4] = {0, 0, 0, 0}, orders_done = 0, tp0 = 0, step = 0;
-                uint32_t a1 = 0, sv[12];
-                auto act_and_grant = [&]() {
+                // the AGV's drop of step k: P computed it during step k-1; a lane that just reset
+                // carries nothing; the first step of a launch runs its AGV on AM (post 1)
+                uint32_t pend = 0;
+                if (k == 0) {
+                    AG_SPIN_T0();
+                    ag_spin(&s_flag1, 1u);
+                    AG_SPIN_ACC();
+                    if (valid) pend = s_p1[0][1][lane].z;   // P1_PEND
+                } else if (valid && !fresh) {
+                    pend = s_res[k & 1][RS_PEND / 4][lane].w;   // RS_PEND = 15
+                }
+                if (valid) {
+                    const int step = E.step(), tp0 = E.total_packaged();
+                    const uint32_t a1 = s_act[k & 1][1][lane];
+                    // completions due this step (NORMAL events older than the step's actions)
+                    int done[4], orders_done = 0;
+                    const bool due0 = pack_due<0>(E, TL, step), due1 = pack_due<1>(E, TL, step);
+                    const bool due2 = pack_due<2>(E, TL, step), due3 = pack_due<3>(E, TL, step);
+                    done[0] = pack_complete<0>(E, TL, due0, &orders_done);
+                    done[1] = pack_complete<1>(E, TL, due1, &orders_done);
+                    done[2] = pack_complete<2>(E, TL, due2, &orders_done);
+                    done[3] = pack_complete<3>(E, TL, due3, &orders_done);
+                    if (pend) agv_pack_drop(E, TL, C, pend);   // routing reads the in-flight counts before the run
                     int st[4] = {0, 0, 0, 0};
                     uint32_t r[4];
                     r[0] = pack_execute<0>(E, (int)(a1 & 0xFFu), &st[0]);
@@ -1390,41 +1467,6 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                                             (uint32_t)orders_done | ((uint32_t)(E.total_packaged() - tp0) << 16),
                                             r[0] | (r[1] << 16), r[2] | (r[3] << 16), 0u, 0u, 0u};
                     snap_put4(snap[k & 1], 4, lane, v);
-                };
-                if (valid) {
-                    step = E.step();
-                    tp0 = E.total_packaged();
-                    const bool due0 = pack_due<0>(E, TL, step), due1 = pack_due<1>(E, TL, step);
-                    const bool due2 = pack_due<2>(E, TL, step), due3 = pack_due<3>(E, TL, step);
-                    done[0] = pack_complete<0>(E, TL, due0, &orders_done);
-                    done[1] = pack_complete<1>(E, TL, due1, &orders_done);
-                    done[2] = pack_complete<2>(E, TL, due2, &orders_done);
-                    done[3] = pack_complete<3>(E, TL, due3, &orders_done);
-                    sv[0] = E.w[1]; sv[1] = E.w[2];
-#pragma unroll
-                    for (int i = 0; i < 10; i++) sv[2 + i] = E.w[20 + i];
-                    a1 = s_act[k & 1][1][lane];
-                    act_and_grant();
-                }
-                AG_SPIN_T0();
-                while (__hip_atomic_load(&s_aflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (uint32_t)(k + 1))
-                    __builtin_amdgcn_s_sleep(1);
-                AG_SPIN_ACC();
-                uint32_t pend = 0;
-                if (valid) {
-                    w0a = s_apost[0][lane];
-                    pend = s_apost[4][lane];
-                }
-                if (__ballot(pend != 0)) {
-                    if (pend) {   // routing reads the in-flight counts before the run
-                        E.w[1] = sv[0]; E.w[2] = sv[1];
-#pragma unroll
-                        for (int i = 0; i < 10; i++) E.w[20 + i] = sv[2 + i];
-                        agv_pack_drop(E, TL, C, pend);
-                        act_and_grant();
-                    }
-                }
-                if (valid) {
                     trunc_prev = step >= C.max_steps;
                     E.set_step(step + 1);
                 }
@@ -1432,7 +1474,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 s_kpost[1][lane] = E.w[2];   // status bits for AM's final store of W2
             }
             AG_ACC(ag_busy);
-            __syncthreads();
+            AG_BARRIER();
         }
         if (valid) {
 #pragma unroll
@@ -1440,43 +1482,71 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 if ((K_WORDS >> i) & 1u) S.words[i * n + e] = E.w[i];
         }
     } else if (wave == AG_P) {
-        __builtin_amdgcn_s_setprio(2);
+        __builtin_amdgcn_s_setprio(3);
+        // W0, W4, W5, W6, W7, W8 after this wave's last AGV: the next pickup's inputs unless AM
+        // reset the env (or the launch starts), when they come from AM's post of this step
+        uint32_t sw[6] = {0u, 0u, 0u, 0u, 0u, 0u};
         for (int k = 0; k <= K; k++) {
             AG_T0();
-            if (k + 1 < K) {   // step k + 1: actions, then the pickup station on AM's post of step k
+            if (k + 1 < K) {   // step k + 1: actions, pickup, then the AGV once AM posted step k's machines
                 int act[NA];
                 synth_uniform(seed, gid0 + (uint32_t)e, step0 + (uint32_t)(k + 1), act);
                 s_act[(k + 1) & 1][0][lane] = pack_actions(act, 0);
                 s_act[(k + 1) & 1][1][lane] = pack_actions(act, 4);
-                AG_SPIN_T0();
-                while (__hip_atomic_load(&s_aflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (uint32_t)(k + 1))
-                    __builtin_amdgcn_s_sleep(1);
-                AG_SPIN_ACC();
-                if (valid) {
-                    Env Ep;
-#pragma unroll
-                    for (int i = 0; i < NSTATE; i++) Ep.w[i] = 0u;
-                    Ep.w[0] = s_apost[0][lane];
-                    Ep.w[4] = s_apost[1][lane];
-                    Ep.w[5] = s_apost[2][lane];
-                    Ep.w[7 + L_PREADY] = s_apost[3][lane];
-                    const uint32_t r = pickup_execute(Ep, TL, C, act[0]);
-                    s_pick[0][lane] = Ep.w[0] >> 24;
-                    s_pick[1][lane] = Ep.w[4];
-                    s_pick[2][lane] = Ep.w[5];
-                    s_pick[3][lane] = Ep.w[7 + L_PREADY];
-                    s_pick[4][lane] = (r & 0xFFu) | ((uint32_t)act[0] << 8);
-                    s_pick[5][lane] = Ep.w[2];
+                AG_MARK(0);
+                bool fresh = k == 0;
+                if (valid && k > 0) {   // AM's reset decision at the top of this step
+                    const uint32_t w0a = s_p1[(k - 1) & 1][0][lane].x;   // P1_W0 of step k-1
+                    const int nord = (int)((w0a >> 16) & 0xFFu);
+                    const int all_done = (int)(s_kpost[0][lane] & 0xFFu) == nord && nord > 0 && (int)(w0a >> 24) == nord;
+                    fresh = autoreset && (all_done || (int)(w0a & 0xFFFFu) >= C.max_steps);
                 }
+                AG_SPIN_T0();
+                const bool wait_first = __ballot(valid && fresh) != 0;
+                if (wait_first) ag_spin(&s_flag1, (uint32_t)(k + 1));
+                AG_MARK(1);
+                Env Ep;
+#pragma unroll
+                for (int i = 0; i < NSTATE; i++) Ep.w[i] = 0u;
+                uint32_t r0 = 0;
+                if (valid) {
+                    if (fresh) {
+                        uint32_t p1[8];
+                        q_get(&s_p1[k & 1][0][lane], 2, p1);
+#pragma unroll
+                        for (int i = 0; i < 6; i++) sw[i] = p1[i];
+                    }
+                    Ep.w[0] = sw[0]; Ep.w[4] = sw[1]; Ep.w[5] = sw[2]; Ep.w[6] = sw[3]; Ep.w[7] = sw[4]; Ep.w[8] = sw[5];
+                    r0 = (pickup_execute(Ep, TL, C, act[0]) & 0xFFu) | ((uint32_t)act[0] << 8);
+                }
+                AG_MARK(2);
+                if (!wait_first) ag_spin(&s_flag1, (uint32_t)(k + 1));
+                AG_SPIN_ACC();
+                AG_MARK(3);
+                if (valid) {
+                    const uint4 p2 = s_p2[lane];
+                    Ep.w[9] = p2.x; Ep.w[10] = p2.y; Ep.w[11] = p2.z; Ep.w[12] = p2.w;
+                    int mv = 0;
+                    uint32_t pend = 0;
+                    const uint32_t r1 = (agv_execute<true>(Ep, TL, C, act[1], &mv, &pend) & 0xFFu) | ((uint32_t)act[1] << 8);
+                    if (mv) Ep.set_loc(mv);
+                    AG_MARK(4);
+                    sw[0] = Ep.w[0]; sw[1] = Ep.w[4]; sw[2] = Ep.w[5]; sw[3] = Ep.w[6]; sw[4] = Ep.w[7]; sw[5] = Ep.w[8];
+                    const uint32_t rs[16] = {Ep.w[0] >> 24, Ep.w[4], Ep.w[5], Ep.w[6], Ep.w[7], Ep.w[8], Ep.w[9],
+                                             Ep.w[10], Ep.w[11], Ep.w[12], r0, r1, Ep.w[2], 0u, 0u, pend};
+                    q_put(&s_res[(k + 1) & 1][0][lane], 4, rs);
+                }
+                AG_MARK(5);
             }
             AG_ACC(ag_busy);
-            __syncthreads();
+            AG_BARRIER();
         }
     } else if (wave == AG_PD) {
         predraw_wave<CR, PB, true, true>(S, K, lane, e, valid, s_mb, s_cp, s_nxt);
     } else {
-        // E0: rewards + int32 / float32 observation fields; E1: int8 fields, masks, term, trunc, status
-        const int part = wave == AG_E0 ? 0 : 1;
+        // E0: rewards; E1: int32 and float32 fields; E2: int8 fields, the pickup's and the AGV's
+        // masks, term, trunc, status; E3: the machines' and packaging masks
+        const int part = wave == AG_E0 ? 0 : wave == AG_E1 ? 1 : wave == AG_E2 ? 2 : 3;
         for (int k = 0; k <= K; k++) {
             AG_T0();
             if (k > 0 && valid) {
@@ -1507,10 +1577,14 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                                  g8 + C.lut[reward_index(a, r & 0xFFu, (int)((r >> 8) & 0xFu))]);
                         }
                     }
-                    PartSink<0> ps{sink};
+                } else if (part == 1) {
+                    FieldSink<(1u << NI32) - 1u, 0u, (1u << NF32) - 1u, 0u> ps{sink};
+                    observe(E, C, ps);
+                } else if (part == 3) {
+                    FieldSink<0u, 0u, 0u, ((1u << NMASK) - 1u) & ~0x7FFu> ps{sink};
                     observe(E, C, ps);
                 } else {
-                    PartSink<1> ps{sink};
+                    FieldSink<0u, (1u << NI8) - 1u, 0u, 0x7FFu> ps{sink};
                     observe(E, C, ps);
                     const int nord = E.norders();
                     const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
@@ -1521,18 +1595,29 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 }
             }
             AG_ACC(ag_busy);
-            __syncthreads();
+            AG_BARRIER();
         }
     }
 #ifdef FJSP_STAMPS
-    if (lane == 0 && blockIdx.x == 0) {   // SIMD of each wave (HW_REG_HW_ID bits 5:4)
+    // stamp slots by role: AM 0, E0 1, K 2, E1 3, P 4, PD 5, E2 6, E3 7 (scripts/diag_ag_stamps.py):
+    // [2 slot] busy, [2 slot + 1] wait, [16] steps, [17] SIMD map, [18..23] AM marks, [24] AM wall,
+    // [25 + slot] last arrivals
+    const int slot = wave == AG_AM ? 0 : wave == AG_E0 ? 1 : wave == AG_K ? 2 : wave == AG_E1 ? 3 : wave == AG_P ? 4
+                   : wave == AG_PD ? 5 : wave == AG_E2 ? 6 : 7;
+    if (lane == 0 && blockIdx.x == 0) {   // SIMD of each role (HW_REG_HW_ID bits 5:4)
         const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
-        atomicOr(&g_agstamps[13], (unsigned long long)((hw >> 4) & 3u) << (4 * wave));
+        atomicOr(&g_agstamps[17], (unsigned long long)((hw >> 4) & 3u) << (4 * slot));
     }
     if (lane == 0 && wave != AG_PD) {
-        atomicAdd(&g_agstamps[2 * wave], (unsigned long long)ag_busy);
-        atomicAdd(&g_agstamps[2 * wave + 1], (unsigned long long)ag_wait);
-        if (wave == AG_AM) atomicAdd(&g_agstamps[12], (unsigned long long)(K + 1));
+        atomicAdd(&g_agstamps[2 * slot], (unsigned long long)ag_busy);
+        atomicAdd(&g_agstamps[2 * slot + 1], (unsigned long long)ag_wait);
+        atomicAdd(&g_agstamps[25 + slot], (unsigned long long)ag_last);
+        if (wave == AG_AM) {
+            atomicAdd(&g_agstamps[16], (unsigned long long)(K + 1));
+            for (int i = 0; i < 6; i++) atomicAdd(&g_agstamps[18 + i], (unsigned long long)amt[i]);
+        }
+        if (wave == AG_P)
+            for (int i = 0; i < 6; i++) atomicAdd(&g_agstamps[33 + i], (unsigned long long)amt[i]);
     }
 #endif
 }
@@ -1952,8 +2037,8 @@ extern "C" int fjsp_debug_dump(uint32_t* out) {
 #endif
 extern "C" int fjsp_debug_agstamps(unsigned long long* out) {   // out[16]: k_step_ag per wave busy / wait, epochs
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_agstamps), sizeof(unsigned long long) * 16));
-    unsigned long long z[16] = {0};
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_agstamps), sizeof(unsigned long long) * 40));
+    unsigned long long z[40] = {0};
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_agstamps), z, sizeof(z)));
     return 0;
 }

@@ -9,6 +9,8 @@ for N in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4096").split("
     env = ve.FJSPVecEnv(N)
     env.reset(seeds=torch.arange(N))
     b = ve.Buffers(K, N, env.device, infos=False)
+    for f in [x for x in os.environ.get("NULL_OUTS", "").split(",") if x]:   # outputs not written
+        setattr(b, f, None)
     env.rollout(K, buffers=b); torch.cuda.synchronize()
     ms = []
     for r in range(5):
@@ -16,4 +18,4 @@ for N in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4096").split("
         e0.record(); env.rollout(K, step0=(r + 1) * K, buffers=b); e1.record(); torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1))
     print(json.dumps({"lib": os.path.basename(os.environ.get("FJSP_LIB", "libfjsp.so")), "N": N, "kernel": env.last_kernel(),
-                      "us_per_step": min(ms) * 1e3 / K, "us_med": sorted(ms)[2] * 1e3 / K}), flush=True)
+                      "null": os.environ.get("NULL_OUTS", ""), "us_per_step": min(ms) * 1e3 / K, "us_med": sorted(ms)[2] * 1e3 / K}), flush=True)
