@@ -1544,8 +1544,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     } else if (wave == AG_PD) {
         predraw_wave<CR, PB, true, true>(S, K, lane, e, valid, s_mb, s_cp, s_nxt);
     } else {
-        // E0: rewards; E1: int32 and float32 fields; E2: int8 fields, the pickup's and the AGV's
-        // masks, term, trunc, status; E3: the machines' and packaging masks
+        // E0: rewards; E1: int32 and float32 fields; E2: int8 fields, term, trunc, status; E3: masks
         const int part = wave == AG_E0 ? 0 : wave == AG_E1 ? 1 : wave == AG_E2 ? 2 : 3;
         for (int k = 0; k <= K; k++) {
             AG_T0();
@@ -1581,10 +1580,10 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                     FieldSink<(1u << NI32) - 1u, 0u, (1u << NF32) - 1u, 0u> ps{sink};
                     observe(E, C, ps);
                 } else if (part == 3) {
-                    FieldSink<0u, 0u, 0u, ((1u << NMASK) - 1u) & ~0x7FFu> ps{sink};
+                    FieldSink<0u, 0u, 0u, (1u << NMASK) - 1u> ps{sink};
                     observe(E, C, ps);
                 } else {
-                    FieldSink<0u, (1u << NI8) - 1u, 0u, 0x7FFu> ps{sink};
+                    FieldSink<0u, (1u << NI8) - 1u, 0u, 0u> ps{sink};
                     observe(E, C, ps);
                     const int nord = E.norders();
                     const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
