@@ -21,7 +21,7 @@ def per_kernel(path, kernel, grid):
     vals = []
     with open(path) as f:
         for row in csv.DictReader(f):
-            if row["Kernel_Name"].startswith(kernel) and int(row["Grid_Size"]) in (grid, 2 * grid, 3 * grid, 4 * grid):
+            if row["Kernel_Name"].startswith(kernel) and int(row["Grid_Size"]) % grid == 0 and int(row["Grid_Size"]) <= 16 * grid:
                 vals.append(float(row["Counter_Value"]))
     return vals
 
@@ -32,8 +32,8 @@ def main():
     ap.add_argument("--src", default=os.path.join(REPO, "gpurun_out", "prof"))
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--steps-per-launch", type=int, default=200)
-    ap.add_argument("--kernel", default="k_step_pipe")
-    ap.add_argument("--variant", default="k_step_pipe<lds,2emit,predraw>", help="fjsp_last_kernel name of the profiled launch")
+    ap.add_argument("--kernel", default="k_step_ag")
+    ap.add_argument("--variant", default="k_step_ag<lds,predraw>", help="fjsp_last_kernel name of the profiled launch")
     ap.add_argument("--algo-bytes-per-env-step", type=int, default=211)
     a = ap.parse_args()
     dst = os.path.join(REPO, "profiles", a.round)
