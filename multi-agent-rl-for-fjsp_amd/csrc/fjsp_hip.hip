@@ -1546,9 +1546,16 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     } else {
         // E0: rewards; E1: int32 and float32 fields; E2: int8 fields, term, trunc, status; E3: masks
         const int part = wave == AG_E0 ? 0 : wave == AG_E1 ? 1 : wave == AG_E2 ? 2 : 3;
+#ifdef FJSP_AG_EMIT_PRIO
+        __builtin_amdgcn_s_setprio(FJSP_AG_EMIT_PRIO);
+#endif
         for (int k = 0; k <= K; k++) {
             AG_T0();
+#ifdef FJSP_X_NOEMIT   // diagnostic timing build only: no outputs
+            if (false) {
+#else
             if (k > 0 && valid) {
+#endif
                 const uint32_t t = (uint32_t)(k - 1);
                 uint32_t v[SNAP_N];
                 snap_get(snap[(k - 1) & 1], lane, v);
