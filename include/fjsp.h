@@ -162,7 +162,9 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
  * fjsp_last_kernel_ms; set 0 while capturing the calls into a hipGraph); "predraw" (0/1,
  * default 1: the pipelined kernel with LDS tables and auto-reset draws every env's next order
  * table ahead on a fourth wave, so auto-resets need no MT draws on the critical path; the
- * results are identical either way). */
+ * results are identical either way); "agents" (0/1, default 1: uniform-random actions with LDS
+ * tables and the pre-draw run k_step_ag, the env's agents split over eight wavefronts of its
+ * workgroup; identical results). */
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value);
 int fjsp_num_envs(const fjsp_handle* h);
 /* Bytes of device state per env (HBM footprint of the SoA state). */
