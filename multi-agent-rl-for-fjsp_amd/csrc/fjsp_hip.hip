@@ -1177,6 +1177,11 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
 constexpr int AG_AM = 0, AG_P = 1, AG_E1 = 2, AG_E2 = 3, AG_K = 4, AG_E0 = 5, AG_PD = 6, AG_E3 = 7, AG_WAVES = 8;
 // packaging-owned state words (K): W1, W13..W16 (packaging run lists), W20..W29
 constexpr uint32_t K_WORDS = (1u << 1) | (0xFu << 13) | (0x3FFu << 20);
+// masks per emit wave: pickup [0,3) | the AGV's pickup / drop [9,11) | the AGV's moves [3,9),
+// machines [11,17), packaging [17,29)
+constexpr uint32_t AG_MASKS_E0 = 0x7u, AG_MASKS_E2 = 0x3u << 9, AG_MASKS_E3 = (0x3Fu << 3) | (0x3FFFFu << 11);
+static_assert((AG_MASKS_E0 | AG_MASKS_E2 | AG_MASKS_E3) == (1u << NMASK) - 1u &&
+              !(AG_MASKS_E0 & AG_MASKS_E2) && !(AG_MASKS_E0 & AG_MASKS_E3) && !(AG_MASKS_E2 & AG_MASKS_E3), "mask split");
 // snapshot slot words (PipeSnap, 32 per lane): AM writes q[0..3], K q[4..7]
 enum : int { SA_W0 = 0, SA_ST, SA_W4, SA_W5, SA_W6, SA_L0, SA_M0 = SA_L0 + 6, SA_M1, SA_R01, SA_R23,
              SK_W1 = 16, SK_P0, SK_N0 = SK_P0 + 4, SK_ST = SK_N0 + 4, SK_G, SK_R45, SK_R67 };
@@ -1204,7 +1209,11 @@ __device__ __forceinline__ void snap_put4(PipeSnap& sp, int q0, int lane, const 
 }
 
 __device__ __forceinline__ void ag_spin(uint32_t* flag, uint32_t v) {
+#ifdef FJSP_AG_TIGHT_SPIN
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) {}
+#else
     while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
+#endif
 }
 
 __global__ void __launch_bounds__(AG_WAVES * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2)))
@@ -1220,7 +1229,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     __shared__ uint8_t s_next[MAX_SLOTS * BLOCK];
     __shared__ uint16_t s_cstep[MAX_SLOTS * BLOCK];
     __shared__ PipeSnap snap[2];
-    __shared__ uint32_t s_act[2][2][BLOCK];
+    __shared__ uint32_t s_act[3][2][BLOCK];   // step k's actions in slot k % 3 (E3 draws two steps ahead)
     // hand-off slots are lane-major uint4 groups (one 16-byte LDS access per 4 words)
     __shared__ uint4 s_p1[2][2][BLOCK];   // AM post 1 (P1_*), by step parity
     __shared__ uint4 s_p2[BLOCK];         // AM post 2: W9..W12 (machine lists) after the machines' actions
@@ -1255,11 +1264,13 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
 #define AG_SPIN_ACC() ((void)0)
 #define AG_MARK(i) ((void)0)
 #endif
-    if (wave == AG_P && K > 0) {
-        int act[NA];
-        synth_uniform(seed, gid0 + (uint32_t)e, step0, act);
-        s_act[0][0][lane] = pack_actions(act, 0);
-        s_act[0][1][lane] = pack_actions(act, 4);
+    if (wave == AG_P) {   // the first two steps' actions
+        for (int j = 0; j < 2 && j < K; j++) {
+            int act[NA];
+            synth_uniform(seed, gid0 + (uint32_t)e, step0 + (uint32_t)j, act);
+            s_act[j][0][lane] = pack_actions(act, 0);
+            s_act[j][1][lane] = pack_actions(act, 4);
+        }
     }
     if (threadIdx.x == 0) s_flag1 = 0;
     if (wave == AG_AM && valid) {
@@ -1305,8 +1316,8 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             if (valid) {
                 kc = s_kpost[0][lane];
                 if (k < K) {
-                    a0 = s_act[k & 1][0][lane];
-                    a1 = s_act[k & 1][1][lane];
+                    a0 = s_act[k % 3][0][lane];
+                    a1 = s_act[k % 3][1][lane];
                     q_get(&s_res[k & 1][0][lane], 4, rs);
                 }
             }
@@ -1436,7 +1447,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 }
                 if (valid) {
                     const int step = E.step(), tp0 = E.total_packaged();
-                    const uint32_t a1 = s_act[k & 1][1][lane];
+                    const uint32_t a1 = s_act[k % 3][1][lane];
                     // completions due this step (NORMAL events older than the step's actions)
                     int done[4], orders_done = 0;
                     const bool due0 = pack_due<0>(E, TL, step), due1 = pack_due<1>(E, TL, step);
@@ -1488,11 +1499,13 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         uint32_t sw[6] = {0u, 0u, 0u, 0u, 0u, 0u};
         for (int k = 0; k <= K; k++) {
             AG_T0();
-            if (k + 1 < K) {   // step k + 1: actions, pickup, then the AGV once AM posted step k's machines
+            if (k + 1 < K) {   // step k + 1: pickup, then the AGV once AM posted step k's machines
                 int act[NA];
-                synth_uniform(seed, gid0 + (uint32_t)e, step0 + (uint32_t)(k + 1), act);
-                s_act[(k + 1) & 1][0][lane] = pack_actions(act, 0);
-                s_act[(k + 1) & 1][1][lane] = pack_actions(act, 4);
+                {
+                    const uint32_t a0 = s_act[(k + 1) % 3][0][lane], a1 = s_act[(k + 1) % 3][1][lane];
+#pragma unroll
+                    for (int a = 0; a < 4; a++) { act[a] = (a0 >> (8 * a)) & 0xFF; act[4 + a] = (a1 >> (8 * a)) & 0xFF; }
+                }
                 AG_MARK(0);
                 bool fresh = k == 0;
                 if (valid && k > 0) {   // AM's reset decision at the top of this step
@@ -1544,13 +1557,24 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     } else if (wave == AG_PD) {
         predraw_wave<CR, PB, true, true>(S, K, lane, e, valid, s_mb, s_cp, s_nxt);
     } else {
-        // E0: rewards; E1: int32 and float32 fields; E2: int8 fields, term, trunc, status; E3: masks
+        // E0: rewards, the pickup's masks; E1: int32 and float32 fields; E2: int8 fields, term,
+        // trunc, status, the AGV's pickup / drop masks; E3: the other masks (balanced by measured
+        // cycles: scripts/diag_ag_stamps.py; E0 shares P's SIMD)
         const int part = wave == AG_E0 ? 0 : wave == AG_E1 ? 1 : wave == AG_E2 ? 2 : 3;
 #ifdef FJSP_AG_EMIT_PRIO
         __builtin_amdgcn_s_setprio(FJSP_AG_EMIT_PRIO);
 #endif
         for (int k = 0; k <= K; k++) {
             AG_T0();
+            if (part == 3 && k + 2 < K) {   // E3 draws step k + 2's actions (uniform random)
+                int act[NA];
+                synth_uniform(seed, gid0 + (uint32_t)e, step0 + (uint32_t)(k + 2), act);
+                s_act[(k + 2) % 3][0][lane] = pack_actions(act, 0);
+                s_act[(k + 2) % 3][1][lane] = pack_actions(act, 4);
+            }
+#ifdef FJSP_AG_EMIT_DELAY   // experiment: let the core waves' step-top LDS reads go first
+            __builtin_amdgcn_s_sleep(FJSP_AG_EMIT_DELAY);
+#endif
 #ifdef FJSP_X_NOEMIT   // diagnostic timing build only: no outputs
             if (false) {
 #else
@@ -1583,14 +1607,16 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                                  g8 + C.lut[reward_index(a, r & 0xFFu, (int)((r >> 8) & 0xFu))]);
                         }
                     }
+                    FieldSink<0u, 0u, 0u, AG_MASKS_E0> ps{sink};
+                    observe(E, C, ps);
                 } else if (part == 1) {
                     FieldSink<(1u << NI32) - 1u, 0u, (1u << NF32) - 1u, 0u> ps{sink};
                     observe(E, C, ps);
                 } else if (part == 3) {
-                    FieldSink<0u, 0u, 0u, (1u << NMASK) - 1u> ps{sink};
+                    FieldSink<0u, 0u, 0u, AG_MASKS_E3> ps{sink};
                     observe(E, C, ps);
                 } else {
-                    FieldSink<0u, (1u << NI8) - 1u, 0u, 0u> ps{sink};
+                    FieldSink<0u, (1u << NI8) - 1u, 0u, AG_MASKS_E2> ps{sink};
                     observe(E, C, ps);
                     const int nord = E.norders();
                     const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
