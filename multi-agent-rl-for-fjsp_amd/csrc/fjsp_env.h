@@ -540,6 +540,108 @@ FJSP_DEV uint32_t agv_execute(Env& E, const Tables& T, const Cfg& C, int action,
     return r;
 }
 
+// agv_execute<true> in two halves (k_step_ag's P wave).  agv_pre needs only the AGV's own words
+// (W6: location and carried tray, W8: storage) and the list words as they were after the AGV's
+// previous step (E): it decides the action's outcome where that does not depend on other agents
+// and prefetches the front slot of the list a PICKUP would pop — a list's front does not change
+// while it is non-empty (the pickup station and the machines only append; only the AGV pops).
+// agv_fin completes the step on the final list words (after the pickup station's action and the
+// machines' actions of the previous step).  Together they equal agv_execute<true>.
+struct AgvPre {
+    int loc, carry, code, src, dst, ml, d, action;
+    bool want6, is_move, moved, ok7, at_pick, at_store, at_pack, store_full;
+    uint32_t pre_len, pnext, pcode, pow;
+};
+FJSP_DEV AgvPre agv_pre(const Env& E, const Tables& T, const Cfg& C, int action) {
+    AgvPre a;
+    a.action = action;
+    a.loc = E.loc();
+    a.carry = E.carry();
+    const bool has = a.carry != NIL;
+    a.is_move = (unsigned)(action - 1) < 5u;
+    a.ml = move_loc(action);
+    a.d = manhattan(a.loc, a.ml);
+    a.moved = a.is_move && a.d != 0;
+    a.src = nib(nibs(0, L_PREADY, L_M1R, L_M0R, L_STORAGE, L_STORAGE), a.loc);
+    a.want6 = action == 6 && !has && a.loc != LOC_PACK;
+    a.code = E.carry_code();
+    const int ty = E.carry_type(), np = E.carry_np(), nk = E.carry_nk();
+    const uint32_t cond = ((uint32_t)(tc_count(a.code) == 0) << LOC_PICKUP) |
+                          ((uint32_t)(np && (ty == 1 || ty == 2)) << LOC_SMALL) |
+                          ((uint32_t)(np && (ty == 3 || ty == 2)) << LOC_BIG) | (1u << LOC_STORAGE) |
+                          ((uint32_t)(nk && !np) << LOC_PACK);
+    a.ok7 = action == 7 && has && ((cond >> a.loc) & 1u);
+    a.at_pick = a.loc == LOC_PICKUP;
+    a.at_store = a.loc == LOC_STORAGE;
+    a.at_pack = a.loc == LOC_PACK;
+    a.store_full = E.ll(L_STORAGE) >= C.storage_cap;
+    const int base = nib(nibs(0xF, 0xF, L_M1Q, L_M0Q, L_STORAGE, L_PKG), a.loc);
+    const bool no_dst = base == 0xF || (a.at_store && a.store_full) || a.at_pack;
+    a.dst = no_dst ? -1 : base;
+    // prefetch the front of the pickup source
+    const uint32_t lws = lword<PICK_LISTS>(E, a.src);
+    a.pre_len = a.want6 ? (lws >> 16) : 0u;
+    a.pnext = 0; a.pcode = 0; a.pow = 0;
+    if (a.pre_len != 0) {
+        const int ps = (int)(lws & 0xFFu);
+        a.pnext = T.snext[ps * T.stride];
+        a.pcode = T.scode[ps * T.stride];
+        a.pow = T.orders[tc_order((int)a.pcode) * T.stride];
+    }
+    return a;
+}
+FJSP_DEV uint32_t agv_fin(Env& E, const Tables& T, const AgvPre& a, int* move_to, uint32_t* pend) {
+    const uint32_t lws = lword<PICK_LISTS>(E, a.src);
+    const uint32_t len = lws >> 16;
+    const bool ok6 = a.want6 && len != 0;
+    const int ps = (int)(lws & 0xFFu);
+    uint32_t next = a.pnext, scode = a.pcode, ow = a.pow;
+    if (ok6 && a.pre_len == 0) {   // the list was empty before: its front is new
+        next = T.snext[ps * T.stride];
+        scode = T.scode[ps * T.stride];
+        ow = T.orders[tc_order((int)scode) * T.stride];
+    } else if (ok6 && a.pre_len == 1 && len >= 2) {   // the single front got a successor
+        next = T.snext[ps * T.stride];
+    }
+    const int carry = a.carry;
+    const bool push = a.ok7 && a.dst >= 0;
+    const uint32_t lwd = lword<DROP_LISTS>(E, a.dst);
+    if (push) {
+        T.snext[carry * T.stride] = (uint8_t)NIL;
+        if ((lwd >> 16) != 0) T.snext[((lwd >> 8) & 0xFFu) * T.stride] = (uint8_t)carry;
+    }
+    const uint32_t n6 = len - 1u;
+    const uint32_t popped = n6 == 0 ? ((uint32_t)NIL | ((uint32_t)NIL << 8)) : (next | (lws & 0xFF00u) | (n6 << 16));
+    const uint32_t nd = lwd >> 16;
+    const uint32_t pushed = (nd == 0 ? (uint32_t)carry : (lwd & 0xFFu)) | ((uint32_t)carry << 8) | ((nd + 1) << 16);
+#pragma unroll
+    for (int i = 0; i < NLIST; i++) {
+        if (!(((PICK_LISTS | DROP_LISTS) >> i) & 1u)) continue;
+        uint32_t v = E.w[7 + i];
+        if ((PICK_LISTS >> i) & 1u) v = (ok6 && a.src == i) ? popped : v;
+        if ((DROP_LISTS >> i) & 1u) v = (push && a.dst == i) ? pushed : v;
+        E.w[7 + i] = v;
+    }
+    *pend = (a.ok7 && a.at_pack) ? (1u | ((uint32_t)carry << 1) | ((uint32_t)a.code << 9) | ((uint32_t)E.carry_color() << 22)) : 0u;
+    const uint32_t rg = tc_range((int)scode);
+    const bool full6 = tc_count((int)scode) > 0;
+    const uint32_t carried = (E.w[6] & 7u) | ((uint32_t)ps << 3) | (scode << 11) |
+                             (full6 ? (((uint32_t)ow_type(ow) << 24) | ((uint32_t)ow_color(ow) << 26) |
+                                       ((uint32_t)((ow & rg) != rg) << 28) | ((uint32_t)(((ow >> 9) & rg) != rg) << 29))
+                                    : 0u);
+    const uint32_t dropped = (E.w[6] & ~(0xFFu << 3)) | ((uint32_t)NIL << 3);
+    E.w[6] = ok6 ? carried : a.ok7 ? dropped : E.w[6];
+    E.set_pool(E.pool() + ((a.ok7 && a.at_pick) ? 1 : 0));
+    E.w[2] |= (a.ok7 && a.at_store && a.store_full) ? ST_TRAY_LOST : 0u;
+    if (a.moved) *move_to = a.ml;
+    const bool success = a.action == 0 || a.is_move || ok6 || a.ok7;
+    uint32_t r = R_EXEC | (success ? 1u : 2u);
+    r |= a.moved ? (4u | ((uint32_t)a.d << 16)) : 0u;
+    r |= ok6 ? 8u : 0u;
+    r |= a.ok7 ? (16u | (a.at_pack ? 32u : 0u)) : 0u;
+    return r;
+}
+
 // The packaging half of a deferred AGV drop (agv_execute<true>): route the tray to its station
 // (FJSPSimulation.add_tray_to_packaging) with the Resource counts as they are now.
 FJSP_DEV void agv_pack_drop(Env& E, const Tables& T, const Cfg& C, uint32_t pend) {

@@ -1145,32 +1145,35 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
 
 // ---------------------------------------------------------------- agent-group pipeline
 // k_step_ag: K fused steps (uniform-random actions, LDS tables, auto-reset with pre-drawn
-// tables), the env's agents split over the wavefronts of its 64-env workgroup.  Per step k the
-// only sequential chain left is  machines' actions (k) -> AGV (k+1) -> machines' actions (k+1):
-//   AM owns every state word but the packaging ones.  At the top of step k it applies the
-//      pickup and AGV results P computed during step k-1 (on a lane that just reset, and on the
-//      first step of a launch, it runs those two agents itself), posts the pickup/AGV words
-//      (post 1), runs the machines' actions (MachineAgent.py:99-139), posts the machine lists
-//      (post 2), then the machines' run phase (:151-169) and its half of the step snapshot.  At
-//      the top of the next step it auto-resets the env (FJSPSimulation.reset(seed=None)) once K
-//      has counted the step's order completions.
-//   P  draws step k+1's actions, runs step k+1's pickup station (PickupStationAgent.py:146-248)
-//      on post 1 and step k+1's AGV (AGVAgent.py:180-368, a drop at packaging deferred) on post
-//      2: in the reference's agent order the pickup and the AGV read nothing that the packaging
+// tables), the env's agents split over the wavefronts of its 64-env workgroup.  Per step the
+// chains that stay sequential are  AGV (k) -> machines' actions (k) -> AGV (k+1)  and
+// AGV (k) -> pickup station (k+1) -> AGV (k+1); everything else hangs off them:
+//   AM owns every state word but the packaging ones.  At the top of step k it auto-resets the
+//      env once K has counted step k-1's order completions (FJSPSimulation.reset(seed=None)),
+//      applies the pickup and AGV results of step k (computed during step k-1; a lane that just
+//      reset, and the first step of a launch, runs those two agents here), runs the machines'
+//      actions (MachineAgent.py:99-139), posts the pickup / AGV words and the machine lists
+//      (release flag), then the machines' run phase (:151-169) and its half of the snapshot.
+//   E3 runs step k+1's pickup station (PickupStationAgent.py:146-248) on P's AGV result of
+//      step k, and posts it (release flag).
+//   P  runs step k+1's AGV (AGVAgent.py:180-368, a drop at packaging deferred): the half that
+//      needs only the AGV's own words (agv_pre: outcome, prefetch of the list front it would
+//      pop) at the top of the step, the rest (agv_fin) once AM's post and E3's pickup are in.
+//      In the reference's agent order the pickup and the AGV read nothing that the packaging
 //      agents or the run phase of step k change.
 //   K  owns the packaging words (W1, W13-16, W20-29): at the top of step k the completions due
 //      (PackagingAgent.py:143-147, older events than the step's actions), the AGV's drop
 //      routed (FJSPSimulation.add_tray_to_packaging, with the in-flight counts before the run),
 //      the stations' actions and grants (:91-141) and the order completions
 //      (FJSPSimulation.py:245-258) — it needs only P's AGV result of the previous step.
-//   E0, E1 turn step k-1's snapshot into the outputs (as k_step_pipe's emit waves);
+//   E0..E3 turn step k-1's snapshot into the outputs; E0 also draws step k+2's actions.
 //   PD pre-draws the next order tables (predraw_wave).
 // The order words are shared by AM (processed bits) and K (packaged / complete bits): both OR
-// atomically (order_or); P reads the static fields and the bits of the tray its AGV picks up,
-// which nothing else changes then.  The tray-slot arena needs no atomics: within a step every
-// slot is written by the one wave that owns the list it joins.  Hand-offs inside a step: AM's
-// posts (release / acquire flags) -> P; everything else crosses the one barrier per step.
-// Result words are 16 bits (result | action << 8).
+// atomically (order_or); P and E3 read the static fields and the bits of the tray the AGV picks
+// up, which nothing else changes then.  The tray-slot arena needs no atomics: within a step
+// every slot is written by the one wave that owns the list it joins.  Hand-offs inside a step:
+// release / acquire flags (AM -> P, E3, K; E3 -> P); everything else crosses the one barrier
+// per step.  Result words are 16 bits (result | action << 8).
 // Waves w and w + 4 share a SIMD (two waves per SIMD issue VALU at twice one wave's rate): K
 // shares AM's (both busy early in the step; AM has the higher priority), P (the critical path
 // after AM's post, higher priority) shares the lightest emit wave's, PD and E3 pair up.
@@ -1208,6 +1211,18 @@ __device__ __forceinline__ void snap_put4(PipeSnap& sp, int q0, int lane, const 
     for (int g = 0; g < 4; g++) sp.q[q0 + g][lane] = make_uint4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
 }
 
+// AM's reset decision at the top of step k (end of step k-1), as P and E0 see it: AM's W0 posted
+// in step k-1 (next_order, num_orders, step) and K's completed orders after step k-1.
+__device__ __forceinline__ bool ag_fresh(int k, bool valid, const uint4 (*s_p1)[2][BLOCK], const uint32_t (*s_kpost)[BLOCK],
+                                         int lane, const Cfg& C, int autoreset) {
+    if (k == 0) return true;   // the first step of a launch runs the pickup and the AGV on AM
+    if (!valid) return false;
+    const uint32_t w0a = s_p1[(k - 1) & 1][0][lane].x;   // P1_W0 of step k-1
+    const int nord = (int)((w0a >> 16) & 0xFFu);
+    const int all_done = (int)(s_kpost[0][lane] & 0xFFu) == nord && nord > 0 && (int)(w0a >> 24) == nord;
+    return autoreset && (all_done || (int)(w0a & 0xFFFFu) >= C.max_steps);
+}
+
 __device__ __forceinline__ void ag_spin(uint32_t* flag, uint32_t v) {
 #ifdef FJSP_AG_TIGHT_SPIN
     while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) {}
@@ -1229,13 +1244,16 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     __shared__ uint8_t s_next[MAX_SLOTS * BLOCK];
     __shared__ uint16_t s_cstep[MAX_SLOTS * BLOCK];
     __shared__ PipeSnap snap[2];
-    __shared__ uint32_t s_act[3][2][BLOCK];   // step k's actions in slot k % 3 (E3 draws two steps ahead)
+    __shared__ uint32_t s_act[3][2][BLOCK];   // step k's actions in slot k % 3 (E0 draws two steps ahead)
     // hand-off slots are lane-major uint4 groups (one 16-byte LDS access per 4 words)
     __shared__ uint4 s_p1[2][2][BLOCK];   // AM post 1 (P1_*), by step parity
     __shared__ uint4 s_p2[BLOCK];         // AM post 2: W9..W12 (machine lists) after the machines' actions
     __shared__ uint4 s_res[2][4][BLOCK];  // P: step k+1's pickup + AGV results (RS_*), by step parity
     __shared__ uint32_t s_kpost[2][BLOCK];      // K after step k: W1 (completed orders), final status
     __shared__ uint32_t s_flag1;   // AM posted step k's pickup / AGV words and machine lists (k + 1)
+    __shared__ uint32_t s_uflag;   // E3 posted step k+1's pickup (k + 1)
+    __shared__ uint4 s_pk[BLOCK];   // E3: W0, W4, W5, W7 after step k+1's pickup
+    __shared__ uint2 s_pkr[BLOCK];  // E3: its result word, status bits
     __shared__ double s_lut[RLUT_SIZE];
     for (int i = threadIdx.x; i < RLUT_SIZE; i += AG_WAVES * BLOCK) s_lut[i] = C.lut[i];
     C.lut = s_lut;
@@ -1272,7 +1290,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             s_act[j][1][lane] = pack_actions(act, 4);
         }
     }
-    if (threadIdx.x == 0) s_flag1 = 0;
+    if (threadIdx.x == 0) { s_flag1 = 0; s_uflag = 0; }
     if (wave == AG_AM && valid) {
         // the env's order table and used slot prefix live in LDS for the launch (copied in before
         // the first barrier: K's first completions read them)
@@ -1494,59 +1512,55 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         }
     } else if (wave == AG_P) {
         __builtin_amdgcn_s_setprio(3);
-        // W0, W4, W5, W6, W7, W8 after this wave's last AGV: the next pickup's inputs unless AM
-        // reset the env (or the launch starts), when they come from AM's post of this step
-        uint32_t sw[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+        // W6..W12 after this wave's last AGV: the next AGV's own words and the list fronts it
+        // prefetches, unless AM reset the env (or the launch starts): then AM's post of the step
+        uint32_t sa[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
         for (int k = 0; k <= K; k++) {
             AG_T0();
-            if (k + 1 < K) {   // step k + 1: pickup, then the AGV once AM posted step k's machines
-                int act[NA];
-                {
-                    const uint32_t a0 = s_act[(k + 1) % 3][0][lane], a1 = s_act[(k + 1) % 3][1][lane];
-#pragma unroll
-                    for (int a = 0; a < 4; a++) { act[a] = (a0 >> (8 * a)) & 0xFF; act[4 + a] = (a1 >> (8 * a)) & 0xFF; }
-                }
+            if (k + 1 < K) {   // step k + 1's AGV: its own half now, the rest on AM's post and E3's pickup
+                const int act1 = (int)((s_act[(k + 1) % 3][0][lane] >> 8) & 0xFFu);
                 AG_MARK(0);
-                bool fresh = k == 0;
-                if (valid && k > 0) {   // AM's reset decision at the top of this step
-                    const uint32_t w0a = s_p1[(k - 1) & 1][0][lane].x;   // P1_W0 of step k-1
-                    const int nord = (int)((w0a >> 16) & 0xFFu);
-                    const int all_done = (int)(s_kpost[0][lane] & 0xFFu) == nord && nord > 0 && (int)(w0a >> 24) == nord;
-                    fresh = autoreset && (all_done || (int)(w0a & 0xFFFFu) >= C.max_steps);
-                }
+                const bool fresh = ag_fresh(k, valid, s_p1, s_kpost, lane, C, autoreset);
                 AG_SPIN_T0();
                 const bool wait_first = __ballot(valid && fresh) != 0;
                 if (wait_first) ag_spin(&s_flag1, (uint32_t)(k + 1));
                 AG_MARK(1);
-                Env Ep;
+                Env Ea;
 #pragma unroll
-                for (int i = 0; i < NSTATE; i++) Ep.w[i] = 0u;
-                uint32_t r0 = 0;
+                for (int i = 0; i < NSTATE; i++) Ea.w[i] = 0u;
+                AgvPre pre{};
                 if (valid) {
                     if (fresh) {
                         uint32_t p1[8];
                         q_get(&s_p1[k & 1][0][lane], 2, p1);
-#pragma unroll
-                        for (int i = 0; i < 6; i++) sw[i] = p1[i];
+                        const uint4 p2 = s_p2[lane];
+                        sa[0] = p1[P1_W6]; sa[1] = p1[P1_W7]; sa[2] = p1[P1_W8];
+                        sa[3] = p2.x; sa[4] = p2.y; sa[5] = p2.z; sa[6] = p2.w;
                     }
-                    Ep.w[0] = sw[0]; Ep.w[4] = sw[1]; Ep.w[5] = sw[2]; Ep.w[6] = sw[3]; Ep.w[7] = sw[4]; Ep.w[8] = sw[5];
-                    r0 = (pickup_execute(Ep, TL, C, act[0]) & 0xFFu) | ((uint32_t)act[0] << 8);
+#pragma unroll
+                    for (int i = 0; i < 7; i++) Ea.w[6 + i] = sa[i];
+                    pre = agv_pre(Ea, TL, C, act1);
                 }
                 AG_MARK(2);
                 if (!wait_first) ag_spin(&s_flag1, (uint32_t)(k + 1));
+                ag_spin(&s_uflag, (uint32_t)(k + 1));
                 AG_SPIN_ACC();
                 AG_MARK(3);
                 if (valid) {
                     const uint4 p2 = s_p2[lane];
-                    Ep.w[9] = p2.x; Ep.w[10] = p2.y; Ep.w[11] = p2.z; Ep.w[12] = p2.w;
+                    const uint4 pk = s_pk[lane];        // E3: W0, W4, W5, W7 after step k+1's pickup
+                    const uint2 pr = s_pkr[lane];       // E3: pickup result, status bits
+                    Ea.w[5] = pk.z; Ea.w[7] = pk.w;
+                    Ea.w[9] = p2.x; Ea.w[10] = p2.y; Ea.w[11] = p2.z; Ea.w[12] = p2.w;
                     int mv = 0;
                     uint32_t pend = 0;
-                    const uint32_t r1 = (agv_execute<true>(Ep, TL, C, act[1], &mv, &pend) & 0xFFu) | ((uint32_t)act[1] << 8);
-                    if (mv) Ep.set_loc(mv);
+                    const uint32_t r1 = (agv_fin(Ea, TL, pre, &mv, &pend) & 0xFFu) | ((uint32_t)act1 << 8);
+                    if (mv) Ea.set_loc(mv);
                     AG_MARK(4);
-                    sw[0] = Ep.w[0]; sw[1] = Ep.w[4]; sw[2] = Ep.w[5]; sw[3] = Ep.w[6]; sw[4] = Ep.w[7]; sw[5] = Ep.w[8];
-                    const uint32_t rs[16] = {Ep.w[0] >> 24, Ep.w[4], Ep.w[5], Ep.w[6], Ep.w[7], Ep.w[8], Ep.w[9],
-                                             Ep.w[10], Ep.w[11], Ep.w[12], r0, r1, Ep.w[2], 0u, 0u, pend};
+#pragma unroll
+                    for (int i = 0; i < 7; i++) sa[i] = Ea.w[6 + i];
+                    const uint32_t rs[16] = {pk.x >> 24, pk.y, Ea.w[5], Ea.w[6], Ea.w[7], Ea.w[8], Ea.w[9],
+                                             Ea.w[10], Ea.w[11], Ea.w[12], pr.x, r1, pr.y | Ea.w[2], 0u, 0u, pend};
                     q_put(&s_res[(k + 1) & 1][0][lane], 4, rs);
                 }
                 AG_MARK(5);
@@ -1557,16 +1571,42 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     } else if (wave == AG_PD) {
         predraw_wave<CR, PB, true, true>(S, K, lane, e, valid, s_mb, s_cp, s_nxt);
     } else {
-        // E0: rewards, the pickup's masks; E1: int32 and float32 fields; E2: int8 fields, term,
-        // trunc, status, the AGV's pickup / drop masks; E3: the other masks (balanced by measured
-        // cycles: scripts/diag_ag_stamps.py; E0 shares P's SIMD)
+        // E0: step k+2's actions, rewards, the pickup's masks; E1: int32 and float32 fields; E2:
+        // int8 fields, term, trunc, status, the AGV's pickup / drop masks; E3: step k+1's pickup
+        // station (for P), the other masks (balanced by measured cycles: scripts/diag_ag_stamps.py;
+        // E0 shares P's SIMD)
         const int part = wave == AG_E0 ? 0 : wave == AG_E1 ? 1 : wave == AG_E2 ? 2 : 3;
+        if (part == 3) __builtin_amdgcn_s_setprio(2);   // E3 runs the pickup station for P first
 #ifdef FJSP_AG_EMIT_PRIO
         __builtin_amdgcn_s_setprio(FJSP_AG_EMIT_PRIO);
 #endif
         for (int k = 0; k <= K; k++) {
             AG_T0();
-            if (part == 3 && k + 2 < K) {   // E3 draws step k + 2's actions (uniform random)
+            if (part == 3 && k + 1 < K) {   // step k+1's pickup station, from P's AGV result of step k
+                const bool fresh = ag_fresh(k, valid, s_p1, s_kpost, lane, C, autoreset);
+                if (__ballot(valid && fresh) != 0) ag_spin(&s_flag1, (uint32_t)(k + 1));
+                if (valid) {
+                    Env Ep;
+#pragma unroll
+                    for (int i = 0; i < NSTATE; i++) Ep.w[i] = 0u;
+                    if (fresh) {
+                        uint32_t p1[8];
+                        q_get(&s_p1[k & 1][0][lane], 2, p1);
+                        Ep.w[0] = p1[P1_W0]; Ep.w[4] = p1[P1_W4]; Ep.w[5] = p1[P1_W5]; Ep.w[7] = p1[P1_W7];
+                    } else {
+                        uint32_t rs[16];
+                        q_get(&s_res[k & 1][0][lane], 2, rs);   // RS_NO, RS_W4, RS_W5..: W5, W6, W7
+                        Ep.w[0] = (s_p1[(k - 1) & 1][0][lane].x & 0x00FFFFFFu) | (rs[RS_NO] << 24);
+                        Ep.w[4] = rs[RS_W4]; Ep.w[5] = rs[RS_W5]; Ep.w[7] = rs[RS_W5 + 2];
+                    }
+                    const int act0 = (int)(s_act[(k + 1) % 3][0][lane] & 0xFFu);
+                    const uint32_t r0 = (pickup_execute(Ep, TL, C, act0) & 0xFFu) | ((uint32_t)act0 << 8);
+                    s_pk[lane] = make_uint4(Ep.w[0], Ep.w[4], Ep.w[5], Ep.w[7]);
+                    s_pkr[lane] = make_uint2(r0, Ep.w[2]);
+                    __hip_atomic_store(&s_uflag, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            if (part == 0 && k + 2 < K) {   // E0 draws step k + 2's actions (uniform random)
                 int act[NA];
                 synth_uniform(seed, gid0 + (uint32_t)e, step0 + (uint32_t)(k + 2), act);
                 s_act[(k + 2) % 3][0][lane] = pack_actions(act, 0);
