@@ -164,7 +164,10 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
  * table ahead on a fourth wave, so auto-resets need no MT draws on the critical path; the
  * results are identical either way); "agents" (0/1, default 1: uniform-random actions with LDS
  * tables and the pre-draw run k_step_ag, the env's agents split over eight wavefronts of its
- * workgroup; identical results). */
+ * workgroup; identical results); "emit_wg" (0/1, default 0: k_step_ag's outputs are written by
+ * emit workgroups of their own, one per core workgroup on another CU, fed step snapshots through
+ * global memory; used while every block has a CU of its own, N <= 64 x CUs / 2; identical
+ * results). */
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value);
 int fjsp_num_envs(const fjsp_handle* h);
 /* Bytes of device state per env (HBM footprint of the SoA state). */

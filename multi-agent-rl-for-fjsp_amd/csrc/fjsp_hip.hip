@@ -34,7 +34,7 @@ constexpr int MT_N = 624;
 __device__ unsigned long long g_stamps[8];
 __device__ unsigned long long g_pgstamps[4];   // pre-draw wave: busy cycles, active steps, busy in active steps, steps
 __device__ unsigned long long g_emitstamps[4];   // emit waves 1, 2: busy cycles, steps
-__device__ unsigned long long g_agstamps[40];   // k_step_ag (scripts/diag_ag_stamps.py)   // k_step_ag: per wave [busy, wait] cycles, epochs
+__device__ unsigned long long g_agstamps[56];   // k_step_ag (scripts/diag_ag_stamps.py)   // k_step_ag: per wave [busy, wait] cycles, epochs
 #define AG_T0() const uint64_t _ag_t0 = __builtin_amdgcn_s_memtime()
 #define AG_ACC(v) ((v) += __builtin_amdgcn_s_memtime() - _ag_t0)
 #else
@@ -105,13 +105,11 @@ __device__ void mt_seed(uint32_t* __restrict__ mt, int e, uint32_t seed) {
 // batch inside the row (a multiple of 4; a batch never crosses the wrap).
 constexpr int MTB = 32;
 
+// the two runs of a refill at pa (mt_batch), as uint4
 template <int B>
-__device__ __forceinline__ void mt_batch(uint32_t* __restrict__ roww, int pos, int& g, uint32_t (&v)[B], int& pa,
-                                         int& cnt) {
-    uint4* row = reinterpret_cast<uint4*>(roww);
-    pa = pos & ~3;
-    cnt = (MT_N - pa) < B ? (MT_N - pa) : B;
-    uint32_t a[B + 4], c[B + 4];
+__device__ __forceinline__ void mt_load(const uint32_t* __restrict__ roww, int pa, uint4 (&va)[(B + 4) / 4],
+                                        uint4 (&vc)[(B + 4) / 4]) {
+    const uint4* row = reinterpret_cast<const uint4*>(roww);
 #pragma unroll
     for (int q = 0; q < (B + 4) / 4; q++) {
         int ia = pa + 4 * q;
@@ -119,9 +117,23 @@ __device__ __forceinline__ void mt_batch(uint32_t* __restrict__ roww, int pos, i
         int ic = pa + 396 + 4 * q;
         ic = ic >= MT_N ? ic - MT_N : ic;
         ic = ic >= MT_N ? ic - MT_N : ic;
-        const uint4 va = row[ia >> 2], vc = row[ic >> 2];
-        a[4 * q] = va.x; a[4 * q + 1] = va.y; a[4 * q + 2] = va.z; a[4 * q + 3] = va.w;
-        c[4 * q] = vc.x; c[4 * q + 1] = vc.y; c[4 * q + 2] = vc.z; c[4 * q + 3] = vc.w;
+        va[q] = row[ia >> 2];
+        vc[q] = row[ic >> 2];
+    }
+}
+
+// mt_batch on runs already loaded (mt_load at pa = pos & ~3, no store to them since)
+template <int B>
+__device__ __forceinline__ void mt_batch_loaded(uint32_t* __restrict__ roww, int pos, int& g, uint32_t (&v)[B], int& pa,
+                                                int& cnt, const uint4 (&va)[(B + 4) / 4], const uint4 (&vc)[(B + 4) / 4]) {
+    uint4* row = reinterpret_cast<uint4*>(roww);
+    pa = pos & ~3;
+    cnt = (MT_N - pa) < B ? (MT_N - pa) : B;
+    uint32_t a[B + 4], c[B + 4];
+#pragma unroll
+    for (int q = 0; q < (B + 4) / 4; q++) {
+        a[4 * q] = va[q].x; a[4 * q + 1] = va[q].y; a[4 * q + 2] = va[q].z; a[4 * q + 3] = va[q].w;
+        c[4 * q] = vc[q].x; c[4 * q + 1] = vc[q].y; c[4 * q + 2] = vc[q].z; c[4 * q + 3] = vc[q].w;
     }
     uint32_t w[B];
 #pragma unroll
@@ -141,6 +153,14 @@ __device__ __forceinline__ void mt_batch(uint32_t* __restrict__ roww, int pos, i
     for (int q = 0; q < B / 4; q++)
         if (4 * q < cnt) row[(pa >> 2) + q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
     if (pa + cnt > g) g = pa + cnt;
+}
+
+template <int B>
+__device__ __forceinline__ void mt_batch(uint32_t* __restrict__ roww, int pos, int& g, uint32_t (&v)[B], int& pa,
+                                         int& cnt) {
+    uint4 va[(B + 4) / 4], vc[(B + 4) / 4];
+    mt_load<B>(roww, pos & ~3, va, vc);
+    mt_batch_loaded<B>(roww, pos, g, v, pa, cnt, va, vc);
 }
 
 // generate_order (FJSPSimulation.py:101-131) as a state machine over the stream: per order
@@ -662,6 +682,16 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
     int ls_prev[CR];       // ASYNC: lanes whose row DMA is in flight (ph == 4) and their source rows
     uint32_t sl_prev[CR];
     bool inflight = false;
+    // ASYNC: the runs of the next refill, loaded a step ahead (after the draw that precedes it):
+    // the draw waits for loads a step old, not for loads it issues; pf_pa = their refill, -1 none
+    uint4 pfa[(PB + 4) / 4], pfc[(PB + 4) / 4];
+    int pf_pa = -1;
+    // ASYNC: the rows in flight, in registers (plain loads are not waited for at the barrier; an
+    // LDS DMA is: the barrier's fence drains it)
+    // (three scalars, not an array: an array here stays in scratch memory and each load is
+    // waited for at once)
+    static_assert(!ASYNC || CR == 1, "one row in flight per step");
+    uint4 cp0 = make_uint4(0u, 0u, 0u, 0u), cp1 = cp0, cp2 = cp0;
     if (valid) {
         const uint32_t pg = S.words[(size_t)PGW * n + e];
         if (pg & 1u) {
@@ -674,7 +704,7 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
         }
     }
 #ifdef FJSP_STAMPS
-    uint64_t pg_busy = 0, pg_act = 0, pg_busy_act = 0;
+    uint64_t pg_busy = 0, pg_act = 0, pg_busy_act = 0, pg_ph[3] = {0, 0, 0};
 #endif
     for (int k = 0; k <= K; k++) {
 #ifdef FJSP_STAMPS
@@ -691,6 +721,7 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
                 pos = (int)(sw & 0x3FFu);
                 g = (int)((sw >> 16) & 0x3FFu);
                 d = OrderDraw{0, 0, 0, 0, 0u};
+                pf_pa = -1;
 #ifdef FJSP_PG_IDLE
                 ph = 0;   // diagnostic: the pre-draw wave only keeps the mailboxes
 #else
@@ -701,43 +732,68 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
         // Copy the live rows of up to CR envs that start a pre-draw (the whole wave, one
         // env at a time: contiguous 1 KB loads): loads first, the per-lane draw in the shadow
         // of their latency, then the stores.  Rows copied in step k are first read in k + 1.
-        auto draw_step = [&]() {
+        // ASYNC: the runs of the next refill from pos (disjoint from the words stored since)
+        auto prefetch = [&](const uint32_t* work) __attribute__((always_inline)) {
+            pf_pa = pos & ~3;
+            mt_load<PB>(work, pf_pa, pfa, pfc);
+        };
+        auto draw_step = [&]() __attribute__((always_inline)) {
             if (valid && ph == 2) {
                 uint32_t* work = S.mt + ((size_t)(src ^ 1u) * n + e) * MT_N;
                 uint32_t v[PB];
                 int pa, cnt;
-                mt_batch<PB>(work, pos, g, v, pa, cnt);
+                if (ASYNC && pf_pa == (pos & ~3)) {
+                    mt_batch_loaded<PB>(work, pos, g, v, pa, cnt, pfa, pfc);
+                } else {
+                    mt_batch<PB>(work, pos, g, v, pa, cnt);
+                }
                 pos += draw_orders<PB>(v, pos - pa, cnt, nord, d, s_nxt + lane, BLOCK);
                 if (pos == MT_N) { pos = 0; g = 0; }
                 if (d.o >= nord) ph = 3;
+                if (ASYNC) {
+                    if (ph == 2) prefetch(work);
+                    else pf_pa = -1;
+                }
             }
         };
-        if (ASYNC && inflight) {   // last step's row DMAs: store them, the lanes draw from the next step on
-            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-            const int pb = (k - 1) & 1;
-#pragma unroll
-            for (int r = 0; r < CR; r++) {
-                const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls_prev[r];
-                uint4* rd = reinterpret_cast<uint4*>(S.mt + ((size_t)(sl_prev[r] ^ 1u) * n + el) * MT_N);
-                rd[lane] = s_cp[pb * CR + r][0][lane];
-                rd[lane + 64] = s_cp[pb * CR + r][1][lane];
-                if (lane + 128 < MT_N / 4) rd[lane + 128] = s_cp[pb * CR + r][2][lane];
-            }
-            inflight = false;
-        }
+#ifdef FJSP_STAMPS
+        const uint64_t pt1 = __builtin_amdgcn_s_memtime();
+#endif
         const int promote = ph;   // ASYNC: ph == 4 lanes become drawable after this step's draw
         uint64_t need = __ballot(valid && ph == 1);
 #ifdef FJSP_STAMPS
         pg_active = need != 0 || __ballot(valid && ph == 2) != 0;
 #endif
         if (ASYNC) {
+            // the draw first (its runs were loaded two steps ago), then last step's rows (loaded
+            // after that step's prefetches), then this step's row loads: each wait is for loads
+            // a step old, never for the ones just issued (vmcnt counts in order)
             draw_step();
+#ifdef FJSP_STAMPS
+            const uint64_t pt2 = __builtin_amdgcn_s_memtime();
+            if (pg_active) { pg_ph[0] += pt1 - pt0; pg_ph[1] += pt2 - pt1; }
+#endif
+            if (ASYNC && inflight) {   // last step's row DMAs: store them, the lanes draw from the next step on
+                const int pb = (k - 1) & 1;
+#pragma unroll
+                for (int r = 0; r < CR; r++) {
+                    const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls_prev[r];
+                    uint4* rd = reinterpret_cast<uint4*>(S.mt + ((size_t)(sl_prev[r] ^ 1u) * n + el) * MT_N);
+                    rd[lane] = cp0;
+                    rd[lane + 64] = cp1;
+                    if (lane + 128 < MT_N / 4) rd[lane + 128] = cp2;
+                }
+                (void)pb;
+                inflight = false;
+            }
+
 #pragma unroll
             for (int r = 0; r < CR; r++)
                 if (promote == 4 && ph == 4 && lane == ls_prev[r]) ph = 2;
+            if (valid && promote == 4 && ph == 2)   // rows stored above: their first refill
+                prefetch(S.mt + ((size_t)(src ^ 1u) * n + e) * MT_N);
             if (need) {
                 const int first = __builtin_ctzll(need);
-                const int cb = k & 1;
 #pragma unroll
                 for (int r = 0; r < CR; r++) {
                     ls_prev[r] = need ? __builtin_ctzll(need) : first;
@@ -745,11 +801,9 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
                     sl_prev[r] = (uint32_t)__builtin_amdgcn_readlane((int)src, ls_prev[r]);
                     const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls_prev[r];
                     const uint4* rs = reinterpret_cast<const uint4*>(S.mt + ((size_t)sl_prev[r] * n + el) * MT_N);
-#pragma unroll
-                    for (int i = 0; i < 3; i++)
-                        __builtin_amdgcn_global_load_lds(
-                            (__attribute__((address_space(1))) void*)(rs + min(lane + 64 * i, MT_N / 4 - 1)),
-                            (__attribute__((address_space(3))) void*)&s_cp[cb * CR + r][i][0], 16, 0, 0);
+                    cp0 = rs[lane];
+                    cp1 = rs[lane + 64];
+                    cp2 = rs[min(lane + 128, MT_N / 4 - 1)];
                     if (lane == ls_prev[r] && ph == 1) ph = 4;
                 }
                 inflight = true;
@@ -797,6 +851,7 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
             const uint64_t dt = __builtin_amdgcn_s_memtime() - pt0;
             pg_busy += dt;
             if (pg_active) { pg_act += 1; pg_busy_act += dt; }
+            (void)pg_ph;
         }
 #endif
         __syncthreads();
@@ -808,6 +863,7 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
         atomicAdd(&g_pgstamps[1], (unsigned long long)pg_act);
         atomicAdd(&g_pgstamps[2], (unsigned long long)pg_busy_act);
         atomicAdd(&g_pgstamps[3], (unsigned long long)(K + 1));
+        if (ASYNC) { atomicAdd(&g_agstamps[52], (unsigned long long)pg_ph[0]); atomicAdd(&g_agstamps[53], (unsigned long long)pg_ph[1]); }
     }
 #endif
     if (valid) {
@@ -1182,9 +1238,14 @@ constexpr int AG_AM = 0, AG_P = 1, AG_E1 = 2, AG_E2 = 3, AG_K = 4, AG_E0 = 5, AG
 constexpr uint32_t K_WORDS = (1u << 1) | (0xFu << 13) | (0x3FFu << 20);
 // masks per emit wave: pickup [0,3) | the AGV's pickup / drop [9,11) | the AGV's moves [3,9),
 // machines [11,17), packaging [17,29)
-constexpr uint32_t AG_MASKS_E0 = 0x7u, AG_MASKS_E2 = 0x3u << 9, AG_MASKS_E3 = (0x3Fu << 3) | (0x3FFFFu << 11);
-static_assert((AG_MASKS_E0 | AG_MASKS_E2 | AG_MASKS_E3) == (1u << NMASK) - 1u &&
-              !(AG_MASKS_E0 & AG_MASKS_E2) && !(AG_MASKS_E0 & AG_MASKS_E3) && !(AG_MASKS_E2 & AG_MASKS_E3), "mask split");
+#ifndef FJSP_AG_E1MASKS
+#define FJSP_AG_E1MASKS 0u
+#endif
+constexpr uint32_t AG_MASKS_E0 = 0x7u, AG_MASKS_E2 = 0x3u << 9, AG_MASKS_E1 = FJSP_AG_E1MASKS,
+                   AG_MASKS_E3 = ((0x3Fu << 3) | (0x3FFFFu << 11)) & ~AG_MASKS_E1;
+static_assert((AG_MASKS_E0 | AG_MASKS_E1 | AG_MASKS_E2 | AG_MASKS_E3) == (1u << NMASK) - 1u &&
+              !(AG_MASKS_E0 & AG_MASKS_E2) && !(AG_MASKS_E0 & AG_MASKS_E3) && !(AG_MASKS_E2 & AG_MASKS_E3) &&
+              !(AG_MASKS_E1 & (AG_MASKS_E0 | AG_MASKS_E2)), "mask split");
 // snapshot slot words (PipeSnap, 32 per lane): AM writes q[0..3], K q[4..7]
 enum : int { SA_W0 = 0, SA_ST, SA_W4, SA_W5, SA_W6, SA_L0, SA_M0 = SA_L0 + 6, SA_M1, SA_R01, SA_R23,
              SK_W1 = 16, SK_P0, SK_N0 = SK_P0 + 4, SK_ST = SK_N0 + 4, SK_G, SK_R45, SK_R67 };
@@ -1219,8 +1280,103 @@ __device__ __forceinline__ bool ag_fresh(int k, bool valid, const uint4 (*s_p1)[
     if (!valid) return false;
     const uint32_t w0a = s_p1[(k - 1) & 1][0][lane].x;   // P1_W0 of step k-1
     const int nord = (int)((w0a >> 16) & 0xFFu);
-    const int all_done = (int)(s_kpost[0][lane] & 0xFFu) == nord && nord > 0 && (int)(w0a >> 24) == nord;
+    const int all_done = (int)(s_kpost[(k - 1) & 1][lane] & 0xFFu) == nord && nord > 0 && (int)(w0a >> 24) == nord;
     return autoreset && (all_done || (int)(w0a & 0xFFFFu) >= C.max_steps);
+}
+
+// One emit role's outputs of step t from the step's snapshot (AM's and K's words, SA_* / SK_*):
+// E0 rewards and the pickup's masks, E1 int32 and float32 fields, E2 int8 fields, term, trunc,
+// status and the AGV's pickup / drop masks, E3 the other masks.
+__device__ __forceinline__ void ag_emit(int part, const uint32_t* v, uint32_t t, uint32_t n, uint32_t ue, const Cfg& C,
+                                        const fjsp_out& out) {
+    Env E;
+#pragma unroll
+    for (int i = 0; i < NSTATE; i++) E.w[i] = 0u;
+    E.w[0] = v[SA_W0]; E.w[2] = v[SA_ST] | v[SK_ST]; E.w[4] = v[SA_W4]; E.w[5] = v[SA_W5];
+    E.w[6] = v[SA_W6];
+#pragma unroll
+    for (int l = 0; l < 6; l++) E.w[7 + l] = v[SA_L0 + l];
+    E.w[17] = v[SA_M0]; E.w[18] = v[SA_M1];
+    E.w[1] = v[SK_W1];
+#pragma unroll
+    for (int s = 0; s < 4; s++) { E.w[20 + s] = v[SK_P0 + s]; E.w[26 + s] = v[SK_N0 + s]; }
+    const StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, ue};
+    if (part == 0) {
+        if (out.rewards) {
+            const uint32_t gs = v[SK_G];
+            const double g8 = global_reward8(C, (int)(gs & 0xFFFFu), (int)(gs >> 16));
+            const uint32_t rw[4] = {v[SA_R01], v[SA_R23], v[SK_R45], v[SK_R67]};
+#pragma unroll
+            for (int a = 0; a < NA; a++) {
+                const uint32_t r = (rw[a >> 1] >> (16 * (a & 1))) & 0xFFFFu;
+                st32(out.rewards, (t * NA + (uint32_t)a) * n + ue,
+                     g8 + C.lut[reward_index(a, r & 0xFFu, (int)((r >> 8) & 0xFu))]);
+            }
+        }
+        FieldSink<0u, 0u, 0u, AG_MASKS_E0> ps{sink};
+        observe(E, C, ps);
+    } else if (part == 1) {
+        FieldSink<(1u << NI32) - 1u, 0u, (1u << NF32) - 1u, AG_MASKS_E1> ps{sink};
+        observe(E, C, ps);
+    } else if (part == 3) {
+        FieldSink<0u, 0u, 0u, AG_MASKS_E3> ps{sink};
+        observe(E, C, ps);
+    } else {
+        FieldSink<0u, (1u << NI8) - 1u, 0u, AG_MASKS_E2> ps{sink};
+        observe(E, C, ps);
+        const int nord = E.norders();
+        const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
+        const int truncated = E.step() >= C.max_steps;
+        if (out.term) st32(out.term, t * n + ue, (uint8_t)all_done);
+        if (out.trunc) st32(out.trunc, t * n + ue, (uint8_t)truncated);
+        if (out.status) st32(out.status, t * n + ue, E.status());
+    }
+}
+
+// Emit workgroups (k_step_ag<..., emit-wg>): the core workgroup's publisher wave (E1) copies
+// each step's snapshot to a global slot and raises the core's published-step count; an emit
+// workgroup of its own (grid blocks ncore..2*ncore-1, on another CU) turns the snapshots into
+// the outputs, so the output stores neither hold up the core's barrier nor share its LDS and
+// SIMDs.  The hand-off is the guide's sc1 form (MI355X_MICROARCH.md, inter-workgroup
+// visibility, first row): every snapshot byte is stored with 8-byte sc1 (write-through) stores,
+// the publisher waits vmcnt(0) for them before ONE lane's sc1 store of the count, the consumer
+// polls it with sc1 loads and reads the bytes with sc1 loads only.  Placement-independent; the
+// launch uses it only when every block of the grid has a CU of its own (co-resident, no
+// deadlock: a core never waits on an emitter).
+struct AgEmit {
+    uint64_t* snap;    // [K][ncore][SNAP_N / 2][BLOCK] snapshot words in pairs; null: emit in the core
+    uint32_t* count;   // [ncore * 32]: base + steps published by core c (one 128-byte line each)
+    int ncore;
+    uint32_t base;     // this launch's count origin (above every count an earlier launch left)
+};
+constexpr int AG_COUNT_STRIDE = 32;
+
+// An emit workgroup's 8 waves: wave w emits role w % 4 of the steps t = w / 4 (mod 2).
+__device__ __forceinline__ void ag_emitter(const AgEmit& X, int core, int wave, int lane, int K, uint32_t n,
+                                           const Cfg& C, const fjsp_out& out) {
+    const uint32_t ue = (uint32_t)(core * BLOCK + lane);
+    const bool valid = ue < n;
+    const int part = wave & 3;
+    uint32_t* cnt = X.count + (size_t)core * AG_COUNT_STRIDE;
+    int avail = 0;
+    for (int t = wave >> 2; t < K; t += 2) {
+        // bounded: the core always finishes (it waits on no emitter); ~0.3 s of polling
+        for (int spin = 0; avail <= t && spin < (1 << 21); spin++) {
+            avail = (int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - X.base);   // sc1 poll
+            if (avail <= t) __builtin_amdgcn_s_sleep(2);
+        }
+        if (avail <= t) return;
+        if (!valid) continue;
+        const uint64_t* src = X.snap + ((size_t)t * X.ncore + core) * (SNAP_N / 2) * BLOCK + lane;
+        uint32_t v[SNAP_N];
+#pragma unroll
+        for (int j = 0; j < SNAP_N / 2; j++) {
+            const uint64_t x = __hip_atomic_load(src + j * BLOCK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1
+            v[2 * j] = (uint32_t)x;
+            v[2 * j + 1] = (uint32_t)(x >> 32);
+        }
+        ag_emit(part, v, (uint32_t)t, n, ue, C, out);
+    }
 }
 
 __device__ __forceinline__ void ag_spin(uint32_t* flag, uint32_t v) {
@@ -1232,7 +1388,7 @@ __device__ __forceinline__ void ag_spin(uint32_t* flag, uint32_t v) {
 }
 
 __global__ void __launch_bounds__(AG_WAVES * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2)))
-k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0, int autoreset, fjsp_out out) {
+k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0, int autoreset, fjsp_out out, AgEmit X) {
     // pre-draw work per step: the draw costs more than its loads' latency here (PD shares its
     // SIMD with E0), so four words per step (~33 steps for 30 orders) beat eight (measured)
     constexpr int CR = FJSP_PG_CR, PB = FJSP_AG_PB;
@@ -1249,9 +1405,11 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     __shared__ uint4 s_p1[2][2][BLOCK];   // AM post 1 (P1_*), by step parity
     __shared__ uint4 s_p2[BLOCK];         // AM post 2: W9..W12 (machine lists) after the machines' actions
     __shared__ uint4 s_res[2][4][BLOCK];  // P: step k+1's pickup + AGV results (RS_*), by step parity
-    __shared__ uint32_t s_kpost[2][BLOCK];      // K after step k: W1 (completed orders), final status
+    __shared__ uint32_t s_kpost[3][BLOCK];      // K after step k: W1 (completed orders) by step parity, final status
     __shared__ uint32_t s_flag1;   // AM posted step k's pickup / AGV words and machine lists (k + 1)
     __shared__ uint32_t s_uflag;   // E3 posted step k+1's pickup (k + 1)
+    __shared__ uint32_t s_kflag;   // K posted its completion count after step k (k + 1)
+    __shared__ uint32_t s_rflag;   // P posted step k+1's pickup / AGV results (k + 1)
     __shared__ uint4 s_pk[BLOCK];   // E3: W0, W4, W5, W7 after step k+1's pickup
     __shared__ uint2 s_pkr[BLOCK];  // E3: its result word, status bits
     __shared__ double s_lut[RLUT_SIZE];
@@ -1259,6 +1417,11 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     C.lut = s_lut;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / BLOCK);
     const int lane = threadIdx.x % BLOCK;
+    if (X.snap && (int)blockIdx.x >= X.ncore) {   // an emit workgroup
+        __syncthreads();   // s_lut
+        ag_emitter(X, (int)blockIdx.x - X.ncore, wave, lane, K, (uint32_t)S.n, C, out);
+        return;
+    }
     const int e = blockIdx.x * BLOCK + lane;
     const bool valid = e < S.n;
     const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
@@ -1290,7 +1453,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             s_act[j][1][lane] = pack_actions(act, 4);
         }
     }
-    if (threadIdx.x == 0) { s_flag1 = 0; s_uflag = 0; }
+    if (threadIdx.x == 0) { s_flag1 = 0; s_uflag = 0; s_kflag = 0; s_rflag = 0; }
     if (wave == AG_AM && valid) {
         // the env's order table and used slot prefix live in LDS for the launch (copied in before
         // the first barrier: K's first completions read them)
@@ -1326,19 +1489,29 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
 #ifdef FJSP_STAMPS
         const uint64_t loop_t0 = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef FJSP_AG_AMPRE
+        // a step's inputs (K's completion count, the actions, P's results), read at the end of the
+        // previous epoch once K and P posted them, so the step top starts on registers
+        uint32_t kc = 0, a0 = 0, a1 = 0, rs[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) rs[i] = 0u;
+        if (valid && K > 0) { a0 = s_act[0][0][lane]; a1 = s_act[0][1][lane]; }
+#endif
         for (int k = 0; k <= K; k++) {
             AG_T0();
             AG_MARK(0);
+#ifndef FJSP_AG_AMPRE
             // this step's inputs, read together: K's completion count, the actions, P's results
             uint32_t kc = 0, a0 = 0, a1 = 0, rs[16];
             if (valid) {
-                kc = s_kpost[0][lane];
+                kc = s_kpost[(k - 1) & 1][lane];
                 if (k < K) {
                     a0 = s_act[k % 3][0][lane];
                     a1 = s_act[k % 3][1][lane];
                     q_get(&s_res[k & 1][0][lane], 4, rs);
                 }
             }
+#endif
             if (valid) {
                 if (k > 0) {   // end of step k - 1: auto-reset once K has counted the completions
                     const int nord = E.norders();
@@ -1402,6 +1575,20 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 E.set_step(E.step() + 1);
                 fresh = false;
             }
+#ifdef FJSP_AG_AMPRE
+            if (k < K) {   // the next step's inputs
+                ag_spin(&s_kflag, (uint32_t)(k + 1));
+                if (k + 1 < K) ag_spin(&s_rflag, (uint32_t)(k + 1));
+                if (valid) {
+                    kc = s_kpost[k & 1][lane];
+                    if (k + 1 < K) {
+                        a0 = s_act[(k + 1) % 3][0][lane];
+                        a1 = s_act[(k + 1) % 3][1][lane];
+                        q_get(&s_res[(k + 1) & 1][0][lane], 4, rs);
+                    }
+                }
+            }
+#endif
             AG_ACC(ag_busy);
             AG_BARRIER();
         }
@@ -1415,7 +1602,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 S.snext[(size_t)q * S.n + e] = TL.snext[q * BLOCK];
                 S.scstep[(size_t)q * S.n + e] = TL.scstep[q * BLOCK];
             }
-            E.w[2] |= s_kpost[1][lane];
+            E.w[2] |= s_kpost[2][lane];
 #pragma unroll
             for (int i = 0; i < NSTATE; i++)
                 if (!((K_WORDS >> i) & 1u)) S.words[i * n + e] = E.w[i];
@@ -1488,7 +1675,8 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                     E.set_ncompleted(E.ncompleted() + orders_done);
                     if (E.p_queued(0) > 127 || E.p_queued(1) > 127 || E.p_queued(2) > 127 || E.p_queued(3) > 127)
                         E.flag(ST_OBS_OVERFLOW | ST_DIVERGED);
-                    s_kpost[0][lane] = E.w[1];
+                    s_kpost[k & 1][lane] = E.w[1];
+                    __hip_atomic_store(&s_kflag, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
                     for (int q = 0; q < 4; q++) r[q] = (r[q] & 0xFFu) | (((a1 >> (8 * q)) & 0xFFu) << 8);
                     const uint32_t v[16] = {E.w[1], E.w[20], E.w[21], E.w[22], E.w[23], E.w[26], E.w[27], E.w[28],
@@ -1500,7 +1688,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                     E.set_step(step + 1);
                 }
             } else if (valid) {
-                s_kpost[1][lane] = E.w[2];   // status bits for AM's final store of W2
+                s_kpost[2][lane] = E.w[2];   // status bits for AM's final store of W2
             }
             AG_ACC(ag_busy);
             AG_BARRIER();
@@ -1562,6 +1750,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                     const uint32_t rs[16] = {pk.x >> 24, pk.y, Ea.w[5], Ea.w[6], Ea.w[7], Ea.w[8], Ea.w[9],
                                              Ea.w[10], Ea.w[11], Ea.w[12], pr.x, r1, pr.y | Ea.w[2], 0u, 0u, pend};
                     q_put(&s_res[(k + 1) & 1][0][lane], 4, rs);
+                    __hip_atomic_store(&s_rflag, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 AG_MARK(5);
             }
@@ -1582,6 +1771,12 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
 #endif
         for (int k = 0; k <= K; k++) {
             AG_T0();
+            if (X.snap && part == 1 && k >= 2) {   // the publisher: steps < k-1 are stored (epochs < k)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0)
+                    __hip_atomic_store(X.count + (size_t)blockIdx.x * AG_COUNT_STRIDE, X.base + (uint32_t)(k - 1), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
             if (part == 3 && k + 1 < K) {   // step k+1's pickup station, from P's AGV result of step k
                 const bool fresh = ag_fresh(k, valid, s_p1, s_kpost, lane, C, autoreset);
                 if (__ballot(valid && fresh) != 0) ag_spin(&s_flag1, (uint32_t)(k + 1));
@@ -1606,6 +1801,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                     __hip_atomic_store(&s_uflag, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
+            AG_MARK(0);
             if (part == 0 && k + 2 < K) {   // E0 draws step k + 2's actions (uniform random)
                 int act[NA];
                 synth_uniform(seed, gid0 + (uint32_t)e, step0 + (uint32_t)(k + 2), act);
@@ -1623,51 +1819,28 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 const uint32_t t = (uint32_t)(k - 1);
                 uint32_t v[SNAP_N];
                 snap_get(snap[(k - 1) & 1], lane, v);
-                Env E;
+#ifdef FJSP_STAMPS
+                __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the snapshot arrived
+#endif
+                AG_MARK(1);
+                if (!X.snap) ag_emit(part, v, t, n, ue, C, out);
+                else if (part == 1) {   // the publisher: the step's snapshot to its global slot
+                    uint64_t* dst = X.snap + ((size_t)t * X.ncore + blockIdx.x) * (SNAP_N / 2) * BLOCK + lane;
 #pragma unroll
-                for (int i = 0; i < NSTATE; i++) E.w[i] = 0u;
-                E.w[0] = v[SA_W0]; E.w[2] = v[SA_ST] | v[SK_ST]; E.w[4] = v[SA_W4]; E.w[5] = v[SA_W5];
-                E.w[6] = v[SA_W6];
-#pragma unroll
-                for (int l = 0; l < 6; l++) E.w[7 + l] = v[SA_L0 + l];
-                E.w[17] = v[SA_M0]; E.w[18] = v[SA_M1];
-                E.w[1] = v[SK_W1];
-#pragma unroll
-                for (int s = 0; s < 4; s++) { E.w[20 + s] = v[SK_P0 + s]; E.w[26 + s] = v[SK_N0 + s]; }
-                const StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, t, n, ue};
-                if (part == 0) {
-                    if (out.rewards) {
-                        const uint32_t gs = v[SK_G];
-                        const double g8 = global_reward8(C, (int)(gs & 0xFFFFu), (int)(gs >> 16));
-                        const uint32_t rw[4] = {v[SA_R01], v[SA_R23], v[SK_R45], v[SK_R67]};
-#pragma unroll
-                        for (int a = 0; a < NA; a++) {
-                            const uint32_t r = (rw[a >> 1] >> (16 * (a & 1))) & 0xFFFFu;
-                            st32(out.rewards, (t * NA + (uint32_t)a) * n + ue,
-                                 g8 + C.lut[reward_index(a, r & 0xFFu, (int)((r >> 8) & 0xFu))]);
-                        }
-                    }
-                    FieldSink<0u, 0u, 0u, AG_MASKS_E0> ps{sink};
-                    observe(E, C, ps);
-                } else if (part == 1) {
-                    FieldSink<(1u << NI32) - 1u, 0u, (1u << NF32) - 1u, 0u> ps{sink};
-                    observe(E, C, ps);
-                } else if (part == 3) {
-                    FieldSink<0u, 0u, 0u, AG_MASKS_E3> ps{sink};
-                    observe(E, C, ps);
-                } else {
-                    FieldSink<0u, (1u << NI8) - 1u, 0u, AG_MASKS_E2> ps{sink};
-                    observe(E, C, ps);
-                    const int nord = E.norders();
-                    const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
-                    const int truncated = E.step() >= C.max_steps;
-                    if (out.term) st32(out.term, t * n + ue, (uint8_t)all_done);
-                    if (out.trunc) st32(out.trunc, t * n + ue, (uint8_t)truncated);
-                    if (out.status) st32(out.status, t * n + ue, E.status());
+                    for (int j = 0; j < SNAP_N / 2; j++)
+                        __hip_atomic_store(dst + j * BLOCK, (uint64_t)v[2 * j] | ((uint64_t)v[2 * j + 1] << 32),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1 (write-through)
                 }
             }
+            AG_MARK(2);
             AG_ACC(ag_busy);
             AG_BARRIER();
+        }
+        if (X.snap && part == 1) {   // all K steps stored
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0)
+                __hip_atomic_store(X.count + (size_t)blockIdx.x * AG_COUNT_STRIDE, X.base + (uint32_t)K, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 #ifdef FJSP_STAMPS
@@ -1690,6 +1863,8 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         }
         if (wave == AG_P)
             for (int i = 0; i < 6; i++) atomicAdd(&g_agstamps[33 + i], (unsigned long long)amt[i]);
+        if (wave == AG_E3 || wave == AG_E2)   // after the pickup post (E3), the snapshot, the stores
+            for (int i = 0; i < 4; i++) atomicAdd(&g_agstamps[(wave == AG_E3 ? 40 : 46) + i], (unsigned long long)amt[i]);
     }
 #endif
 }
@@ -1746,6 +1921,12 @@ struct fjsp_handle {
     int use_pipe;    // two-wave pipelined k_step_many for lean outputs (FJSP_PIPE / fjsp_set_option)
     int use_pg;      // pre-draw wave in the pipelined kernel (FJSP_PREDRAW / fjsp_set_option "predraw")
     int use_ag;      // agent-group pipeline k_step_ag for uniform-random actions (FJSP_AGENTS / "agents")
+    int use_emit_wg; // k_step_ag's outputs from emit workgroups of their own (FJSP_EMIT_WG / "emit_wg")
+    int num_cu;      // compute units of the device (emit workgroups need a CU per block)
+    uint64_t* ag_snap;      // k_step_ag snapshot slots (AgEmit::snap), grown on demand
+    size_t ag_snap_bytes;
+    uint32_t* ag_count;     // AgEmit::count, one 128-byte line per core workgroup
+    uint32_t ag_base;       // the largest count a launch can have left there
     const char* last_kernel;   // name of the last step kernel launched (fjsp_last_kernel)
 };
 
@@ -1867,6 +2048,14 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
         h->use_pg = pd ? atoi(pd) : 1;
         const char* ag = getenv("FJSP_AGENTS");
         h->use_ag = ag ? atoi(ag) : 1;
+        const char* ew = getenv("FJSP_EMIT_WG");
+        h->use_emit_wg = ew ? atoi(ew) : 0;   // measured slower at 4096 envs: opt-in
+        h->ag_snap = nullptr;
+        h->ag_snap_bytes = 0;
+        h->ag_count = nullptr;
+        h->ag_base = 0;
+        h->num_cu = 0;
+        if (hipDeviceGetAttribute(&h->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) h->num_cu = 0;
     }
     h->dcfg.step_size = c.step_size;
     h->dcfg.max_steps = c.max_episode_steps;
@@ -1902,6 +2091,10 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     if (e != hipSuccess) { (void)hipFree(h->base); delete h; return hip_fail("init", e); }
     e = hipMalloc(&h->lut_dev, sizeof(double) * RLUT_SIZE);
     if (e != hipSuccess) { (void)hipFree(h->base); delete h; return hip_fail("hipMalloc(reward table)", e); }
+    e = hipMalloc(&h->ag_count, (n + BLOCK - 1) / BLOCK * AG_COUNT_STRIDE * sizeof(uint32_t));
+    if (e == hipSuccess)
+        e = hipMemsetAsync(h->ag_count, 0, (n + BLOCK - 1) / BLOCK * AG_COUNT_STRIDE * sizeof(uint32_t), h->stream);
+    if (e != hipSuccess) { (void)hipFree(h->lut_dev); (void)hipFree(h->base); delete h; return hip_fail("hipMalloc(emit counts)", e); }
     h->dcfg.lut = h->lut_dev;
     {
         fjsp_reward_weights w;
@@ -1927,6 +2120,8 @@ int fjsp_destroy(fjsp_handle* h) {
     (void)hipEventDestroy(h->ev1);
     (void)hipFree(h->lut_dev);
     (void)hipFree(h->base);
+    (void)hipFree(h->ag_count);
+    if (h->ag_snap) (void)hipFree(h->ag_snap);
     delete h;
     return 0;
 }
@@ -1938,6 +2133,7 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
     if (!strcmp(name, "pipeline")) { h->use_pipe = value != 0; return 0; }
     if (!strcmp(name, "predraw")) { h->use_pg = value != 0; return 0; }
     if (!strcmp(name, "agents")) { h->use_ag = value != 0; return 0; }
+    if (!strcmp(name, "emit_wg")) { h->use_emit_wg = value != 0; return 0; }
     if (!strcmp(name, "timing")) { h->timing = value != 0; if (!h->timing) h->timed = 0; return 0; }
     return fail("unknown option");
 }
@@ -2031,7 +2227,38 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
     const bool pg = h->use_pg && lds && two_emit && autoreset;
     // the agent-group pipeline: state-independent (uniform-random) actions, LDS tables, pre-draw
     const bool ag = h->use_ag && h->use_pipe && !full && !staged && pg && action_mode == FJSP_ACTIONS_UNMASKED;
-    h->last_kernel = ag ? "k_step_ag<lds,predraw>"
+    // k_step_ag's emit workgroups: one more block per core block, each on a CU of its own
+    const int ncore = (int)grid.x;
+    bool ewg = ag && h->use_emit_wg && h->num_cu > 0 && 2 * ncore <= h->num_cu;
+    const size_t snap_bytes = (size_t)K * (size_t)ncore * (SNAP_N / 2) * BLOCK * sizeof(uint64_t);
+    if (ewg && snap_bytes > h->ag_snap_bytes) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIPCHK(hipStreamIsCapturing(h->stream, &cs));
+        if (cs != hipStreamCaptureStatusNone) {
+            ewg = false;   // no allocation while a graph is being captured: emit in the core
+        } else {
+            if (h->ag_snap) {
+                HIPCHK(hipStreamSynchronize(h->stream));
+                HIPCHK(hipFree(h->ag_snap));
+                h->ag_snap = nullptr;
+                h->ag_snap_bytes = 0;
+            }
+            HIPCHK(hipMalloc(&h->ag_snap, snap_bytes));
+            h->ag_snap_bytes = snap_bytes;
+        }
+    }
+    AgEmit X{nullptr, nullptr, ncore, 0u};
+    if (ewg) {
+        if ((uint64_t)h->ag_base + (uint64_t)K + 1 >= (1ull << 31)) {   // restart the counts (rare)
+            HIPCHK(hipMemsetAsync(h->ag_count, 0, (size_t)ncore * AG_COUNT_STRIDE * sizeof(uint32_t), h->stream));
+            h->ag_base = 0;
+        }
+        X.snap = h->ag_snap;
+        X.count = h->ag_count;
+        X.base = h->ag_base + 1u;
+        h->ag_base += (uint32_t)K + 1u;
+    }
+    h->last_kernel = ag ? (ewg ? "k_step_ag<lds,predraw,emit-wg>" : "k_step_ag<lds,predraw>")
                    : (h->use_pipe && !full && !staged)
                          ? (lds ? (two_emit ? (pg ? "k_step_pipe<lds,2emit,predraw>" : "k_step_pipe<lds,2emit>")
                                             : "k_step_pipe<lds,1emit>")
@@ -2040,8 +2267,8 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
                    : staged ? (lds ? "k_step_many<lds,staged>" : "k_step_many<staged>")
                    : (lds ? "k_step_many<lds>" : "k_step_many");
     if (ag) {
-        hipLaunchKernelGGL(k_step_ag, grid, dim3(AG_WAVES * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0,
-                           step0, autoreset, o);
+        hipLaunchKernelGGL(k_step_ag, dim3(ewg ? 2 * ncore : ncore), dim3(AG_WAVES * BLOCK), 0, h->stream, h->S, h->dcfg,
+                           K, action_seed, env_gid0, step0, autoreset, o, X);
     } else if (h->use_pipe && !full && !staged) {
         // a second emit wave pays while the CUs are not full (N <= 16384 at 64 envs per CU)
         const bool two = two_emit;
@@ -2109,8 +2336,8 @@ extern "C" int fjsp_debug_dump(uint32_t* out) {
 #endif
 extern "C" int fjsp_debug_agstamps(unsigned long long* out) {   // out[16]: k_step_ag per wave busy / wait, epochs
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_agstamps), sizeof(unsigned long long) * 40));
-    unsigned long long z[40] = {0};
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_agstamps), sizeof(unsigned long long) * 56));
+    unsigned long long z[56] = {0};
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_agstamps), z, sizeof(z)));
     return 0;
 }

@@ -6,7 +6,7 @@ import torch
 ve = importlib.import_module("multi-agent-rl-for-fjsp_amd.vec_env")
 K = 200
 for N in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4096").split(",")]:
-    env = ve.FJSPVecEnv(N)
+    env = ve.FJSPVecEnv(N, **({"max_episode_steps": int(os.environ["MAX_STEPS"])} if os.environ.get("MAX_STEPS") else {}))
     env.reset(seeds=torch.arange(N))
     b = ve.Buffers(K, N, env.device, infos=False)
     for f in [x for x in os.environ.get("NULL_OUTS", "").split(",") if x]:   # outputs not written
