@@ -743,16 +743,27 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
                 uint32_t v[PB];
                 int pa, cnt;
                 if (ASYNC && pf_pa == (pos & ~3)) {
+                    // the refill after this one first (a refill reads no word this one stores),
+                    // then this one on runs loaded a step ago
+                    const int pn = pf_pa + PB >= MT_N ? 0 : pf_pa + PB;
+                    uint4 pna[(PB + 4) / 4], pnc[(PB + 4) / 4];
+                    mt_load<PB>(work, pn, pna, pnc);
                     mt_batch_loaded<PB>(work, pos, g, v, pa, cnt, pfa, pfc);
+#pragma unroll
+                    for (int q = 0; q < (PB + 4) / 4; q++) { pfa[q] = pna[q]; pfc[q] = pnc[q]; }
+                    pf_pa = pn;
+                    pos += draw_orders<PB>(v, pos - pa, cnt, nord, d, s_nxt + lane, BLOCK);
+                    if (pos == MT_N) { pos = 0; g = 0; }
+                    if (d.o >= nord) { ph = 3; pf_pa = -1; }
                 } else {
                     mt_batch<PB>(work, pos, g, v, pa, cnt);
-                }
-                pos += draw_orders<PB>(v, pos - pa, cnt, nord, d, s_nxt + lane, BLOCK);
-                if (pos == MT_N) { pos = 0; g = 0; }
-                if (d.o >= nord) ph = 3;
-                if (ASYNC) {
-                    if (ph == 2) prefetch(work);
-                    else pf_pa = -1;
+                    pos += draw_orders<PB>(v, pos - pa, cnt, nord, d, s_nxt + lane, BLOCK);
+                    if (pos == MT_N) { pos = 0; g = 0; }
+                    if (d.o >= nord) ph = 3;
+                    if (ASYNC) {
+                        if (ph == 2) prefetch(work);
+                        else pf_pa = -1;
+                    }
                 }
             }
         };
@@ -1233,7 +1244,12 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
 // Waves w and w + 4 share a SIMD (two waves per SIMD issue VALU at twice one wave's rate): K
 // shares AM's (both busy early in the step; AM has the higher priority), P (the critical path
 // after AM's post, higher priority) shares the lightest emit wave's, PD and E3 pair up.
-constexpr int AG_AM = 0, AG_P = 1, AG_E1 = 2, AG_E2 = 3, AG_K = 4, AG_E0 = 5, AG_PD = 6, AG_E3 = 7, AG_WAVES = 8;
+#ifndef FJSP_AG_LAYOUT   // wave of each role: AM, P, E1, E2, K, E0, PD, E3 (waves w and w + 4 share a SIMD)
+#define FJSP_AG_LAYOUT 0, 1, 2, 3, 4, 5, 6, 7
+#endif
+constexpr int AG_LAYOUT[8] = {FJSP_AG_LAYOUT};
+constexpr int AG_AM = AG_LAYOUT[0], AG_P = AG_LAYOUT[1], AG_E1 = AG_LAYOUT[2], AG_E2 = AG_LAYOUT[3], AG_K = AG_LAYOUT[4],
+              AG_E0 = AG_LAYOUT[5], AG_PD = AG_LAYOUT[6], AG_E3 = AG_LAYOUT[7], AG_WAVES = 8;
 // packaging-owned state words (K): W1, W13..W16 (packaging run lists), W20..W29
 constexpr uint32_t K_WORDS = (1u << 1) | (0xFu << 13) | (0x3FFu << 20);
 // masks per emit wave: pickup [0,3) | the AGV's pickup / drop [9,11) | the AGV's moves [3,9),
