@@ -1470,30 +1470,53 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         }
     }
     if (threadIdx.x == 0) { s_flag1 = 0; s_uflag = 0; s_kflag = 0; s_rflag = 0; }
-    if (wave == AG_AM && valid) {
-        // the env's order table and used slot prefix live in LDS for the launch (copied in before
-        // the first barrier: K's first completions read them)
-        const uint32_t w0 = S.words[e], nslots = S.words[5 * n + e] >> 24;
-        for (uint32_t o = 0; o < ((w0 >> 16) & 0xFFu); o++) TL.orders[o * BLOCK] = S.orders[(size_t)o * S.n + e];
-        for (uint32_t q = 0; q < nslots; q++) {
-            TL.scode[q * BLOCK] = S.scode[(size_t)q * S.n + e];
-            TL.snext[q * BLOCK] = S.snext[(size_t)q * S.n + e];
-            TL.scstep[q * BLOCK] = S.scstep[(size_t)q * S.n + e];
+    if (valid) {
+        // the env's order table, used slot prefix and pre-drawn table live in LDS for the launch
+        // (copied in before the first barrier: K's first completions read them), copied by all
+        // eight waves, rows r = wave (mod 8), loads batched: a per-lane loop with an LDS store
+        // after each load waits out one HBM round trip per row (~30 µs per launch)
+        const uint32_t w0 = S.words[e], nslots = S.words[5 * n + e] >> 24, pg = S.words[(size_t)PGW * n + e];
+        const uint32_t no = (w0 >> 16) & 0xFFu, npd = (pg & 1u) ? (pg >> 24) & 0x7Fu : 0u;
+        uint32_t ov[MAX_ORDERS / AG_WAVES], pv[MAX_ORDERS / AG_WAVES];
+#pragma unroll
+        for (int j = 0; j < MAX_ORDERS / AG_WAVES; j++) {
+            const uint32_t o = (uint32_t)(wave + AG_WAVES * j);
+            ov[j] = o < no ? S.orders[(size_t)o * n + e] : 0u;
+            pv[j] = o < npd ? S.nxt[(size_t)o * n + e] : 0u;
         }
-        s_mb[0][0][lane] = ((w0 >> 16) & 0xFFu) << 8;   // episode counter 0 | num_orders
-        s_mb[1][0][lane] = S.words[3 * n + e];
-    }
-    if (wave == AG_PD && valid) {
-        const uint32_t pg = S.words[(size_t)PGW * n + e];
-        uint32_t r = 0, c = 0;
-        if (pg & 1u) {   // a table finished in an earlier launch
-            const int no = (int)((pg >> 24) & 0x7Fu);
-            for (int o = 0; o < no; o++) s_nxt[o * BLOCK + lane] = S.nxt[(size_t)o * n + e];
-            r = 1u | ((uint32_t)no << 9);
-            c = ((pg >> 1) & 0x3FFu) | (((pg >> 11) & 0x3FFu) << 16) | (((pg >> 21) & 1u) << 31);
+#pragma unroll
+        for (int j = 0; j < MAX_ORDERS / AG_WAVES; j++) {
+            const uint32_t o = (uint32_t)(wave + AG_WAVES * j);
+            if (o < no) TL.orders[o * BLOCK] = ov[j];
+            if (o < npd) s_nxt[o * BLOCK + lane] = pv[j];
         }
-        s_mb[2][0][lane] = r;
-        s_mb[3][0][lane] = c;
+        for (uint32_t q0 = (uint32_t)wave; q0 < nslots; q0 += 4 * AG_WAVES) {
+            uint32_t cv[4], xv[4], tv[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t q = q0 + (uint32_t)(AG_WAVES * j);
+                cv[j] = q < nslots ? S.scode[(size_t)q * n + e] : 0u;
+                xv[j] = q < nslots ? S.snext[(size_t)q * n + e] : 0u;
+                tv[j] = q < nslots ? S.scstep[(size_t)q * n + e] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t q = q0 + (uint32_t)(AG_WAVES * j);
+                if (q < nslots) {
+                    TL.scode[q * BLOCK] = (uint16_t)cv[j];
+                    TL.snext[q * BLOCK] = (uint8_t)xv[j];
+                    TL.scstep[q * BLOCK] = (uint16_t)tv[j];
+                }
+            }
+        }
+        if (wave == AG_AM) {
+            s_mb[0][0][lane] = no << 8;   // episode counter 0 | num_orders
+            s_mb[1][0][lane] = S.words[3 * n + e];
+        }
+        if (wave == AG_PD) {   // a table finished in an earlier launch
+            s_mb[2][0][lane] = (pg & 1u) ? 1u | (npd << 9) : 0u;
+            s_mb[3][0][lane] = (pg & 1u) ? ((pg >> 1) & 0x3FFu) | (((pg >> 11) & 0x3FFu) << 16) | (((pg >> 21) & 1u) << 31) : 0u;
+        }
     }
     __syncthreads();
     if (wave == AG_AM) {
@@ -1612,12 +1635,8 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         if (lane == 0) atomicAdd(&g_agstamps[24], (unsigned long long)(__builtin_amdgcn_s_memtime() - loop_t0));
 #endif
         if (valid) {
-            for (int o = 0; o < E.norders(); o++) S.orders[(size_t)o * S.n + e] = TL.orders[o * BLOCK];
-            for (int q = 0; q < E.slot_next(); q++) {
-                S.scode[(size_t)q * S.n + e] = TL.scode[q * BLOCK];
-                S.snext[(size_t)q * S.n + e] = TL.snext[q * BLOCK];
-                S.scstep[(size_t)q * S.n + e] = TL.scstep[q * BLOCK];
-            }
+            s_act[0][0][lane] = (uint32_t)E.norders();   // for the copy-out by all waves below
+            s_act[0][1][lane] = (uint32_t)E.slot_next();
             E.w[2] |= s_kpost[2][lane];
 #pragma unroll
             for (int i = 0; i < NSTATE; i++)
@@ -1857,6 +1876,16 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             if (lane == 0)
                 __hip_atomic_store(X.count + (size_t)blockIdx.x * AG_COUNT_STRIDE, X.base + (uint32_t)K, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    if (valid) {   // the order table and the used slot prefix back to HBM, rows r = wave (mod 8)
+        const uint32_t no = s_act[0][0][lane], ns = s_act[0][1][lane];
+        for (uint32_t o = (uint32_t)wave; o < no; o += AG_WAVES) S.orders[(size_t)o * n + e] = TL.orders[o * BLOCK];
+        for (uint32_t q = (uint32_t)wave; q < ns; q += AG_WAVES) {
+            S.scode[(size_t)q * n + e] = TL.scode[q * BLOCK];
+            S.snext[(size_t)q * n + e] = TL.snext[q * BLOCK];
+            S.scstep[(size_t)q * n + e] = TL.scstep[q * BLOCK];
         }
     }
 #ifdef FJSP_STAMPS

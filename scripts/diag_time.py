@@ -4,7 +4,7 @@ import importlib, json, sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 ve = importlib.import_module("multi-agent-rl-for-fjsp_amd.vec_env")
-K = 200
+K = int(os.environ.get("K", "200"))
 for N in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4096").split(",")]:
     env = ve.FJSPVecEnv(N, **({"max_episode_steps": int(os.environ["MAX_STEPS"])} if os.environ.get("MAX_STEPS") else {}))
     env.reset(seeds=torch.arange(N))
