@@ -42,7 +42,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=None, help="default 2000 (step) / 4 A2C batches (a2c)")
     ap.add_argument("--warmup", type=int, default=None, help="default 200 (step) / 1 A2C batch (a2c)")
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
-    ap.add_argument("--chunk", type=int, default=200, help="env steps per fused launch")
+    ap.add_argument("--chunk", type=int, default=1000,
+                    help="env steps per fused launch (also timed at 200 per launch: chunk_200 in the JSON)")
+    ap.add_argument("--no-chunk-compare", action="store_true", help="skip the 200-step-launch comparison")
     ap.add_argument("--num-orders", type=int, default=30)
     ap.add_argument("--masked", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -202,7 +204,7 @@ def main():
     buf = vec_env.Buffers(chunk, N, dev, infos=False)
     stream = torch.cuda.current_stream(dev)
 
-    def run(nsteps, step0, timing=None):
+    def run(nsteps, step0, timing=None, chunk=chunk, buf=buf):
         done = 0
         while done < nsteps:
             k = min(chunk, nsteps - done)
@@ -242,6 +244,21 @@ def main():
     total_env_steps = args.steps * N * world
     value = total_env_steps / elapsed
     achieved = ALGO_BYTES_FUSED * N * steps_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    # the same workload in 200-step launches (r01's first headline configuration), rank-local
+    chunk_200 = None
+    if chunk != 200 and args.steps >= 200 and not args.no_chunk_compare:
+        buf200 = vec_env.Buffers(200, N, dev, infos=False)
+        s1 = run(200, s0 + args.steps, chunk=200, buf=buf200)
+        torch.cuda.synchronize()
+        t200 = []
+        tc = time.perf_counter()
+        run(args.steps, s1, t200, chunk=200, buf=buf200)
+        torch.cuda.synchronize()
+        el200 = time.perf_counter() - tc
+        ms200 = float(np.mean([a.elapsed_time(b) for a, b, _ in t200]))
+        chunk_200 = {"value": args.steps * N / el200, "unit": "env-steps/s", "steps_per_launch": 200,
+                     "avg_launch_ms": ms200, "note": "rank-local, same workload in 200-step launches"}
+        del buf200
 
     # one-launch-per-step mode (actions resident in HBM, k_step): the RL-loop path
     per_step = None
@@ -346,6 +363,7 @@ def main():
                          "algo_bytes_per_env_step": ALGO_BYTES_FUSED,
                          "env_steps_per_launch": N * steps_per_launch},
             "cpu_baseline": cpu,
+            "chunk_200": chunk_200,
             "per_step_launch": per_step,
             "a2c_training": a2c,
             "scale_16x_envs": scale,

@@ -2,7 +2,7 @@
 evidence under profiles/: copies of the stats / trace / counter CSVs for round ROUND, the
 per-launch HBM traffic JSON bench.py reads (profiles/pmc_<workload>.json) and a short summary.
 
-usage: python scripts/summarize_profiles.py r01 [--envs 4096] [--steps-per-launch 200]
+usage: python scripts/summarize_profiles.py r01 [--envs 4096] [--steps-per-launch 1000]
 
 HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3 section): FETCH_SIZE
 and WRITE_SIZE are kB; FETCH_SIZE counts half of a wide streaming read on gfx950, so reads are
@@ -31,7 +31,7 @@ def main():
     ap.add_argument("round")
     ap.add_argument("--src", default=os.path.join(REPO, "gpurun_out", "prof"))
     ap.add_argument("--envs", type=int, default=4096)
-    ap.add_argument("--steps-per-launch", type=int, default=200)
+    ap.add_argument("--steps-per-launch", type=int, default=1000)
     ap.add_argument("--kernel", default="k_step_ag")
     ap.add_argument("--variant", default="k_step_ag<lds,predraw>", help="fjsp_last_kernel name of the profiled launch")
     ap.add_argument("--algo-bytes-per-env-step", type=int, default=211)
