@@ -195,3 +195,18 @@ def test_agents_emit_in_core_beyond_one_cu_per_block(G):
             assert env.last_kernel() == AG
     for k in LEAN:
         assert P.bits_equal(runs[0][k], runs[1][k]), k
+
+
+@pytest.mark.parametrize("n", [250, 1001])
+def test_agents_byte_rows_not_quad_aligned(G, n):
+    """Env counts that are not a multiple of 4 or of the 64-env workgroup (byte rows at odd
+    offsets, a partial last workgroup): k_step_ag == k_step_pipe."""
+    runs = []
+    for agents in (1, 0):
+        env = _env(G, n, agents)
+        env.reset(seeds=torch.arange(n) + 9, num_orders=4)
+        runs.append(_chunks(G, env, [70, 1, 60], seed=8))
+        if agents:
+            assert env.last_kernel() == AG
+    for k in LEAN:
+        assert P.bits_equal(runs[0][k], runs[1][k]), k
