@@ -1424,8 +1424,6 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     __shared__ uint32_t s_kpost[3][BLOCK];      // K after step k: W1 (completed orders) by step parity, final status
     __shared__ uint32_t s_flag1;   // AM posted step k's pickup / AGV words and machine lists (k + 1)
     __shared__ uint32_t s_uflag;   // E3 posted step k+1's pickup (k + 1)
-    __shared__ uint32_t s_kflag;   // K posted its completion count after step k (k + 1)
-    __shared__ uint32_t s_rflag;   // P posted step k+1's pickup / AGV results (k + 1)
     __shared__ uint4 s_pk[BLOCK];   // E3: W0, W4, W5, W7 after step k+1's pickup
     __shared__ uint2 s_pkr[BLOCK];  // E3: its result word, status bits
     __shared__ double s_lut[RLUT_SIZE];
@@ -1469,7 +1467,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             s_act[j][1][lane] = pack_actions(act, 4);
         }
     }
-    if (threadIdx.x == 0) { s_flag1 = 0; s_uflag = 0; s_kflag = 0; s_rflag = 0; }
+    if (threadIdx.x == 0) { s_flag1 = 0; s_uflag = 0; }
     if (valid) {
         // the env's order table, used slot prefix and pre-drawn table live in LDS for the launch
         // (copied in before the first barrier: K's first completions read them), copied by all
@@ -1528,18 +1526,9 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
 #ifdef FJSP_STAMPS
         const uint64_t loop_t0 = __builtin_amdgcn_s_memtime();
 #endif
-#ifdef FJSP_AG_AMPRE
-        // a step's inputs (K's completion count, the actions, P's results), read at the end of the
-        // previous epoch once K and P posted them, so the step top starts on registers
-        uint32_t kc = 0, a0 = 0, a1 = 0, rs[16];
-#pragma unroll
-        for (int i = 0; i < 16; i++) rs[i] = 0u;
-        if (valid && K > 0) { a0 = s_act[0][0][lane]; a1 = s_act[0][1][lane]; }
-#endif
         for (int k = 0; k <= K; k++) {
             AG_T0();
             AG_MARK(0);
-#ifndef FJSP_AG_AMPRE
             // this step's inputs, read together: K's completion count, the actions, P's results
             uint32_t kc = 0, a0 = 0, a1 = 0, rs[16];
             if (valid) {
@@ -1550,7 +1539,6 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                     q_get(&s_res[k & 1][0][lane], 4, rs);
                 }
             }
-#endif
             if (valid) {
                 if (k > 0) {   // end of step k - 1: auto-reset once K has counted the completions
                     const int nord = E.norders();
@@ -1614,20 +1602,6 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 E.set_step(E.step() + 1);
                 fresh = false;
             }
-#ifdef FJSP_AG_AMPRE
-            if (k < K) {   // the next step's inputs
-                ag_spin(&s_kflag, (uint32_t)(k + 1));
-                if (k + 1 < K) ag_spin(&s_rflag, (uint32_t)(k + 1));
-                if (valid) {
-                    kc = s_kpost[k & 1][lane];
-                    if (k + 1 < K) {
-                        a0 = s_act[(k + 1) % 3][0][lane];
-                        a1 = s_act[(k + 1) % 3][1][lane];
-                        q_get(&s_res[(k + 1) & 1][0][lane], 4, rs);
-                    }
-                }
-            }
-#endif
             AG_ACC(ag_busy);
             AG_BARRIER();
         }
@@ -1711,7 +1685,6 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                     if (E.p_queued(0) > 127 || E.p_queued(1) > 127 || E.p_queued(2) > 127 || E.p_queued(3) > 127)
                         E.flag(ST_OBS_OVERFLOW | ST_DIVERGED);
                     s_kpost[k & 1][lane] = E.w[1];
-                    __hip_atomic_store(&s_kflag, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
                     for (int q = 0; q < 4; q++) r[q] = (r[q] & 0xFFu) | (((a1 >> (8 * q)) & 0xFFu) << 8);
                     const uint32_t v[16] = {E.w[1], E.w[20], E.w[21], E.w[22], E.w[23], E.w[26], E.w[27], E.w[28],
@@ -1785,7 +1758,6 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                     const uint32_t rs[16] = {pk.x >> 24, pk.y, Ea.w[5], Ea.w[6], Ea.w[7], Ea.w[8], Ea.w[9],
                                              Ea.w[10], Ea.w[11], Ea.w[12], pr.x, r1, pr.y | Ea.w[2], 0u, 0u, pend};
                     q_put(&s_res[(k + 1) & 1][0][lane], 4, rs);
-                    __hip_atomic_store(&s_rflag, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 AG_MARK(5);
             }
