@@ -666,7 +666,11 @@ FJSP_DEV void agv_pack_drop(Env& E, const Tables& T, const Cfg& C, uint32_t pend
 
 // MachineAgent.execute_action (MachineAgent.py:99-139); grant happens in the run.
 template <int M>
-FJSP_DEV uint32_t machine_execute(Env& E, const Tables& T, int action, int* start_slot) {
+// next_known >= 0: the queue front's successor, known without reading the table (k_step_ag's
+// AM reads it before the AGV's drop: the drop only appends, so a front with a successor keeps
+// it, a lone front gets the dropped tray, now the tail, and an empty queue's dropped tray is
+// alone); -1: read it.
+FJSP_DEV uint32_t machine_execute(Env& E, const Tables& T, int action, int* start_slot, int next_known = -1) {
     constexpr int LQ = M == 0 ? L_M0Q : L_M1Q;
     constexpr int LR = M == 0 ? L_M0R : L_M1R;
     const bool busy = E.m_busy(M);
@@ -674,7 +678,15 @@ FJSP_DEV uint32_t machine_execute(Env& E, const Tables& T, int action, int* star
     const int cur = E.m_cur(M);
     const bool go = action == 1 && idle_q;            // START: pop the queue front
     const bool sig = action == 2 && !busy && cur != NIL;   // SIGNAL: current tray -> ready_trays
-    if (go) *start_slot = list_pop<LQ>(E, T);
+    if (go) {
+        if (next_known < 0) {
+            *start_slot = list_pop<LQ>(E, T);
+        } else {
+            const int h = E.lh(LQ), n = E.ll(LQ) - 1;
+            E.set_list(LQ, n == 0 ? NIL : next_known, n == 0 ? NIL : E.lt(LQ), n);
+            *start_slot = h;
+        }
+    }
     if (sig) {
         list_push<LR>(E, T, cur);
         E.set_m_cur(M, NIL);

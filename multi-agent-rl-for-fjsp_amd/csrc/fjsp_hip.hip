@@ -1529,6 +1529,16 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         for (int k = 0; k <= K; k++) {
             AG_T0();
             AG_MARK(0);
+            // the machine queues' front successors as P's AGV of step k saw the queues (AM's own
+            // lists: the run phase leaves them alone), read with this step's inputs: the START
+            // pops then need no table read after the AGV's drop (machine_execute)
+            int pl0 = 0, pl1 = 0, pn0 = NIL, pn1 = NIL;
+            if (valid && k < K) {
+                pl0 = E.ll(L_M0Q);
+                pl1 = E.ll(L_M1Q);
+                if (pl0 >= 2) pn0 = TL.snext[E.lh(L_M0Q) * BLOCK];
+                if (pl1 >= 2) pn1 = TL.snext[E.lh(L_M1Q) * BLOCK];
+            }
             // this step's inputs, read together: K's completion count, the actions, P's results
             uint32_t kc = 0, a0 = 0, a1 = 0, rs[16];
             if (valid) {
@@ -1578,8 +1588,10 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 }
                 AG_MARK(2);
                 int s0 = -1, s1 = -1;
-                const uint32_t r2 = (machine_execute<0>(E, TL, act[2], &s0) & 0xFFu) | ((uint32_t)act[2] << 8);
-                const uint32_t r3 = (machine_execute<1>(E, TL, act[3], &s1) & 0xFFu) | ((uint32_t)act[3] << 8);
+                const int nk0 = fresh ? -1 : pl0 >= 2 ? pn0 : E.lt(L_M0Q);
+                const int nk1 = fresh ? -1 : pl1 >= 2 ? pn1 : E.lt(L_M1Q);
+                const uint32_t r2 = (machine_execute<0>(E, TL, act[2], &s0, nk0) & 0xFFu) | ((uint32_t)act[2] << 8);
+                const uint32_t r3 = (machine_execute<1>(E, TL, act[3], &s1, nk1) & 0xFFu) | ((uint32_t)act[3] << 8);
                 AG_MARK(3);
                 {   // the post: pickup / AGV words (P1_*), machine lists
                     const uint32_t p1[8] = {E.w[0], E.w[4], E.w[5], E.w[6], E.w[7], E.w[8], pend, 0u};
