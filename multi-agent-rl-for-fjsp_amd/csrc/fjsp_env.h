@@ -600,9 +600,9 @@ FJSP_DEV uint32_t agv_fin(Env& E, const Tables& T, const AgvPre& a, int* move_to
         next = T.snext[ps * T.stride];
         scode = T.scode[ps * T.stride];
         ow = T.orders[tc_order((int)scode) * T.stride];
-    } else if (ok6 && a.pre_len == 1 && len >= 2) {   // the single front got a successor
-        next = T.snext[ps * T.stride];
-    }
+    } else if (ok6 && a.pre_len == 1 && len >= 2) {   // the single front got a successor: the
+        next = (lws >> 8) & 0xFFu;                      // tray pushed since (one push per list per
+    }                                                   // step: pickup, a machine's SIGNAL), the tail
     const int carry = a.carry;
     const bool push = a.ok7 && a.dst >= 0;
     const uint32_t lwd = lword<DROP_LISTS>(E, a.dst);
