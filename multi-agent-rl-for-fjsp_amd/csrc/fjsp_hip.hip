@@ -1257,8 +1257,19 @@ constexpr uint32_t K_WORDS = (1u << 1) | (0xFu << 13) | (0x3FFu << 20);
 #ifndef FJSP_AG_E1MASKS
 #define FJSP_AG_E1MASKS 0u
 #endif
-constexpr uint32_t AG_MASKS_E0 = 0x7u, AG_MASKS_E2 = 0x3u << 9, AG_MASKS_E1 = FJSP_AG_E1MASKS,
-                   AG_MASKS_E3 = ((0x3Fu << 3) | (0x3FFFFu << 11)) & ~AG_MASKS_E1;
+#ifndef FJSP_AG_E0MASKS   // masks E0 takes over from E3
+#define FJSP_AG_E0MASKS 0u
+#endif
+#ifndef FJSP_AG_E0I8      // int8 fields E0 takes over from E2
+#define FJSP_AG_E0I8 0u
+#endif
+#ifndef FJSP_AG_E1I8      // int8 fields E1 takes over from E2
+#define FJSP_AG_E1I8 0u
+#endif
+constexpr uint32_t AG_MASKS_E0 = 0x7u | FJSP_AG_E0MASKS, AG_MASKS_E2 = 0x3u << 9, AG_MASKS_E1 = FJSP_AG_E1MASKS,
+                   AG_MASKS_E3 = ((0x3Fu << 3) | (0x3FFFFu << 11)) & ~AG_MASKS_E1 & ~AG_MASKS_E0;
+constexpr uint32_t AG_I8_E0 = FJSP_AG_E0I8, AG_I8_E1 = FJSP_AG_E1I8, AG_I8_E2 = ((1u << NI8) - 1u) & ~AG_I8_E0 & ~AG_I8_E1;
+static_assert(!(AG_I8_E0 & AG_I8_E1), "int8 split");
 static_assert((AG_MASKS_E0 | AG_MASKS_E1 | AG_MASKS_E2 | AG_MASKS_E3) == (1u << NMASK) - 1u &&
               !(AG_MASKS_E0 & AG_MASKS_E2) && !(AG_MASKS_E0 & AG_MASKS_E3) && !(AG_MASKS_E2 & AG_MASKS_E3) &&
               !(AG_MASKS_E1 & (AG_MASKS_E0 | AG_MASKS_E2)), "mask split");
@@ -1329,16 +1340,16 @@ __device__ __forceinline__ void ag_emit(int part, const uint32_t* v, uint32_t t,
                      g8 + C.lut[reward_index(a, r & 0xFFu, (int)((r >> 8) & 0xFu))]);
             }
         }
-        FieldSink<0u, 0u, 0u, AG_MASKS_E0> ps{sink};
+        FieldSink<0u, AG_I8_E0, 0u, AG_MASKS_E0> ps{sink};
         observe(E, C, ps);
     } else if (part == 1) {
-        FieldSink<(1u << NI32) - 1u, 0u, (1u << NF32) - 1u, AG_MASKS_E1> ps{sink};
+        FieldSink<(1u << NI32) - 1u, AG_I8_E1, (1u << NF32) - 1u, AG_MASKS_E1> ps{sink};
         observe(E, C, ps);
     } else if (part == 3) {
         FieldSink<0u, 0u, 0u, AG_MASKS_E3> ps{sink};
         observe(E, C, ps);
     } else {
-        FieldSink<0u, (1u << NI8) - 1u, 0u, AG_MASKS_E2> ps{sink};
+        FieldSink<0u, AG_I8_E2, 0u, AG_MASKS_E2> ps{sink};
         observe(E, C, ps);
         const int nord = E.norders();
         const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
