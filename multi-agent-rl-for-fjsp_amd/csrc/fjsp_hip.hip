@@ -517,6 +517,39 @@ __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t
     env_store(E, S.words, S.n, e);
 }
 
+// The env's order table and used tray-slot prefix into LDS tables (one lane per env): the
+// loads of eight rows are issued together and waited for once (a load-then-store loop per row
+// waits out one HBM round trip per row, ~30 us per launch at 30 orders and a few dozen slots).
+__device__ __forceinline__ void tables_copy_in(const DevState& S, const Tables& T, int e, int norders, int nslots) {
+    const size_t n = (size_t)S.n;
+    for (int o0 = 0; o0 < norders; o0 += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = o0 + j < norders ? S.orders[(size_t)(o0 + j) * n + e] : 0u;
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (o0 + j < norders) T.orders[(o0 + j) * T.stride] = v[j];
+    }
+    for (int q0 = 0; q0 < nslots; q0 += 8) {
+        uint32_t c[8], x[8], t[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const bool in = q0 + j < nslots;
+            const size_t i = (size_t)(q0 + j) * n + e;
+            c[j] = in ? S.scode[i] : 0u;
+            x[j] = in ? S.snext[i] : 0u;
+            t[j] = in ? S.scstep[i] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (q0 + j < nslots) {
+                T.scode[(q0 + j) * T.stride] = (uint16_t)c[j];
+                T.snext[(q0 + j) * T.stride] = (uint8_t)x[j];
+                T.scstep[(q0 + j) * T.stride] = (uint16_t)t[j];
+            }
+    }
+}
+
 // K fused steps.  LDS = true stages the env's order table and tray-slot arena in LDS for
 // the whole launch (one 64-lane workgroup = 64 envs, 97.5 KB of LDS), so the linked-list
 // walks and order-word read-modify-writes of the step are ds_* round trips (~100 cycles)
@@ -546,12 +579,7 @@ __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, u
         T.snext = s_next + lane;
         T.scstep = s_cstep + lane;
         T.stride = BLOCK;
-        for (int o = 0; o < E.norders(); o++) T.orders[o * BLOCK] = S.orders[(size_t)o * S.n + e];
-        for (int s = 0; s < E.slot_next(); s++) {
-            T.scode[s * BLOCK] = S.scode[(size_t)s * S.n + e];
-            T.snext[s * BLOCK] = S.snext[(size_t)s * S.n + e];
-            T.scstep[s * BLOCK] = S.scstep[(size_t)s * S.n + e];
-        }
+        tables_copy_in(S, T, e, E.norders(), E.slot_next());
     } else {
         T = tables_of(S, e);
     }
@@ -964,14 +992,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
             T.snext = s_next + lane;
             T.scstep = s_cstep + lane;
             T.stride = BLOCK;
-            if (valid) {
-                for (int o = 0; o < E.norders(); o++) T.orders[o * BLOCK] = S.orders[(size_t)o * S.n + e];
-                for (int q = 0; q < E.slot_next(); q++) {
-                    T.scode[q * BLOCK] = S.scode[(size_t)q * S.n + e];
-                    T.snext[q * BLOCK] = S.snext[(size_t)q * S.n + e];
-                    T.scstep[q * BLOCK] = S.scstep[(size_t)q * S.n + e];
-                }
-            }
+            if (valid) tables_copy_in(S, T, e, E.norders(), E.slot_next());
         }
 #ifdef FJSP_STAMPS
         for (int i = 0; i < 8; i++) E.st_acc[i] = 0;
