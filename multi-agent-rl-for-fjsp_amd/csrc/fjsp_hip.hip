@@ -697,8 +697,9 @@ __device__ __forceinline__ uint32_t pack_actions(const int* act, int lo) {
 // s_mb / s_cp / s_nxt are the kernel's LDS mailboxes, row-copy staging and next tables.
 // FINAL_MB: the sim side also posts in the final epoch K (k_step_ag resets at the top of an
 // epoch), so a table it consumed or abandoned there must not be stored as ready.
-// ASYNC: a row DMA issued in step k is waited for and stored in step k + 1 (its latency hides
-// behind the barrier instead of the step); s_cp holds two sets of CR rows.
+// ASYNC (k_step_ag): a row loaded in step k is held in registers and stored in step k + 1, and
+// each MT refill is loaded a step ahead: their latency hides behind the barrier instead of
+// the step (plain loads; an LDS DMA would be drained by the barrier's fence).  s_cp unused.
 template <int CR, int PB, bool FINAL_MB = false, bool ASYNC = false>
 __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane, int e, bool valid,
                                              uint32_t (*s_mb)[2][BLOCK], uint4 (*s_cp)[3][BLOCK], uint32_t* s_nxt) {
@@ -1443,7 +1444,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     __shared__ uint32_t s_orders[MAX_ORDERS * BLOCK];
     __shared__ uint32_t s_nxt[MAX_ORDERS * BLOCK];
     __shared__ uint32_t s_mb[4][2][BLOCK];   // AM <-> PD mailboxes (predraw_wave)
-    __shared__ uint4 s_cp[2 * CR][3][BLOCK];   // two steps of row DMAs in flight (predraw_wave<ASYNC>)
+    __shared__ uint4 s_cp[1][3][BLOCK];   // unused by predraw_wave<ASYNC> (rows travel in registers)
     __shared__ uint16_t s_code[MAX_SLOTS * BLOCK];
     __shared__ uint8_t s_next[MAX_SLOTS * BLOCK];
     __shared__ uint16_t s_cstep[MAX_SLOTS * BLOCK];
