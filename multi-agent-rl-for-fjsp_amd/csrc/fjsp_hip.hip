@@ -1266,8 +1266,9 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
 // Waves w and w + 4 share a SIMD (two waves per SIMD issue VALU at twice one wave's rate): K
 // shares AM's (both busy early in the step; AM has the higher priority), P (the critical path
 // after AM's post, higher priority) shares the lightest emit wave's, PD and E3 pair up.
-#ifndef FJSP_AG_LAYOUT   // wave of each role: AM, P, E1, E2, K, E0, PD, E3 (waves w and w + 4 share a SIMD)
-#define FJSP_AG_LAYOUT 0, 1, 2, 3, 4, 5, 6, 7
+#ifndef FJSP_AG_LAYOUT   // wave of each role: AM, P, E1, E2, K, E0, PD, E3 (waves w and w + 4 share a SIMD):
+                         // AM+PD, P+E0, E1+K, E2+E3 (0.6 % faster than AM+K, E1+PD: scripts/gpu_variants.sh)
+#define FJSP_AG_LAYOUT 0, 1, 2, 3, 6, 5, 4, 7
 #endif
 constexpr int AG_LAYOUT[8] = {FJSP_AG_LAYOUT};
 constexpr int AG_AM = AG_LAYOUT[0], AG_P = AG_LAYOUT[1], AG_E1 = AG_LAYOUT[2], AG_E2 = AG_LAYOUT[3], AG_K = AG_LAYOUT[4],
