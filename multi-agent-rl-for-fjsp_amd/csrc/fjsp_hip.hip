@@ -1597,8 +1597,6 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                         epi = (epi + 1) & 0xFF;
                     }
                 }
-                s_mb[0][(k + 1) & 1][lane] = (uint32_t)epi | ((uint32_t)E.norders() << 8);
-                s_mb[1][(k + 1) & 1][lane] = E.w[3];
             }
             AG_MARK(1);
             if (k < K && valid) {
@@ -1647,6 +1645,10 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 trunc_prev = E.step() >= C.max_steps;
                 E.set_step(E.step() + 1);
                 fresh = false;
+            }
+            if (valid) {   // PD's mailbox for the next step (off the way to the post: its release waits for them)
+                s_mb[0][(k + 1) & 1][lane] = (uint32_t)epi | ((uint32_t)E.norders() << 8);
+                s_mb[1][(k + 1) & 1][lane] = E.w[3];
             }
             AG_ACC(ag_busy);
             AG_BARRIER();
