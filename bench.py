@@ -5,10 +5,12 @@ Workload (BASELINE.json configs[2], the metric's "4096 parallel envs on 1 MI355X
 reference environments per GPU (num_orders=30, default CONFIG), synthetic uniformly random
 actions (action_space.sample() semantics) from the on-device counter RNG, auto-reset on
 truncation/termination (MT19937 stream continued like reset(seed=None)).  One bench "step" =
-one FJSPSimulation.step() of every env on this GPU; obs (reference dtypes), fp64 rewards,
-term and trunc of every step are written to an HBM trajectory slab.  Steps are executed by
-the fused step kernel (k_step_pipe: two-wave pipelined, LDS tables) in launches of --chunk
-steps; the variant launched is reported in config.kernel.
+one rollout batch: --batch-steps (default 256, the reference's A2C batch / rollout horizon,
+train.py:59 --batch_size 256) consecutive FJSPSimulation.step() calls of every env on this GPU,
+i.e. 256 x 4096 env-steps; obs (reference dtypes), fp64 rewards, term and trunc of every
+env-step are written to an HBM trajectory slab.  The env-steps of the timed region are
+executed by the fused step kernel in launches of --chunk env-steps; the variant launched is
+reported in config.kernel.  value = env-steps per second (BASELINE.json's metric).
 
 Multi-GPU (torchrun): one process per GPU, envs sharded by global id (rank * envs + e) with
 no data-path collective ("scaling": "weak"); the only collectives are the barrier and the
@@ -39,16 +41,19 @@ HBM_PEAK_GBS = 8000.0                     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="default 2000 (step) / 4 A2C batches (a2c)")
-    ap.add_argument("--warmup", type=int, default=None, help="default 200 (step) / 1 A2C batch (a2c)")
+    ap.add_argument("--steps", type=int, default=None, help="bench steps: default 20 rollout batches (step) / 4 A2C batches (a2c)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 5 rollout batches (step) / 1 A2C batch (a2c)")
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
-    ap.add_argument("--chunk", type=int, default=1000,
+    ap.add_argument("--batch-steps", type=int, default=256,
+                    help="env-steps of every env per bench step (one rollout batch, train.py:59)")
+    ap.add_argument("--chunk", type=int, default=1024,
                     help="env steps per fused launch (also timed at 200 per launch: chunk_200 in the JSON)")
     ap.add_argument("--no-chunk-compare", action="store_true", help="skip the 200-step-launch comparison")
     ap.add_argument("--num-orders", type=int, default=30)
     ap.add_argument("--masked", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0,
+                    help="wall budget of each CPU baseline leg (single thread, all cores)")
     ap.add_argument("--no-step-mode", action="store_true", help="skip the one-launch-per-step measurement")
     ap.add_argument("--workload", choices=["step", "a2c"], default="step",
                     help="step: env-step throughput (the headline metric); a2c: the batched A2C "
@@ -58,14 +63,37 @@ def parse():
     ap.add_argument("--no-scale", action="store_true", help="skip the 16x-envs leg of the step workload")
     a = ap.parse_args()
     if a.steps is None:
-        a.steps = 2000 if a.workload == "step" else 4
+        a.steps = 20 if a.workload == "step" else 4
     if a.warmup is None:
-        a.warmup = 200 if a.workload == "step" else 1
+        a.warmup = 5 if a.workload == "step" else 1
     return a
 
 
-def cpu_baseline(args, workers):
-    """The oracle (C port of the reference, kind='port') on the host cores, bounded sample."""
+def host_cores():
+    """(threads to use, description): the CPUs this process may run on, capped by the cgroup
+    CPU quota when one is set (a GPU box shows the whole machine's CPUs in nproc / affinity but
+    grants one GPU's share)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except Exception:
+        pass
+    use = min(aff, quota) if quota else aff
+    return use, {"nproc": nproc, "affinity": aff, "cgroup_cpu_quota": quota}
+
+
+def cpu_baseline(args):
+    """The oracle (C restatement of the reference step with a SimPy event heap, kind='port') on
+    the host: one thread, then one thread per available core (env shards), bounded samples of
+    the same workload (random-action rollouts, auto-reset)."""
     from oracle import oracle as O
     O.lib()
     steps = 200
@@ -73,27 +101,31 @@ def cpu_baseline(args, workers):
     O.rollout(16, steps, num_orders=args.num_orders, record=False)
     per_env_step = (time.perf_counter() - t0) / (16 * steps)
     envs_per_thread = max(1, int(args.cpu_seconds / (per_env_step * steps)))
-    res = [None] * workers
 
-    def work(i):
-        t = time.perf_counter()
-        O.rollout(envs_per_thread, steps, seeds=np.arange(i * envs_per_thread, (i + 1) * envs_per_thread),
-                  gid0=i * envs_per_thread, num_orders=args.num_orders, record=False,
-                  policy=1 if args.masked else 0)
-        res[i] = time.perf_counter() - t
+    def leg(workers):
+        def work(i):
+            O.rollout(envs_per_thread, steps, seeds=np.arange(i * envs_per_thread, (i + 1) * envs_per_thread),
+                      gid0=i * envs_per_thread, num_orders=args.num_orders, record=False,
+                      policy=1 if args.masked else 0)
 
-    th = [threading.Thread(target=work, args=(i,)) for i in range(workers)]
-    t0 = time.perf_counter()
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    wall = time.perf_counter() - t0
-    total = workers * envs_per_thread * steps
-    return {"value": total / wall, "unit": "env-steps/s", "cores": workers, "kind": "port",
-            "sample": f"{workers} threads x {envs_per_thread} envs x {steps} steps of the same workload "
-                      f"(oracle/fjsp_oracle.c, C restatement of FJSPSimulation.step with a SimPy event heap); "
-                      f"wall {wall:.2f}s",
+        th = [threading.Thread(target=work, args=(i,)) for i in range(workers)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        wall = time.perf_counter() - t0
+        return workers * envs_per_thread * steps / wall, wall
+
+    v1, w1 = leg(1)
+    cores, info = host_cores()
+    vn, wn = leg(cores)
+    return {"value": vn, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "value_1thread": v1,
+            "sample": f"{envs_per_thread} envs x {steps} steps per thread of the same workload (oracle/fjsp_oracle.c, "
+                      f"C restatement of FJSPSimulation.step with a SimPy event heap): 1 thread {w1:.1f}s wall, "
+                      f"{cores} threads (one per available core) {wn:.1f}s wall",
+            "host": info,
             "reference_python_1core": "8.0-9.0k env-steps/s (measured in the build container, BASELINE.md)"}
 
 
@@ -118,8 +150,7 @@ def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=
 
     def batch():
         learner.collect()
-        ret, adv = learner.advantages()
-        learner.update(ret, adv)
+        learner.update()
         learner.roll_over()
     for _ in range(warmup):
         batch()
@@ -133,8 +164,7 @@ def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=
         learner.collect()
         torch.cuda.synchronize()
         tc += time.perf_counter() - c0
-        ret, adv = learner.advantages()
-        learner.update(ret, adv)
+        learner.update()
         learner.roll_over()
     torch.cuda.synchronize()
     if dist:
@@ -200,7 +230,8 @@ def main():
             dist.destroy_process_group()
         return
     env.reset(seeds=torch.arange(base, base + N), num_orders=args.num_orders)
-    chunk = max(1, min(args.chunk, args.steps))
+    B = args.batch_steps                      # env-steps of every env per bench step
+    chunk = max(1, min(args.chunk, args.steps * B))
     buf = vec_env.Buffers(chunk, N, dev, infos=False)
     stream = torch.cuda.current_stream(dev)
 
@@ -218,7 +249,7 @@ def main():
             done += k
         return step0 + nsteps
 
-    s0 = run(args.warmup, 0)
+    s0 = run(args.warmup * B, 0)
     kernel_name = env.last_kernel()
     torch.cuda.synchronize()
     if dist:
@@ -226,7 +257,7 @@ def main():
     torch.cuda.synchronize()
     timing = []
     t0 = time.perf_counter()
-    run(args.steps, s0, timing)
+    run(args.steps * B, s0, timing)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -241,29 +272,30 @@ def main():
     full = [ms for ms, k in zip(kern_ms, kern_steps) if k == chunk] or kern_ms
     avg_launch_ms = float(np.mean(full))
     steps_per_launch = chunk
-    total_env_steps = args.steps * N * world
+    total_env_steps = args.steps * B * N * world
     value = total_env_steps / elapsed
     achieved = ALGO_BYTES_FUSED * N * steps_per_launch / (avg_launch_ms * 1e-3) / 1e9
     # the same workload in 200-step launches (r01's first headline configuration), rank-local
     chunk_200 = None
-    if chunk != 200 and args.steps >= 200 and not args.no_chunk_compare:
+    if chunk != 200 and args.steps * B >= 200 and not args.no_chunk_compare:
         buf200 = vec_env.Buffers(200, N, dev, infos=False)
-        s1 = run(200, s0 + args.steps, chunk=200, buf=buf200)
+        s1 = run(200, s0 + args.steps * B, chunk=200, buf=buf200)
         torch.cuda.synchronize()
         t200 = []
         tc = time.perf_counter()
-        run(args.steps, s1, t200, chunk=200, buf=buf200)
+        n200 = (args.steps * B // 200) * 200
+        run(n200, s1, t200, chunk=200, buf=buf200)
         torch.cuda.synchronize()
         el200 = time.perf_counter() - tc
         ms200 = float(np.mean([a.elapsed_time(b) for a, b, _ in t200]))
-        chunk_200 = {"value": args.steps * N / el200, "unit": "env-steps/s", "steps_per_launch": 200,
+        chunk_200 = {"value": n200 * N / el200, "unit": "env-steps/s", "steps_per_launch": 200,
                      "avg_launch_ms": ms200, "note": "rank-local, same workload in 200-step launches"}
         del buf200
 
     # one-launch-per-step mode (actions resident in HBM, k_step): the RL-loop path
     per_step = None
     if not args.no_step_mode:
-        K = min(200, args.steps)
+        K = 200
         acts = torch.randint(0, 256, (K, 8, N), dtype=torch.int32, device=dev)
         nact = torch.tensor([3, 8, 3, 3, 3, 3, 3, 3], dtype=torch.int32, device=dev).view(1, 8, 1)
         acts = ((acts * nact) >> 8).to(torch.uint8).contiguous()
@@ -329,18 +361,23 @@ def main():
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1:
-        try:
-            workers = max(1, min(16, len(os.sched_getaffinity(0))))
-        except Exception:
-            workers = max(1, min(16, os.cpu_count() or 1))
-        cpu = cpu_baseline(args, workers)
+        cpu = cpu_baseline(args)
 
     workload = f"fjsp_step_{N}envs"
+    # HBM bytes from the PMC passes (profiles/pmc_<workload>.json, scripts/gpu_pmc.sh): keyed per
+    # env-step so the figure applies to this launch length (exact when the profiled launch length
+    # is this one, else scaled; traffic_source says which)
     pmc = load_pmc(workload)
-    traffic = None
-    if (pmc and pmc.get("steps_per_launch") == steps_per_launch and pmc.get("envs") == N
-            and pmc.get("kernel_variant") == kernel_name):
-        traffic = pmc.get("hbm_bytes_per_launch")
+    traffic, traffic_src = None, None
+    if pmc and pmc.get("envs") == N and pmc.get("kernel_variant") == kernel_name and pmc.get("hbm_bytes_per_env_step"):
+        traffic = pmc["hbm_bytes_per_env_step"] * N * steps_per_launch
+        traffic_src = (f"profiles/pmc_{workload}.json, {pmc.get('steps_per_launch')}-step launches"
+                       + ("" if pmc.get("steps_per_launch") == steps_per_launch else ", scaled per env-step"))
+    if per_step is not None:
+        pk = load_pmc(f"k_step_{N}envs")
+        if pk and pk.get("kernel_variant") == per_step["kernel"] and pk.get("hbm_bytes_per_env_step"):
+            per_step["traffic_bytes_per_env_step"] = pk["hbm_bytes_per_env_step"]
+            per_step["traffic_source"] = f"profiles/pmc_k_step_{N}envs.json"
     if rank == 0:
         out = {
             "metric": "env-steps/sec (all agents) at N parallel envs, 1/2/4/8 MI355X",
@@ -358,10 +395,12 @@ def main():
             "config": {"workload": workload, "envs_per_gpu": N, "global_envs": N * world,
                        "num_orders": args.num_orders, "policy": "masked-random" if args.masked else "random",
                        "steps_per_launch": steps_per_launch, "kernel": kernel_name,
+                       "bench_step": f"one rollout batch = {B} env-steps of each of the {N} envs",
+                       "env_steps_per_bench_step": B * N * world,
                        "parallelism": f"env-shard x{world} (no data-path collective)"},
             "agent_steps_per_s": value * 8,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kernel_name, "avg_launch_ms": avg_launch_ms,
                          "algo_bytes_per_env_step": ALGO_BYTES_FUSED,
                          "env_steps_per_launch": N * steps_per_launch},

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define FJSP_ABI_VERSION 2
+#define FJSP_ABI_VERSION 3
 
 #define FJSP_NUM_AGENTS 8      /* pickup, agv, small, big, pkg_blue_1, pkg_blue_2, pkg_red, pkg_green */
 #define FJSP_OBS_I32 20        /* pickup 7 + agv 13 (position = 2) int32 observation fields */
@@ -167,7 +167,9 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
  * workgroup; identical results); "emit_wg" (0/1, default 0: k_step_ag's outputs are written by
  * emit workgroups of their own, one per core workgroup on another CU, fed step snapshots through
  * global memory; used while every block has a CU of its own, N <= 64 x CUs / 2; identical
- * results). */
+ * results); "env_id_base" (0..2^32-1, default 0: the handle is the shard [value, value + N) of a
+ * larger job — every env's MT19937 stream is re-seeded to np.random.seed(value + e), exactly
+ * the stream env value + e of one big handle starts from; stream-ordered). */
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value);
 int fjsp_num_envs(const fjsp_handle* h);
 /* Bytes of device state per env (HBM footprint of the SoA state). */
@@ -240,7 +242,8 @@ int64_t fjsp_snapshot_bytes(const fjsp_handle* h);
  *   critic_w: P(W1 [256][40]) | b1 [256] | P(W2 [256][256]) | b2 [256] | P(W3 [128][256]) |
  *            b3 [128] | W4 [128] | b4 [16]
  * Out: actions u8 [8][N] (argmax if deterministic, else an inverse-CDF draw from the masked
- * distribution keyed by (*seed, env, step, agent); `seed` is a DEVICE pointer so a captured
+ * distribution keyed by (*seed, env_gid0 + env, step, agent) — the env's global id, so the
+ * shards of a multi-GPU job draw independent streams; `seed` is a DEVICE pointer so a captured
  * hipGraph can be re-keyed between replays), values f32 [N], optional masked
  * probabilities f32 [8][8][N] (NULL to skip).  Stream-ordered on `stream`. */
 #define FJSP_POLICY_ACTOR_DPAD 16
@@ -248,7 +251,8 @@ int64_t fjsp_snapshot_bytes(const fjsp_handle* h);
 #define FJSP_POLICY_ACTOR_FLOATS (256 * 16 + 256 + 256 * 256 + 256 + 8 * 256 + 16)
 #define FJSP_POLICY_CRITIC_FLOATS (256 * 40 + 256 + 256 * 256 + 256 + 128 * 256 + 128 + 128 + 16)
 int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const float* actor_w, const float* critic_w,
-                    const uint64_t* seed, uint32_t step, int32_t deterministic, uint8_t* actions, float* values,
+                    const uint64_t* seed, uint32_t env_gid0, uint32_t step, int32_t deterministic, uint8_t* actions,
+                    float* values,
                     float* probs, void* stream);
 int fjsp_snapshot(fjsp_handle* h, void* dst);
 int fjsp_restore(fjsp_handle* h, const void* src);

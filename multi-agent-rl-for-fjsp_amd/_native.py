@@ -66,7 +66,7 @@ EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_c
            "fjsp_snapshot_bytes", "fjsp_snapshot", "fjsp_restore", "fjsp_last_kernel", "fjsp_a2c_policy"]
 POLICY_ACTOR_FLOATS = 256 * 16 + 256 + 256 * 256 + 256 + 8 * 256 + 16
 POLICY_CRITIC_FLOATS = 256 * 40 + 256 + 256 * 256 + 256 + 128 * 256 + 128 + 128 + 16
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _lib = None
 
@@ -131,7 +131,7 @@ def lib():
         "fjsp_snapshot": (I, [P, P]),
         "fjsp_restore": (I, [P, P]),
         "fjsp_last_kernel": (ctypes.c_char_p, [P]),
-        "fjsp_a2c_policy": (I, [P, P, I, P, P, P, U32, I, P, P, P, P]),
+        "fjsp_a2c_policy": (I, [P, P, I, P, P, P, U32, U32, I, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

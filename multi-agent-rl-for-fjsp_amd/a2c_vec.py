@@ -15,9 +15,12 @@ a2c.py:647-731) and the same checkpoint format (a2c.py:733-775) — restated for
   * one update per `batch_size` vector steps uses all batch_size x N transitions; the loss
     means / advantage statistics are over that whole batch (for N = 1 this is exactly the
     reference's update);
-  * multi-GPU (config 5): every rank steps its own env shard, computes local sums and one
-    bucketed all_reduce (RCCL) of the gradients makes the update identical to a single learner
-    over all ranks' transitions (distributed.py).
+  * multi-GPU (config 5): every rank steps its own env shard (envs keyed by global id: MT
+    streams and action draws), then either computes local sums and one bucketed all_reduce
+    (RCCL) of the gradients (exchange="allreduce", default) or gathers its transitions into the
+    learner rank, which updates over the whole batch and broadcasts the parameters
+    (exchange="gather", the reference's memory -> finish_trajectory -> _update); both equal a
+    single learner over all ranks' transitions (distributed.py).
 
 Padding is exact: padded input columns are zero and their weights receive zero gradient;
 padded action logits are -inf before the softmax.
@@ -170,6 +173,38 @@ def categorical_log_prob(p, actions):
     return torch.log(q.clamp(min=eps, max=1 - eps)).gather(1, actions.unsqueeze(1)).squeeze(1)
 
 
+_M64 = (1 << 64) - 1
+
+
+def _fmix64(z):
+    """splitmix64's finaliser on int64 tensors (wrapping multiply, logical shifts): the same
+    hash csrc/fjsp_policy.hip draws its actions with."""
+    def shr(x, k):
+        return (x >> k) & ((1 << (64 - k)) - 1)
+
+    def s64(c):
+        return c - (1 << 64) if c >= (1 << 63) else c
+    z = z ^ shr(z, 30)
+    z = z * s64(0xBF58476D1CE4E5B9)
+    z = z ^ shr(z, 27)
+    z = z * s64(0x94D049BB133111EB)
+    return z ^ shr(z, 31)
+
+
+def counter_uniform(seed, gid, step, device):
+    """U [8, 1, B] in [0, 1) keyed by (seed, global env id, step, agent) exactly as the fused
+    policy kernel's draw (fjsp_policy.hip): shards of a multi-GPU job draw independent streams
+    and the eager and fused paths see the same uniforms."""
+    def s64(c):
+        c &= _M64
+        return c - (1 << 64) if c >= (1 << 63) else c
+    g = torch.as_tensor(gid, device=device).to(torch.int64) & 0xFFFFFFFF
+    inner = _fmix64((g << 32) | (int(step) & 0xFFFFFFFF))
+    role = torch.tensor([s64((a + 1) * 0x9E3779B97F4A7C15) for a in range(NA)], dtype=torch.int64, device=device)
+    h = _fmix64((s64(seed) ^ inner)[None, :] ^ role[:, None])            # [8, B]
+    return ((h >> 40) & 0xFFFFFF).to(torch.float32).mul_(1.0 / 16777216.0).unsqueeze(1)
+
+
 def sample_categorical(p, u=None):
     """One draw per (agent, env) from p [8, 8, B] by inverse CDF: action = #{k : cdf_k < x}
     with x = (1 - U) * cdf_last, U ~ [0, 1) -> x in (0, total]; a zero-probability action can
@@ -299,6 +334,23 @@ def update_step(actors, critic, optim_actor, optim_critic, feats, masks, actions
     return al.cpu().tolist(), float(cl.cpu()[0])
 
 
+def batch_advantages(rewards, values, done, gamma, lamb, use_gae=True):
+    """finish_trajectory (transition_memory.py:45-105) over a [T, ., N] batch with the fp64
+    GAE kernel.  rewards f64 [T, 8, N], values f32 [T + 1, N] (row T = V(s_T), the batch-end
+    bootstrap, a2c.py:321-332), done u8/bool [T, N] (an episode end bootstraps 0, a2c.py:357).
+    Returns ret, adv f64 [T, 8, N]."""
+    from .vec_env import gae
+    T, _, N = rewards.shape
+    vals = values[:T, None, :].expand(T, NA, N).contiguous()
+    boot = values[T].double()[None, :].expand(NA, N).contiguous()
+    ret, adv = gae(rewards.contiguous().view(T, NA * N), vals.view(T, NA * N), done.to(torch.uint8).contiguous(),
+                   boot.view(NA * N), gamma, lamb)
+    ret, adv = ret.view(T, NA, N), adv.view(T, NA, N)
+    if not use_gae:
+        adv = ret - vals.double()
+    return ret, adv
+
+
 class VecMultiAgentA2C:
     """MultiAgentA2C for an FJSPVecEnv (N envs on this GPU; optionally one shard of a
     multi-GPU job through `group`).
@@ -308,7 +360,7 @@ class VecMultiAgentA2C:
 
     def __init__(self, env, batch_size=256, gamma=0.99, lamb=0.95, lr_actor=3e-4, lr_critic=1e-3,
                  use_gae=True, entropy_coef=0.01, max_grad_norm=0.5, hidden=256, seed=None, group=None,
-                 use_graph=True, fused_policy=True):
+                 use_graph=True, fused_policy=True, exchange="allreduce"):
         self.env = env
         self.device = env.device
         self.N = env.num_envs
@@ -318,6 +370,9 @@ class VecMultiAgentA2C:
         self.entropy_coef = float(entropy_coef)
         self.max_grad_norm = float(max_grad_norm)
         self.group = group
+        if exchange not in ("allreduce", "gather"):
+            raise ValueError("exchange must be 'allreduce' or 'gather'")
+        self.exchange = exchange
         self.possible_agents = list(AGENTS)
         self.obs_dims = dict(zip(AGENTS, OBS_DIMS))
         self.act_dims = dict(zip(AGENTS, N_ACTIONS))
@@ -334,10 +389,12 @@ class VecMultiAgentA2C:
         self.use_graph = bool(use_graph) and self.device.type == "cuda"
         # fused policy kernel (csrc/fjsp_policy.hip): one launch per vector step
         self.fused_policy = bool(fused_policy) and self.device.type == "cuda" and hidden == 256
+        # sampling key: (seed, batch) -> counter hash per (global env id, step, agent); the same
+        # on every rank, the env's global id separates the shards
+        self._rng_host = int.from_bytes(__import__("os").urandom(7), "little") if seed is None else int(seed)
         if self.fused_policy:
             self._pw_actor, self._pw_critic = pack_policy_weights(self.actors, self.critic)
             self._rng = torch.zeros(1, dtype=torch.int64, device=self.device)
-            self._rng_host = int.from_bytes(__import__("os").urandom(7), "little") if seed is None else int(seed)
             self._rng.fill_(self._rng_host)
         self._graph = None
         self._graph_det = None
@@ -379,6 +436,9 @@ class VecMultiAgentA2C:
         o.masks = b["masks"][0].data_ptr()
         o.feats = b["feats"][0].data_ptr()
         self.env._sync_stream()
+        if seeds is None and getattr(self.env, "_pending_seeds", None) is not None:
+            seeds = self.env._pending_seeds   # FJSPVecEnv.seed(...) before the learner's reset
+        self.env._pending_seeds = None
         s = None
         if seeds is not None:
             s = torch.as_tensor(seeds, device=self.device).to(torch.int64).bitwise_and(0xFFFFFFFF).to(torch.int32)
@@ -388,12 +448,14 @@ class VecMultiAgentA2C:
 
     # ------------------------------------------------------------ predict
     @torch.no_grad()
-    def policy_fused(self, feats, masks, t, deterministic, act_out, val_out, probs_out=None):
+    def policy_fused(self, feats, masks, t, deterministic, act_out, val_out, probs_out=None, gid0=None):
         """fjsp_a2c_policy on this stream: actions u8 [8, N] -> act_out, values -> val_out."""
         stream = torch.cuda.current_stream(self.device).cuda_stream
         P = lambda x: None if x is None else ctypes.c_void_p(x.data_ptr())  # noqa: E731
         rc = nat.lib().fjsp_a2c_policy(P(feats), P(masks), int(feats.shape[-1]), P(self._pw_actor),
-                                       P(self._pw_critic), P(self._rng), int(t), int(bool(deterministic)),
+                                       P(self._pw_critic), P(self._rng), int(gid0 if gid0 is not None else
+                                                                                self.env.env_id_base),
+                                       int(t), int(bool(deterministic)),
                                        P(act_out), P(val_out), P(probs_out), ctypes.c_void_p(stream))
         nat.check(rc)
 
@@ -403,11 +465,17 @@ class VecMultiAgentA2C:
             pack_policy_weights(self.actors, self.critic, self._pw_actor, self._pw_critic)
 
     @torch.no_grad()
-    def policy(self, feats, masks, deterministic=False):
+    def policy(self, feats, masks, deterministic=False, t=0, gid0=None):
         """predict (a2c.py:168-252) for all agents and envs: actions long [8, B], the masked
-        probabilities [8, 8, B] and the critic's value [B]."""
+        probabilities [8, 8, B] and the critic's value [B].  Draws use the fused kernel's
+        counter hash keyed by (seed, global env id, t, agent)."""
         pm = masked_probs(self.actors(actor_inputs(feats, self.gidx)), agent_masks(masks, self.midx))
-        act = torch.argmax(pm, dim=1) if deterministic else sample_categorical(pm)
+        if deterministic:
+            act = torch.argmax(pm, dim=1)
+        else:
+            g0 = self.env.env_id_base if gid0 is None else gid0
+            gid = torch.arange(g0, g0 + pm.shape[2], device=pm.device)
+            act = sample_categorical(pm, counter_uniform(self._rng_host, gid, t, pm.device))
         v = self.critic(feats.t()).view(-1)
         return act, pm, v
 
@@ -425,8 +493,8 @@ class VecMultiAgentA2C:
         (tests).  After one eager batch the whole batch (batch_size x (policy + step) plus the
         bootstrap value, ~40 launches per step) is captured once into a hipGraph and replayed:
         the buffers and parameters are static, Adam updates the weights in place."""
+        self._rng_host += 1
         if self.fused_policy:
-            self._rng_host += 1
             self._rng.fill_(self._rng_host)   # re-keys the sampling of the (captured) batch
         if action_fn is None and self.use_graph:
             if self._graph is not None and self._graph_det == deterministic:
@@ -461,7 +529,7 @@ class VecMultiAgentA2C:
             if self.fused_policy and action_fn is None:
                 self.policy_fused(b["feats"][t], b["masks"][t], t, deterministic, b["actions"][t], b["values"][t])
             else:
-                act, _, v = self.policy(b["feats"][t], b["masks"][t], deterministic)
+                act, _, v = self.policy(b["feats"][t], b["masks"][t], deterministic, t=t)
                 if action_fn is not None:
                     act = action_fn(t, b["masks"][t]).to(self.device).long()
                 b["actions"][t].copy_(act)
@@ -474,31 +542,62 @@ class VecMultiAgentA2C:
     def advantages(self):
         """finish_trajectory over the batch (transition_memory.py:45-105) with the fp64 GAE
         kernel: an episode end bootstraps 0 (a2c.py:357), the batch end V(s_T) (a2c.py:321-332)."""
-        from .vec_env import gae
         b = self._bufs
-        T, N = self.batch_size, self.N
-        done = (b["term"] | b["trunc"]).contiguous()
-        vals = b["values"][:T, None, :].expand(T, NA, N).contiguous()
-        boot = b["values"][T].double()[None, :].expand(NA, N).contiguous()
-        ret, adv = gae(b["rewards"].view(T, NA * N), vals.view(T, NA * N), done, boot.view(NA * N),
-                       self.gamma, self.lamb)
-        ret, adv = ret.view(T, NA, N), adv.view(T, NA, N)
-        if not self.use_gae:
-            adv = ret - vals.double()
-        return ret, adv
+        return batch_advantages(b["rewards"], b["values"], b["term"] | b["trunc"], self.gamma, self.lamb,
+                                self.use_gae)
 
-    def update(self, ret, adv):
-        """_update (a2c.py:647-703) over the batch's T x N transitions."""
-        b = self._bufs
-        T = self.batch_size
-        al, cl = update_step(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
-                             b["masks"][:T], b["actions"], ret, adv, self.gidx, self.midx, self.entropy_coef,
-                             self.max_grad_norm, self.group)
+    def update(self, ret=None, adv=None):
+        """_update (a2c.py:647-703) over the batch's T x N transitions (x world with a group).
+
+        exchange "allreduce": GAE on this rank, one flat gradient all_reduce (distributed.py);
+        exchange "gather": the transitions go to the learner rank (ret / adv are recomputed
+        there over the gathered batch), the new parameters come back in one broadcast."""
+        if self.exchange == "gather" and self.group is not None:
+            al, cl = self._update_gathered()
+        else:
+            if ret is None:
+                ret, adv = self.advantages()
+            b = self._bufs
+            T = self.batch_size
+            al, cl = update_step(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
+                                 b["masks"][:T], b["actions"], ret, adv, self.gidx, self.midx, self.entropy_coef,
+                                 self.max_grad_norm, self.group)
         for a, x in zip(AGENTS, al):
             self.actor_loss_history[a].append(x)
         self.critic_loss_history.append(cl)
         self.repack()
         return al, cl
+
+    def _update_gathered(self):
+        """Experience gather into the learner (rank 0 of the group): the reference's
+        transition_memory filled with every rank's transitions, finish_trajectory + _update
+        over the whole batch (a2c.py:324-336), then the parameters broadcast back."""
+        from . import distributed as D
+        import torch.distributed as dist
+        b = self._bufs
+        T = self.batch_size
+        slab = {"feats": b["feats"][:T], "masks": b["masks"][:T], "actions": b["actions"], "rewards": b["rewards"],
+                "values": b["values"], "done": b["term"] | b["trunc"]}
+        full = D.gather_slabs(slab, dst=0, group=self.group)
+        params = list(self.actors.parameters()) + list(self.critic.parameters())
+        stats = torch.zeros(NA + 1, dtype=torch.float32, device=self.device)
+        if dist.get_rank(self.group) == 0:
+            cat = lambda x: x.movedim(0, -2).reshape(*x.shape[1:-1], -1)   # [W, ..., n] -> [..., W*n]  # noqa: E731
+            g = {k: cat(v) for k, v in full.items()}
+            ret, adv = batch_advantages(g["rewards"], g["values"], g["done"], self.gamma, self.lamb, self.use_gae)
+            al, cl = update_step(self.actors, self.critic, self.optim_actor, self.optim_critic, g["feats"], g["masks"],
+                                 g["actions"], ret, adv, self.gidx, self.midx, self.entropy_coef,
+                                 self.max_grad_norm, D.LOCAL)
+            stats.copy_(torch.tensor(al + [cl], dtype=torch.float32))
+        D.broadcast_flat(params + [stats], src=0, group=self.group)
+        v = stats.cpu().tolist()
+        return v[:NA], v[NA]
+
+    def exchange_bytes_per_batch(self):
+        """Bytes one rank sends per batch with exchange="gather" (the transition slab)."""
+        T, N = self.batch_size, self.N
+        per_env_step = GLOBAL_DIM * 4 + 29 + NA + NA * 8 + 4 + 1
+        return T * N * per_env_step + N * 4
 
     def roll_over(self):
         """The last observation of the batch becomes the first of the next."""
@@ -513,8 +612,7 @@ class VecMultiAgentA2C:
         steps = 0
         while steps < total_timesteps:
             self.collect(deterministic, action_fn)
-            ret, adv = self.advantages()
-            self.update(ret, adv)
+            self.update()
             self.roll_over()
             steps += self.batch_size * self.N
         return self
@@ -526,10 +624,19 @@ class VecMultiAgentA2C:
         actions (deterministic) until each env's episode ends or max_steps.  Returns per-env
         numpy arrays as the reference's test() dict (+ the actions [T, 8, N] with trace).
         Runs on `env` (a separate FJSPVecEnv, as the reference builds a fresh test env) or,
-        by default, resets the training env (the next collect() starts new episodes)."""
+        by default, on the training env, which is reset afterwards with the training
+        num_orders (the next collect() starts new episodes from fresh observations)."""
+        on_train = env is None or env is self.env
+        res = self._test(num_orders, max_steps, seeds, deterministic, trace, self.env if env is None else env,
+                         use_heuristic)
+        if on_train and self._bufs is not None:
+            self.reset(num_orders=getattr(self, "num_orders", 25))
+        return res
+
+    @torch.no_grad()
+    def _test(self, num_orders, max_steps, seeds, deterministic, trace, env, use_heuristic):
         import numpy as np
         from .vec_env import Buffers
-        env = self.env if env is None else env
         if use_heuristic:
             return env.evaluate("heuristic", num_orders=num_orders, max_steps=max_steps, seeds=seeds)
         N = env.num_envs
@@ -546,9 +653,9 @@ class VecMultiAgentA2C:
         acts = []
         for t in range(int(max_steps)):
             if self.fused_policy:
-                self.policy_fused(feats, masks, t, deterministic, act, val)
+                self.policy_fused(feats, masks, t, deterministic, act, val, gid0=env.env_id_base)
             else:
-                act.copy_(self.policy(feats, masks, deterministic)[0])
+                act.copy_(self.policy(feats, masks, deterministic, t=t, gid0=env.env_id_base)[0])
             if trace:
                 acts.append(act.cpu().numpy().copy())
             env.step(act, autoreset=False, buffers=b)
@@ -594,13 +701,19 @@ class VecMultiAgentA2C:
         self.load_state_dicts(ck)
 
     def load_state_dicts(self, ck):
+        """load_model (a2c.py:756-775): only the agents the checkpoint holds are overwritten
+        (the others keep their weights); the critic if present."""
         nets = []
         for i, a in enumerate(AGENTS):
             net = ActorNet(OBS_DIMS[i], N_ACTIONS[i], self.actors.hidden)
-            net.load_state_dict(ck["actor_nets"][a])
+            sd = ck.get("actor_nets", {}).get(a)
+            if sd is None:
+                sd = self.actors.actor_state_dict(i)
+            net.load_state_dict(sd)
             nets.append(net)
         self.actors.load_actor_nets([n.to(self.device) for n in nets])
-        self.critic.load_state_dict(ck["critic_net"])
+        if ck.get("critic_net") is not None:
+            self.critic.load_state_dict(ck["critic_net"])
         if getattr(self, "fused_policy", False):
             self.repack()
 

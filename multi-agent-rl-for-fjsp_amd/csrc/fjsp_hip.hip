@@ -1993,6 +1993,7 @@ struct fjsp_handle {
     uint32_t* ag_count;     // AgEmit::count, one 128-byte line per core workgroup
     uint32_t ag_base;       // the largest count a launch can have left there
     const char* last_kernel;   // name of the last step kernel launched (fjsp_last_kernel)
+    uint32_t env_id_base;      // global id of env 0 (fjsp_set_option "env_id_base")
 };
 
 static thread_local std::string g_err;
@@ -2094,7 +2095,7 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     if (fjsp_check_config(&c)) return -1;
     if (num_envs <= 0) return fail("num_envs must be > 0");
     DeviceGuard g(device);
-    fjsp_handle* h = new fjsp_handle();
+    fjsp_handle* h = new fjsp_handle();   // value-initialised: every pointer starts null
     h->cfg = c;
     h->n = num_envs;
     h->device = device;
@@ -2139,8 +2140,10 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     const size_t b_mt = (size_t)2 * MT_N * n * 4, b_nxt = (size_t)MAX_ORDERS * n * 4;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     h->bytes = al(b_words) + al(b_orders) + al(b_scode) + al(b_snext) + al(b_scstep) + al(b_nxt) + al(b_mt);
+    // every failure below goes through fjsp_destroy, which frees whatever was allocated
+    auto bail = [&](const char* what, hipError_t err) { fjsp_destroy(h); return hip_fail(what, err); };
     hipError_t e = hipMalloc(&h->base, h->bytes);
-    if (e != hipSuccess) { delete h; return hip_fail("hipMalloc(state)", e); }
+    if (e != hipSuccess) { h->base = nullptr; return bail("hipMalloc(state)", e); }
     char* p = (char*)h->base;
     h->S.words = (uint32_t*)p; p += al(b_words);
     h->S.orders = (uint32_t*)p; p += al(b_orders);
@@ -2151,28 +2154,31 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     h->S.mt = (uint32_t*)p;
     h->S.n = num_envs;
     e = hipMemsetAsync(h->base, 0, h->bytes, h->stream);
-    if (e == hipSuccess) e = hipEventCreate(&h->ev0);
-    if (e == hipSuccess) e = hipEventCreate(&h->ev1);
-    if (e != hipSuccess) { (void)hipFree(h->base); delete h; return hip_fail("init", e); }
+    if (e != hipSuccess) return bail("init", e);
+    e = hipEventCreate(&h->ev0);
+    if (e != hipSuccess) { h->ev0 = nullptr; return bail("hipEventCreate", e); }
+    e = hipEventCreate(&h->ev1);
+    if (e != hipSuccess) { h->ev1 = nullptr; return bail("hipEventCreate", e); }
     e = hipMalloc(&h->lut_dev, sizeof(double) * RLUT_SIZE);
-    if (e != hipSuccess) { (void)hipFree(h->base); delete h; return hip_fail("hipMalloc(reward table)", e); }
+    if (e != hipSuccess) { h->lut_dev = nullptr; return bail("hipMalloc(reward table)", e); }
     e = hipMalloc(&h->ag_count, (n + BLOCK - 1) / BLOCK * AG_COUNT_STRIDE * sizeof(uint32_t));
-    if (e == hipSuccess)
-        e = hipMemsetAsync(h->ag_count, 0, (n + BLOCK - 1) / BLOCK * AG_COUNT_STRIDE * sizeof(uint32_t), h->stream);
-    if (e != hipSuccess) { (void)hipFree(h->lut_dev); (void)hipFree(h->base); delete h; return hip_fail("hipMalloc(emit counts)", e); }
+    if (e != hipSuccess) { h->ag_count = nullptr; return bail("hipMalloc(emit counts)", e); }
+    e = hipMemsetAsync(h->ag_count, 0, (n + BLOCK - 1) / BLOCK * AG_COUNT_STRIDE * sizeof(uint32_t), h->stream);
+    if (e != hipSuccess) return bail("hipMemset(emit counts)", e);
     h->dcfg.lut = h->lut_dev;
     {
         fjsp_reward_weights w;
         fjsp_default_reward_weights(&w);
         build_reward_lut(reinterpret_cast<const double*>(&w), c.step_size, h->lut_host);
         e = hipMemcpy(h->lut_dev, h->lut_host, sizeof(double) * RLUT_SIZE, hipMemcpyHostToDevice);
-        if (e != hipSuccess) { (void)hipFree(h->lut_dev); (void)hipFree(h->base); delete h; return hip_fail("reward table", e); }
+        if (e != hipSuccess) return bail("reward table", e);
     }
     // default streams: env e behaves like a process that called np.random.seed(e)
+    // (fjsp_set_option "env_id_base" re-keys them by global id)
     hipLaunchKernelGGL(k_seed, dim3((h->n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, h->stream, h->S,
                        (const uint32_t*)nullptr, 0u);
     e = hipGetLastError();
-    if (e != hipSuccess) { (void)hipFree(h->base); delete h; return hip_fail("k_seed", e); }
+    if (e != hipSuccess) return bail("k_seed", e);
     *out = h;
     return 0;
 }
@@ -2181,11 +2187,11 @@ int fjsp_destroy(fjsp_handle* h) {
     if (!h) return 0;
     DeviceGuard g(h->device);
     (void)hipStreamSynchronize(h->stream);
-    (void)hipEventDestroy(h->ev0);
-    (void)hipEventDestroy(h->ev1);
-    (void)hipFree(h->lut_dev);
-    (void)hipFree(h->base);
-    (void)hipFree(h->ag_count);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->lut_dev) (void)hipFree(h->lut_dev);
+    if (h->base) (void)hipFree(h->base);
+    if (h->ag_count) (void)hipFree(h->ag_count);
     if (h->ag_snap) (void)hipFree(h->ag_snap);
     delete h;
     return 0;
@@ -2200,6 +2206,17 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
     if (!strcmp(name, "agents")) { h->use_ag = value != 0; return 0; }
     if (!strcmp(name, "emit_wg")) { h->use_emit_wg = value != 0; return 0; }
     if (!strcmp(name, "timing")) { h->timing = value != 0; if (!h->timing) h->timed = 0; return 0; }
+    if (!strcmp(name, "env_id_base")) {
+        // the handle is shard [value, value + n) of a larger job: env e's default stream becomes
+        // np.random.seed(value + e), as for env value + e of one big handle (stream-ordered)
+        if (value < 0 || value > 0xFFFFFFFFll) return fail("env_id_base must be in 0..2^32-1");
+        DeviceGuard g(h->device);
+        hipLaunchKernelGGL(k_seed, dim3((h->n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, h->stream, h->S,
+                           (const uint32_t*)nullptr, (uint32_t)value);
+        HIPCHK(hipGetLastError());
+        h->env_id_base = (uint32_t)value;
+        return 0;
+    }
     return fail("unknown option");
 }
 

@@ -140,7 +140,7 @@ __device__ __forceinline__ void hidden256(const float* __restrict__ W, const flo
 __global__ void __launch_bounds__(256, 2) k_policy(const float* __restrict__ feats, const int8_t* __restrict__ masks,
                                                    int n, const float* __restrict__ actor_w,
                                                    const float* __restrict__ critic_w, const uint64_t* __restrict__ seedp,
-                                                   uint32_t step, int deterministic, uint8_t* __restrict__ actions,
+                                                   uint32_t gid0, uint32_t step, int deterministic, uint8_t* __restrict__ actions,
                                                    float* __restrict__ values, float* __restrict__ probs_out) {
     __shared__ float s_x[FJSP_POLICY_CRITIC_DPAD * TILE];   // inputs; later the logits [8][64]
     __shared__ float s_h[HID * TILE];                        // h1, then h2 (then critic h3)
@@ -216,7 +216,8 @@ __global__ void __launch_bounds__(256, 2) k_policy(const float* __restrict__ fea
             for (int j = 1; j < na; j++) if (p[j] > best) { best = p[j]; act = j; }
         } else {
             const uint64_t seed = *seedp;
-            const uint64_t h = fmix64(seed ^ fmix64(((uint64_t)(uint32_t)e << 32) | step) ^
+            // keyed by the env's GLOBAL id: shards of a multi-GPU job draw independent streams
+            const uint64_t h = fmix64(seed ^ fmix64(((uint64_t)(gid0 + (uint32_t)e) << 32) | step) ^
                                       (uint64_t)(role + 1) * 0x9E3779B97F4A7C15ull);
             const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
             float cdf[8], tot = 0.0f;
@@ -236,14 +237,15 @@ __global__ void __launch_bounds__(256, 2) k_policy(const float* __restrict__ fea
 int fjsp_internal_fail(const char* msg);   // fjsp_hip.hip: sets fjsp_last_error()
 
 extern "C" int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const float* actor_w,
-                               const float* critic_w, const uint64_t* seed, uint32_t step, int32_t deterministic,
+                               const float* critic_w, const uint64_t* seed, uint32_t env_gid0, uint32_t step,
+                               int32_t deterministic,
                                uint8_t* actions, float* values, float* probs, void* stream) {
     if (n <= 0) return fjsp_internal_fail("fjsp_a2c_policy: n must be > 0");
     if (!feats || !masks || !actor_w || !critic_w || !seed || !actions || !values)
         return fjsp_internal_fail("fjsp_a2c_policy: null buffer");
     dim3 grid((n + TILE - 1) / TILE, NAG + 1);
-    hipLaunchKernelGGL(k_policy, grid, dim3(256), 0, (hipStream_t)stream, feats, masks, n, actor_w, critic_w, seed, step,
-                       deterministic, actions, values, probs);
+    hipLaunchKernelGGL(k_policy, grid, dim3(256), 0, (hipStream_t)stream, feats, masks, n, actor_w, critic_w, seed, env_gid0,
+                       step, deterministic, actions, values, probs);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

@@ -9,8 +9,13 @@ on one GPU.  The only exchange is once per A2C batch:
     tiny all_reduces of advantage statistics -> the update equals a single learner's over all
     ranks' transitions.  On xGMI (point-to-point links) one 2.7 MB ring all_reduce per batch is
     per-link bound and costs well under a millisecond;
-  * gather_transitions: the §8(e) alternative — all_gather of a rank's transition slab into
-    a learner-side [world, ...] tensor (e.g. to feed an external learner).
+  * exchange="gather" (VecMultiAgentA2C): the north star's experience gather — every rank's
+    transition slab (features, masks, actions, rewards, values, episode ends; ~258 B per
+    env-step) is gathered into the learner rank in ONE collective (gather_slabs), the learner
+    runs GAE + the update over the whole batch exactly as a single learner would, and ONE flat
+    broadcast (broadcast_flat) hands the new parameters (and the loss values) back;
+  * gather_transitions: all_gather of a rank's transition slab into a [world, ...] tensor on
+    every rank (e.g. to feed an external learner).
 
 The torch.distributed backend is "nccl" (= RCCL on ROCm) on GPUs and "gloo" in CPU tests.
 """
@@ -20,7 +25,12 @@ import torch
 import torch.distributed as dist
 
 
+LOCAL = "local"   # group argument meaning "this process only" (no collective, even when initialised)
+
+
 def active(group=None):
+    if group is LOCAL:
+        return False
     return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
 
 
@@ -102,6 +112,53 @@ def gather_transitions(slab, group=None):
     out = torch.empty(world * flat.numel(), dtype=slab.dtype, device=slab.device)
     dist.all_gather_into_tensor(out, flat, group=group)
     return out.view((world,) + tuple(slab.shape))
+
+
+def _backend(group=None):
+    return dist.get_backend(group) if active(group) else None
+
+
+def gather_slabs(slabs, dst=0, group=None):
+    """Gather a dict of per-rank tensors (same shapes on every rank) into rank `dst` with ONE
+    collective: every tensor is viewed as bytes and packed into one flat buffer.  Returns on
+    `dst` a dict of [world, *shape] tensors, None on the other ranks (single process: the
+    slabs with a leading axis of 1)."""
+    names = list(slabs)
+    if not active(group):
+        return {k: slabs[k].unsqueeze(0) for k in names}
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    flat = torch.cat([slabs[k].contiguous().view(-1).view(torch.uint8) for k in names])
+    gloo = _backend(group) == "gloo"
+    src = flat.cpu() if gloo else flat     # gloo gathers host tensors
+    bufs = [torch.empty_like(src) for _ in range(world)] if rank == dst else None
+    dist.gather(src, gather_list=bufs, dst=dst, group=group)
+    if rank != dst:
+        return None
+    allb = torch.stack(bufs).to(flat.device)       # [world, bytes]
+    out, off = {}, 0
+    for k in names:
+        t = slabs[k]
+        nb = t.numel() * t.element_size()
+        out[k] = allb[:, off:off + nb].contiguous().view(t.dtype).view((world,) + tuple(t.shape))
+        off += nb
+    return out
+
+
+def broadcast_flat(tensors, src=0, group=None):
+    """Broadcast a list of tensors from `src` with ONE flat f32 bucket (in place)."""
+    if not active(group):
+        return
+    flat = torch.cat([t.detach().reshape(-1).to(torch.float32) for t in tensors])
+    gloo = _backend(group) == "gloo"
+    buf = flat.cpu() if gloo else flat
+    dist.broadcast(buf, src=src, group=group)
+    buf = buf.to(flat.device)
+    off = 0
+    with torch.no_grad():
+        for t in tensors:
+            n = t.numel()
+            t.copy_(buf[off:off + n].view_as(t).to(t.dtype))
+            off += n
 
 
 def broadcast_params(module, src=0, group=None):

@@ -92,8 +92,11 @@ class FJSPVecEnv:
         self._h = h
         self._step_buf = None
         self._num_orders = 30
+        self._pending_seeds = None
         if self.env_id_base:
-            self.seed(torch.arange(self.env_id_base, self.env_id_base + self.num_envs, dtype=torch.int64))
+            # default streams keyed by global id: env e starts from np.random.seed(env_id_base + e),
+            # whichever call resets it first (reset(seed=None), a learner's reset, ...)
+            nat.check(L.fjsp_set_option(h, b"env_id_base", self.env_id_base))
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -103,3 +103,98 @@ def test_shard_ranges_cover_global_ids():
         base, n = D.shard_range(4096, rank)
         ids.extend(range(base, base + n))
     assert ids == list(range(8 * 4096))
+
+
+# ---------------------------------------------------------------- experience gather (exchange="gather")
+class _CpuEnv:
+    """Stand-in for FJSPVecEnv in the CPU test: the learner only needs the device, the shard
+    size and its global id base here (the transitions are given)."""
+
+    def __init__(self, n, base):
+        self.device = torch.device("cpu")
+        self.num_envs = n
+        self.env_id_base = base
+
+
+def _gae_cpu(rewards, values, done, gamma, lamb, use_gae=True):
+    """transition_memory.py:83-105 in torch fp64 (test stand-in for the GAE kernel)."""
+    T, _, n = rewards.shape
+    v = values.double()
+    ret = torch.zeros_like(rewards)
+    adv = torch.zeros_like(rewards)
+    r_acc = v[T].expand(8, n).clone()
+    g_acc = torch.zeros(8, n, dtype=torch.float64)
+    nxt = v[T].expand(8, n).clone()
+    for t in range(T - 1, -1, -1):
+        end = done[t].bool().expand(8, n)
+        r_acc = torch.where(end, torch.zeros_like(r_acc), r_acc)
+        g_acc = torch.where(end, torch.zeros_like(g_acc), g_acc)
+        nv = torch.where(end, torch.zeros_like(nxt), nxt)
+        r_acc = rewards[t] + gamma * r_acc
+        delta = (rewards[t] + gamma * nv) - v[t].expand(8, n)
+        g_acc = delta + (gamma * lamb) * g_acc
+        ret[t], adv[t] = r_acc, g_acc
+        nxt = v[t].expand(8, n)
+    return ret, adv
+
+
+def _rollout_batch(seed=0):
+    feats, masks, acts, _, _ = _batch(seed)
+    g = torch.Generator().manual_seed(seed + 1)
+    feats = torch.cat([feats, feats[-1:]], dim=0)                 # [T + 1, 38, N]
+    masks = torch.cat([masks, masks[-1:]], dim=0)
+    values = torch.randn(T + 1, N, generator=g) * 5
+    rewards = torch.randn(T, 8, N, generator=g, dtype=torch.float64)
+    term = (torch.rand(T, N, generator=g) < 0.05).to(torch.uint8)
+    trunc = torch.zeros(T, N, dtype=torch.uint8)
+    return dict(feats=feats, masks=masks, actions=acts, values=values, rewards=rewards, term=term, trunc=trunc)
+
+
+def _learner(n, base, group, exchange):
+    A.batch_advantages = _gae_cpu     # CPU stand-in for the GAE kernel (the learner's only GPU call here)
+    L = A.VecMultiAgentA2C(_CpuEnv(n, base), batch_size=T, seed=11, group=group, use_graph=False,
+                           fused_policy=False, exchange=exchange)
+    L._alloc()
+    return L
+
+
+def _fill(L, sl):
+    for k, v in _rollout_batch().items():
+        L._bufs[k].copy_(v[..., sl])
+
+
+def _gather_worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+    n = N // world
+    L = _learner(n, rank * n, dist.group.WORLD, "gather")
+    _fill(L, slice(rank * n, (rank + 1) * n))
+    al, cl = L.update()
+    params = torch.cat([p.detach().reshape(-1) for p in list(L.actors.parameters()) + list(L.critic.parameters())])
+    slabs = D.gather_slabs({"a": torch.full((2, 3), rank, dtype=torch.int16),
+                            "b": torch.full((4,), 0.5 + rank, dtype=torch.float64)}, dst=0)
+    torch.save({"al": al, "cl": cl, "params": params, "slabs": slabs}, os.path.join(out_dir, f"g{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_exchange_equals_single_learner(tmp_path):
+    """exchange="gather": the learner rank's update over the gathered batch IS the single
+    learner's update (same data, same ops), and the broadcast hands it to every rank."""
+    mp.spawn(_gather_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r = [torch.load(os.path.join(tmp_path, f"g{k}.pt"), weights_only=True) for k in range(2)]
+    L = _learner(N, 0, None, "allreduce")
+    _fill(L, slice(0, N))
+    al, cl = L.update()
+    params = torch.cat([p.detach().reshape(-1) for p in list(L.actors.parameters()) + list(L.critic.parameters())])
+    assert torch.equal(r[0]["params"], r[1]["params"])      # the broadcast replicated the learner's update
+    d = (r[0]["params"] - params).abs() / 3e-4               # same data and ops; the thread count of the
+    assert float((d > 1e-2).float().mean()) < 1e-3           # CPU GEMMs differs (reduction order only)
+    for k in range(2):
+        assert np.allclose(r[k]["al"], al, rtol=1e-5, atol=1e-7) and r[k]["cl"] == pytest.approx(cl, rel=1e-5)
+    s = r[0]["slabs"]
+    assert s["a"].shape == (2, 2, 3) and bool((s["a"][1] == 1).all()) and bool((s["a"][0] == 0).all())
+    assert s["b"].dtype == torch.float64 and float(s["b"][1, 0]) == 1.5
+    assert r[1]["slabs"] is None

@@ -166,3 +166,25 @@ def test_fused_policy_kernel_matches_torch_policy(M):
         counts.scatter_add_(1, act.long().unsqueeze(1), torch.ones(8, 1, n, device=env.device))
     freq = counts / R
     assert float((freq - pm_t).abs().mean()) < 0.01
+
+
+def test_eager_and_fused_draws_share_the_counter_hash(M):
+    """Both policy paths draw with the (seed, global env id, step, agent) counter hash: with the
+    same key the sampled actions agree except where the probabilities differ by rounding right
+    at a CDF step; a shard's draws (env_id_base) are the big handle's for the same global ids."""
+    A, V = M["A"], M["V"]
+    n = 512
+    env = V.FJSPVecEnv(n, env_id_base=3 * n)
+    learner = A.VecMultiAgentA2C(env, batch_size=8, seed=21, use_graph=False)
+    learner.reset(num_orders=25)
+    feats, masks = env.pack_a2c()
+    act = torch.zeros(8, n, dtype=torch.uint8, device=env.device)
+    val = torch.zeros(n, dtype=torch.float32, device=env.device)
+    learner._rng.fill_(learner._rng_host)
+    learner.policy_fused(feats, masks, 7, False, act, val)
+    act_t = learner.policy(feats, masks, deterministic=False, t=7)[0]
+    torch.cuda.synchronize()
+    assert float((act.long() == act_t).float().mean()) > 0.999
+    u_shard = A.counter_uniform(learner._rng_host, torch.arange(3 * n, 4 * n), 7, "cpu")
+    u_big = A.counter_uniform(learner._rng_host, torch.arange(0, 4 * n), 7, "cpu")
+    assert torch.equal(u_shard, u_big[..., 3 * n:])
