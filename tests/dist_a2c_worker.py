@@ -23,22 +23,22 @@ def flat(L):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--n", type=int, required=True)
-    ap.add_argument("--batch", type=int, required=True)
-    ap.add_argument("--batches", type=int, default=2)
-    ap.add_argument("--exchange", default="allreduce")
-    ap.add_argument("--out", required=True)
+    ap.add_argument("--shard-envs", type=int, required=True)
+    ap.add_argument("--shard-batch", type=int, required=True)
+    ap.add_argument("--shard-batches", type=int, default=2)
+    ap.add_argument("--shard-exchange", default="allreduce")
+    ap.add_argument("--shard-out", required=True)
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     V = importlib.import_module("multi-agent-rl-for-fjsp_amd.vec_env")
     A = importlib.import_module("multi-agent-rl-for-fjsp_amd.a2c_vec")
-    env = V.FJSPVecEnv(a.n, device="cuda:0", env_id_base=rank * a.n)
-    L = A.VecMultiAgentA2C(env, batch_size=a.batch, seed=5, group=dist.group.WORLD, exchange=a.exchange)
+    env = V.FJSPVecEnv(a.shard_envs, device="cuda:0", env_id_base=rank * a.shard_envs)
+    L = A.VecMultiAgentA2C(env, batch_size=a.shard_batch, seed=5, group=dist.group.WORLD, exchange=a.shard_exchange)
     L.reset(num_orders=25)
     first = None
-    for i in range(a.batches):
+    for i in range(a.shard_batches):
         L.collect()
         if i == 0:
             b = L._bufs
@@ -52,7 +52,7 @@ def main():
     torch.save({"first": first, "params1": params1, "params": flat(L), "critic": L.critic_loss_history,
                 "actor": [L.actor_loss_history[k] for k in A.AGENTS],
                 "exchange_bytes": L.exchange_bytes_per_batch()},
-               os.path.join(a.out, f"rank{rank}.pt"))
+               os.path.join(a.shard_out, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 

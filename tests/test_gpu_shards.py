@@ -125,7 +125,8 @@ def test_two_rank_a2c_equals_single_learner(G, tmp_path, exchange):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(REPO, "tests", "dist_a2c_worker.py"),
-           "--n", str(n), "--batch", str(T), "--batches", "2", "--exchange", exchange, "--out", str(tmp_path)]
+           "--shard-envs", str(n), "--shard-batch", str(T), "--shard-batches", "2", "--shard-exchange", exchange,
+           "--shard-out", str(tmp_path)]
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     ranks = [torch.load(tmp_path / f"rank{k}.pt", weights_only=True) for k in range(2)]
