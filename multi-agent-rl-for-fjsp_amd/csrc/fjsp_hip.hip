@@ -34,18 +34,12 @@ constexpr int MT_N = 624;
 __device__ unsigned long long g_stamps[8];
 __device__ unsigned long long g_pgstamps[4];   // pre-draw wave: busy cycles, active steps, busy in active steps, steps
 __device__ unsigned long long g_emitstamps[4];   // emit waves 1, 2: busy cycles, steps
-__device__ unsigned long long g_agstamps[56];   // k_step_ag (scripts/diag_ag_stamps.py)   // k_step_ag: per wave [busy, wait] cycles, epochs
+__device__ unsigned long long g_agstamps[64];   // k_step_ag (scripts/diag_ag_stamps.py)   // k_step_ag: per wave [busy, wait] cycles, epochs
 #define AG_T0() const uint64_t _ag_t0 = __builtin_amdgcn_s_memtime()
 #define AG_ACC(v) ((v) += __builtin_amdgcn_s_memtime() - _ag_t0)
 #else
 #define AG_T0() ((void)0)
 #define AG_ACC(v) ((void)0)
-#endif
-#ifdef FJSP_X_DEBUG   // bring-up build only: per-lane values of workgroup 1, step 0
-__device__ uint32_t g_dbg[8][64];
-#define FJSP_DBG(i, v) do { if (blockIdx.x == 1) g_dbg[i][lane] = (v); } while (0)
-#else
-#define FJSP_DBG(i, v) ((void)0)
 #endif
 
 struct DevState {
@@ -243,11 +237,7 @@ __device__ __forceinline__ void env_reset_predrawn(Env& E, const Tables& T, cons
 // Auto-reset inside the step kernels is a cold path (once per ~200 steps): a non-inlined call
 // keeps the MT reader's registers out of the hot loop's allocation.  Everything is passed and
 // returned by value so the env state never has its address taken (it stays in VGPRs).
-#ifdef FJSP_RESET_INLINE
-__device__ __forceinline__
-#else
 __device__ __attribute__((noinline))
-#endif
 Env env_reset_cold(Env E, Tables T, Cfg C, DevState S, int e, int num_orders, bool clear_pg = true) {
     env_reset(E, T, C, S, e, num_orders, clear_pg);
     return E;
@@ -498,12 +488,18 @@ __device__ __forceinline__ void step_and_emit(Env& E, const Tables& T, const Cfg
 template <bool CANON>
 __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t* __restrict__ actions, uint64_t order_packed,
                                                 int autoreset, fjsp_out out) {
+#ifdef FJSP_STAMPS
+    const uint64_t t_entry = __builtin_amdgcn_s_memtime();
+#endif
     __shared__ double s_lut[RLUT_SIZE];
     for (int i = threadIdx.x; i < RLUT_SIZE; i += BLOCK) s_lut[i] = C.lut[i];
     __syncthreads();
     C.lut = s_lut;
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     if (e >= S.n) return;
+#ifdef FJSP_STAMPS
+    const uint64_t t_lut = __builtin_amdgcn_s_memtime();
+#endif
     Tables T = tables_of(S, e);
     Env E;
     env_load(E, S.words, S.n, e);
@@ -513,8 +509,22 @@ __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t
     uint8_t order[NA];
 #pragma unroll
     for (int i = 0; i < NA; i++) order[i] = (uint8_t)(order_packed >> (8 * i));
+#ifdef FJSP_STAMPS   // slots: 0 entry -> LUT -> state + action loads landed, 1 action phase, 2 run,
+                     // 3 rewards, 4 observe, 5 term / trunc / status, 6 auto-reset + next obs, 7 state store drained
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int i = 0; i < 8; i++) E.st_acc[i] = 0;
+    E.st_t0 = __builtin_amdgcn_s_memtime();
+    E.st_acc[0] = E.st_t0 - t_entry;
+    (void)t_lut;
+#endif
     step_and_emit<CANON>(E, T, C, S, e, act, order, autoreset, out, 0);
     env_store(E, S.words, S.n, e);
+#ifdef FJSP_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FJSP_STAMP_AT(E, 7);
+    if (threadIdx.x == 0)
+        for (int i = 0; i < 8; i++) atomicAdd((unsigned long long*)&g_stamps[i], (unsigned long long)E.st_acc[i]);
+#endif
 }
 
 // The env's order table and used tray-slot prefix into LDS tables (one lane per env): the
@@ -684,15 +694,9 @@ __device__ __forceinline__ uint32_t pack_actions(const int* act, int lo) {
 // posts its episode counter, num_orders and cursor word, the pre-draw wave whether its table
 // is ready for that episode counter and the cursor word after it.  A finished table outlives
 // the launch (W[PGW], S.nxt); every other reset path clears it.
-#ifndef FJSP_PG_CR
-#define FJSP_PG_CR 1   // pre-draw work per step: MT rows copied (whole wave) ...
-#endif
-#ifndef FJSP_PG_PB
-#define FJSP_PG_PB 8   // ... and words drawn per env
-#endif
-#ifndef FJSP_AG_PB
-#define FJSP_AG_PB 4   // words drawn per env per step in k_step_ag
-#endif
+constexpr int PG_CR = 1;   // pre-draw work per step: MT rows copied (whole wave) ...
+constexpr int PG_PB = 8;   // ... and words drawn per env
+constexpr int AG_PB = 4;   // words drawn per env per step in k_step_ag
 // The pre-draw wave (k_step_pipe<..., PG>, k_step_ag): see the comment above k_step_pipe.
 // s_mb / s_cp / s_nxt are the kernel's LDS mailboxes, row-copy staging and next tables.
 // FINAL_MB: the sim side also posts in the final epoch K (k_step_ag resets at the top of an
@@ -751,11 +755,7 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
                 g = (int)((sw >> 16) & 0x3FFu);
                 d = OrderDraw{0, 0, 0, 0, 0u};
                 pf_pa = -1;
-#ifdef FJSP_PG_IDLE
-                ph = 0;   // diagnostic: the pre-draw wave only keeps the mailboxes
-#else
                 ph = nord > 0 ? 1 : 3;
-#endif
             }
         }
         // Copy the live rows of up to CR envs that start a pre-draw (the whole wave, one
@@ -925,11 +925,11 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
     static_assert(!PG || LDS, "the pre-drawn tables live in LDS");
     // pre-draw work per step (sized so the wave stays off the critical path): rows copied by
     // the whole wave (CR envs, 1 KB per load), words drawn per env
-    constexpr int CR = FJSP_PG_CR, PB = FJSP_PG_PB;
+    constexpr int CR = PG_CR, PB = PG_PB;
     __shared__ uint32_t s_orders[LDS ? MAX_ORDERS * BLOCK : 1];
     __shared__ uint32_t s_nxt[PG ? MAX_ORDERS * BLOCK : 1];
     __shared__ uint32_t s_mb[PG ? 4 : 1][2][BLOCK];   // sim: epi | nord << 8, cursor word; pre-draw: ready, cursor
-    __shared__ uint4 s_cp[PG ? FJSP_PG_CR : 1][3][BLOCK];   // MT rows in flight (pre-draw copies)
+    __shared__ uint4 s_cp[PG ? PG_CR : 1][3][BLOCK];   // MT rows in flight (pre-draw copies)
     // Pickup + AGV ahead (PG, uniform-random actions).  Neither agent's next action depends on
     // anything the packaging agents or the run phase of the current step change, except where
     // a drop at packaging routes the tray (deferred: agv_pack_drop).  So after the machines'
@@ -1124,11 +1124,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
                 s_act[(k + 1) & 1][0][lane] = pack_actions(act_next, 0);
                 s_act[(k + 1) & 1][1][lane] = pack_actions(act_next, 4);
             }
-#ifdef FJSP_X_NOEMIT   // diagnostic timing build only: the emit waves write no outputs
-            const bool have = false;
-#else
             const bool have = k > 0 && valid;
-#endif
             const uint32_t t = (uint32_t)(k - 1);
             uint32_t v[SNAP_N];
             Env E;
@@ -1266,36 +1262,19 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
 // Waves w and w + 4 share a SIMD (two waves per SIMD issue VALU at twice one wave's rate): K
 // shares AM's (both busy early in the step; AM has the higher priority), P (the critical path
 // after AM's post, higher priority) shares the lightest emit wave's, PD and E3 pair up.
-#ifndef FJSP_AG_LAYOUT   // wave of each role: AM, P, E1, E2, K, E0, PD, E3 (waves w and w + 4 share a SIMD):
-                         // AM+PD, P+E0, E1+K, E2+E3 (0.6 % faster than AM+K, E1+PD: scripts/gpu_variants.sh)
-#define FJSP_AG_LAYOUT 0, 1, 2, 3, 6, 5, 4, 7
-#endif
-constexpr int AG_LAYOUT[8] = {FJSP_AG_LAYOUT};
+// wave of each role: AM, P, E1, E2, K, E0, PD, E3 (waves w and w + 4 share a SIMD): AM+PD, P+E0,
+// E1+K, E2+E3 (0.6 % faster than AM+K, E1+PD; other pairings measured within noise)
+constexpr int AG_LAYOUT[8] = {0, 1, 2, 3, 6, 5, 4, 7};
 constexpr int AG_AM = AG_LAYOUT[0], AG_P = AG_LAYOUT[1], AG_E1 = AG_LAYOUT[2], AG_E2 = AG_LAYOUT[3], AG_K = AG_LAYOUT[4],
               AG_E0 = AG_LAYOUT[5], AG_PD = AG_LAYOUT[6], AG_E3 = AG_LAYOUT[7], AG_WAVES = 8;
 // packaging-owned state words (K): W1, W13..W16 (packaging run lists), W20..W29
 constexpr uint32_t K_WORDS = (1u << 1) | (0xFu << 13) | (0x3FFu << 20);
 // masks per emit wave: pickup [0,3) | the AGV's pickup / drop [9,11) | the AGV's moves [3,9),
 // machines [11,17), packaging [17,29)
-#ifndef FJSP_AG_E1MASKS
-#define FJSP_AG_E1MASKS 0u
-#endif
-#ifndef FJSP_AG_E0MASKS   // masks E0 takes over from E3
-#define FJSP_AG_E0MASKS 0u
-#endif
-#ifndef FJSP_AG_E0I8      // int8 fields E0 takes over from E2
-#define FJSP_AG_E0I8 0u
-#endif
-#ifndef FJSP_AG_E1I8      // int8 fields E1 takes over from E2
-#define FJSP_AG_E1I8 0u
-#endif
-constexpr uint32_t AG_MASKS_E0 = 0x7u | FJSP_AG_E0MASKS, AG_MASKS_E2 = 0x3u << 9, AG_MASKS_E1 = FJSP_AG_E1MASKS,
-                   AG_MASKS_E3 = ((0x3Fu << 3) | (0x3FFFFu << 11)) & ~AG_MASKS_E1 & ~AG_MASKS_E0;
-constexpr uint32_t AG_I8_E0 = FJSP_AG_E0I8, AG_I8_E1 = FJSP_AG_E1I8, AG_I8_E2 = ((1u << NI8) - 1u) & ~AG_I8_E0 & ~AG_I8_E1;
-static_assert(!(AG_I8_E0 & AG_I8_E1), "int8 split");
-static_assert((AG_MASKS_E0 | AG_MASKS_E1 | AG_MASKS_E2 | AG_MASKS_E3) == (1u << NMASK) - 1u &&
-              !(AG_MASKS_E0 & AG_MASKS_E2) && !(AG_MASKS_E0 & AG_MASKS_E3) && !(AG_MASKS_E2 & AG_MASKS_E3) &&
-              !(AG_MASKS_E1 & (AG_MASKS_E0 | AG_MASKS_E2)), "mask split");
+// (other splits of the fields over the emit waves measured within 1 %)
+constexpr uint32_t AG_MASKS_E0 = 0x7u, AG_MASKS_E2 = 0x3u << 9, AG_MASKS_E3 = (0x3Fu << 3) | (0x3FFFFu << 11);
+static_assert((AG_MASKS_E0 | AG_MASKS_E2 | AG_MASKS_E3) == (1u << NMASK) - 1u && !(AG_MASKS_E0 & AG_MASKS_E2) &&
+              !(AG_MASKS_E0 & AG_MASKS_E3) && !(AG_MASKS_E2 & AG_MASKS_E3), "mask split");
 // snapshot slot words (PipeSnap, 32 per lane): AM writes q[0..3], K q[4..7]
 enum : int { SA_W0 = 0, SA_ST, SA_W4, SA_W5, SA_W6, SA_L0, SA_M0 = SA_L0 + 6, SA_M1, SA_R01, SA_R23,
              SK_W1 = 16, SK_P0, SK_N0 = SK_P0 + 4, SK_ST = SK_N0 + 4, SK_G, SK_R45, SK_R67 };
@@ -1363,16 +1342,16 @@ __device__ __forceinline__ void ag_emit(int part, const uint32_t* v, uint32_t t,
                      g8 + C.lut[reward_index(a, r & 0xFFu, (int)((r >> 8) & 0xFu))]);
             }
         }
-        FieldSink<0u, AG_I8_E0, 0u, AG_MASKS_E0> ps{sink};
+        FieldSink<0u, 0u, 0u, AG_MASKS_E0> ps{sink};
         observe(E, C, ps);
     } else if (part == 1) {
-        FieldSink<(1u << NI32) - 1u, AG_I8_E1, (1u << NF32) - 1u, AG_MASKS_E1> ps{sink};
+        FieldSink<(1u << NI32) - 1u, 0u, (1u << NF32) - 1u, 0u> ps{sink};
         observe(E, C, ps);
     } else if (part == 3) {
         FieldSink<0u, 0u, 0u, AG_MASKS_E3> ps{sink};
         observe(E, C, ps);
     } else {
-        FieldSink<0u, AG_I8_E2, 0u, AG_MASKS_E2> ps{sink};
+        FieldSink<0u, (1u << NI8) - 1u, 0u, AG_MASKS_E2> ps{sink};
         observe(E, C, ps);
         const int nord = E.norders();
         const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
@@ -1383,65 +1362,18 @@ __device__ __forceinline__ void ag_emit(int part, const uint32_t* v, uint32_t t,
     }
 }
 
-// Emit workgroups (k_step_ag<..., emit-wg>): the core workgroup's publisher wave (E1) copies
-// each step's snapshot to a global slot and raises the core's published-step count; an emit
-// workgroup of its own (grid blocks ncore..2*ncore-1, on another CU) turns the snapshots into
-// the outputs, so the output stores neither hold up the core's barrier nor share its LDS and
-// SIMDs.  The hand-off is the guide's sc1 form (MI355X_MICROARCH.md, inter-workgroup
-// visibility, first row): every snapshot byte is stored with 8-byte sc1 (write-through) stores,
-// the publisher waits vmcnt(0) for them before ONE lane's sc1 store of the count, the consumer
-// polls it with sc1 loads and reads the bytes with sc1 loads only.  Placement-independent; the
-// launch uses it only when every block of the grid has a CU of its own (co-resident, no
-// deadlock: a core never waits on an emitter).
-struct AgEmit {
-    uint64_t* snap;    // [K][ncore][SNAP_N / 2][BLOCK] snapshot words in pairs; null: emit in the core
-    uint32_t* count;   // [ncore * 32]: base + steps published by core c (one 128-byte line each)
-    int ncore;
-    uint32_t base;     // this launch's count origin (above every count an earlier launch left)
-};
-constexpr int AG_COUNT_STRIDE = 32;
-
-// An emit workgroup's 8 waves: wave w emits role w % 4 of the steps t = w / 4 (mod 2).
-__device__ __forceinline__ void ag_emitter(const AgEmit& X, int core, int wave, int lane, int K, uint32_t n,
-                                           const Cfg& C, const fjsp_out& out) {
-    const uint32_t ue = (uint32_t)(core * BLOCK + lane);
-    const bool valid = ue < n;
-    const int part = wave & 3;
-    uint32_t* cnt = X.count + (size_t)core * AG_COUNT_STRIDE;
-    int avail = 0;
-    for (int t = wave >> 2; t < K; t += 2) {
-        // bounded: the core always finishes (it waits on no emitter); ~0.3 s of polling
-        for (int spin = 0; avail <= t && spin < (1 << 21); spin++) {
-            avail = (int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - X.base);   // sc1 poll
-            if (avail <= t) __builtin_amdgcn_s_sleep(2);
-        }
-        if (avail <= t) return;
-        if (!valid) continue;
-        const uint64_t* src = X.snap + ((size_t)t * X.ncore + core) * (SNAP_N / 2) * BLOCK + lane;
-        uint32_t v[SNAP_N];
-#pragma unroll
-        for (int j = 0; j < SNAP_N / 2; j++) {
-            const uint64_t x = __hip_atomic_load(src + j * BLOCK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1
-            v[2 * j] = (uint32_t)x;
-            v[2 * j + 1] = (uint32_t)(x >> 32);
-        }
-        ag_emit(part, v, (uint32_t)t, n, ue, C, out);
-    }
-}
-
 __device__ __forceinline__ void ag_spin(uint32_t* flag, uint32_t v) {
-#ifdef FJSP_AG_TIGHT_SPIN
-    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) {}
-#else
     while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
-#endif
 }
 
 __global__ void __launch_bounds__(AG_WAVES * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2)))
-k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0, int autoreset, fjsp_out out, AgEmit X) {
+k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0, int autoreset, fjsp_out out) {
+#ifdef FJSP_STAMPS
+    const uint64_t t_entry = __builtin_amdgcn_s_memtime();
+#endif
     // pre-draw work per step: the draw costs more than its loads' latency here (PD shares its
     // SIMD with E0), so four words per step (~33 steps for 30 orders) beat eight (measured)
-    constexpr int CR = FJSP_PG_CR, PB = FJSP_AG_PB;
+    constexpr int CR = PG_CR, PB = AG_PB;
     __shared__ uint32_t s_orders[MAX_ORDERS * BLOCK];
     __shared__ uint32_t s_nxt[MAX_ORDERS * BLOCK];
     __shared__ uint32_t s_mb[4][2][BLOCK];   // AM <-> PD mailboxes (predraw_wave)
@@ -1465,11 +1397,6 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     C.lut = s_lut;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / BLOCK);
     const int lane = threadIdx.x % BLOCK;
-    if (X.snap && (int)blockIdx.x >= X.ncore) {   // an emit workgroup
-        __syncthreads();   // s_lut
-        ag_emitter(X, (int)blockIdx.x - X.ncore, wave, lane, K, (uint32_t)S.n, C, out);
-        return;
-    }
     const int e = blockIdx.x * BLOCK + lane;
     const bool valid = e < S.n;
     const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
@@ -1551,6 +1478,9 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         }
     }
     __syncthreads();
+#ifdef FJSP_STAMPS   // [56] launch prologue (entry -> tables in LDS), summed over workgroups
+    if (threadIdx.x == 0) atomicAdd(&g_agstamps[56], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_entry));
+#endif
     if (wave == AG_AM) {
         __builtin_amdgcn_s_setprio(3);   // the machines -> AGV chain is the critical path
         Env E;
@@ -1821,17 +1751,8 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         // E0 shares P's SIMD)
         const int part = wave == AG_E0 ? 0 : wave == AG_E1 ? 1 : wave == AG_E2 ? 2 : 3;
         if (part == 3) __builtin_amdgcn_s_setprio(2);   // E3 runs the pickup station for P first
-#ifdef FJSP_AG_EMIT_PRIO
-        __builtin_amdgcn_s_setprio(FJSP_AG_EMIT_PRIO);
-#endif
         for (int k = 0; k <= K; k++) {
             AG_T0();
-            if (X.snap && part == 1 && k >= 2) {   // the publisher: steps < k-1 are stored (epochs < k)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0)
-                    __hip_atomic_store(X.count + (size_t)blockIdx.x * AG_COUNT_STRIDE, X.base + (uint32_t)(k - 1), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            }
             if (part == 3 && k + 1 < K) {   // step k+1's pickup station, from P's AGV result of step k
                 const bool fresh = ag_fresh(k, valid, s_p1, s_kpost, lane, C, autoreset);
                 if (__ballot(valid && fresh) != 0) ag_spin(&s_flag1, (uint32_t)(k + 1));
@@ -1863,14 +1784,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 s_act[(k + 2) % 3][0][lane] = pack_actions(act, 0);
                 s_act[(k + 2) % 3][1][lane] = pack_actions(act, 4);
             }
-#ifdef FJSP_AG_EMIT_DELAY   // experiment: let the core waves' step-top LDS reads go first
-            __builtin_amdgcn_s_sleep(FJSP_AG_EMIT_DELAY);
-#endif
-#ifdef FJSP_X_NOEMIT   // diagnostic timing build only: no outputs
-            if (false) {
-#else
             if (k > 0 && valid) {
-#endif
                 const uint32_t t = (uint32_t)(k - 1);
                 uint32_t v[SNAP_N];
                 snap_get(snap[(k - 1) & 1], lane, v);
@@ -1878,27 +1792,17 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the snapshot arrived
 #endif
                 AG_MARK(1);
-                if (!X.snap) ag_emit(part, v, t, n, ue, C, out);
-                else if (part == 1) {   // the publisher: the step's snapshot to its global slot
-                    uint64_t* dst = X.snap + ((size_t)t * X.ncore + blockIdx.x) * (SNAP_N / 2) * BLOCK + lane;
-#pragma unroll
-                    for (int j = 0; j < SNAP_N / 2; j++)
-                        __hip_atomic_store(dst + j * BLOCK, (uint64_t)v[2 * j] | ((uint64_t)v[2 * j + 1] << 32),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1 (write-through)
-                }
+                ag_emit(part, v, t, n, ue, C, out);
             }
             AG_MARK(2);
             AG_ACC(ag_busy);
             AG_BARRIER();
         }
-        if (X.snap && part == 1) {   // all K steps stored
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0)
-                __hip_atomic_store(X.count + (size_t)blockIdx.x * AG_COUNT_STRIDE, X.base + (uint32_t)K, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
     __syncthreads();
+#ifdef FJSP_STAMPS
+    const uint64_t t_out = __builtin_amdgcn_s_memtime();
+#endif
     if (valid) {   // the order table and the used slot prefix back to HBM, rows r = wave (mod 8)
         const uint32_t no = s_act[0][0][lane], ns = s_act[0][1][lane];
         for (uint32_t o = (uint32_t)wave; o < no; o += AG_WAVES) S.orders[(size_t)o * n + e] = TL.orders[o * BLOCK];
@@ -1917,6 +1821,11 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     if (lane == 0 && blockIdx.x == 0) {   // SIMD of each role (HW_REG_HW_ID bits 5:4)
         const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
         atomicOr(&g_agstamps[17], (unsigned long long)((hw >> 4) & 3u) << (4 * slot));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0 && wave == AG_AM) {   // [57] copy-out drained, [58] entry -> end (AM's wave)
+        atomicAdd(&g_agstamps[57], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_out));
+        atomicAdd(&g_agstamps[58], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_entry));
     }
     if (lane == 0 && wave != AG_PD) {
         atomicAdd(&g_agstamps[2 * slot], (unsigned long long)ag_busy);
@@ -1986,12 +1895,6 @@ struct fjsp_handle {
     int use_pipe;    // two-wave pipelined k_step_many for lean outputs (FJSP_PIPE / fjsp_set_option)
     int use_pg;      // pre-draw wave in the pipelined kernel (FJSP_PREDRAW / fjsp_set_option "predraw")
     int use_ag;      // agent-group pipeline k_step_ag for uniform-random actions (FJSP_AGENTS / "agents")
-    int use_emit_wg; // k_step_ag's outputs from emit workgroups of their own (FJSP_EMIT_WG / "emit_wg")
-    int num_cu;      // compute units of the device (emit workgroups need a CU per block)
-    uint64_t* ag_snap;      // k_step_ag snapshot slots (AgEmit::snap), grown on demand
-    size_t ag_snap_bytes;
-    uint32_t* ag_count;     // AgEmit::count, one 128-byte line per core workgroup
-    uint32_t ag_base;       // the largest count a launch can have left there
     const char* last_kernel;   // name of the last step kernel launched (fjsp_last_kernel)
     uint32_t env_id_base;      // global id of env 0 (fjsp_set_option "env_id_base")
 };
@@ -2114,14 +2017,6 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
         h->use_pg = pd ? atoi(pd) : 1;
         const char* ag = getenv("FJSP_AGENTS");
         h->use_ag = ag ? atoi(ag) : 1;
-        const char* ew = getenv("FJSP_EMIT_WG");
-        h->use_emit_wg = ew ? atoi(ew) : 0;   // measured slower at 4096 envs: opt-in
-        h->ag_snap = nullptr;
-        h->ag_snap_bytes = 0;
-        h->ag_count = nullptr;
-        h->ag_base = 0;
-        h->num_cu = 0;
-        if (hipDeviceGetAttribute(&h->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) h->num_cu = 0;
     }
     h->dcfg.step_size = c.step_size;
     h->dcfg.max_steps = c.max_episode_steps;
@@ -2161,10 +2056,6 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     if (e != hipSuccess) { h->ev1 = nullptr; return bail("hipEventCreate", e); }
     e = hipMalloc(&h->lut_dev, sizeof(double) * RLUT_SIZE);
     if (e != hipSuccess) { h->lut_dev = nullptr; return bail("hipMalloc(reward table)", e); }
-    e = hipMalloc(&h->ag_count, (n + BLOCK - 1) / BLOCK * AG_COUNT_STRIDE * sizeof(uint32_t));
-    if (e != hipSuccess) { h->ag_count = nullptr; return bail("hipMalloc(emit counts)", e); }
-    e = hipMemsetAsync(h->ag_count, 0, (n + BLOCK - 1) / BLOCK * AG_COUNT_STRIDE * sizeof(uint32_t), h->stream);
-    if (e != hipSuccess) return bail("hipMemset(emit counts)", e);
     h->dcfg.lut = h->lut_dev;
     {
         fjsp_reward_weights w;
@@ -2191,8 +2082,6 @@ int fjsp_destroy(fjsp_handle* h) {
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->lut_dev) (void)hipFree(h->lut_dev);
     if (h->base) (void)hipFree(h->base);
-    if (h->ag_count) (void)hipFree(h->ag_count);
-    if (h->ag_snap) (void)hipFree(h->ag_snap);
     delete h;
     return 0;
 }
@@ -2204,7 +2093,6 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
     if (!strcmp(name, "pipeline")) { h->use_pipe = value != 0; return 0; }
     if (!strcmp(name, "predraw")) { h->use_pg = value != 0; return 0; }
     if (!strcmp(name, "agents")) { h->use_ag = value != 0; return 0; }
-    if (!strcmp(name, "emit_wg")) { h->use_emit_wg = value != 0; return 0; }
     if (!strcmp(name, "timing")) { h->timing = value != 0; if (!h->timing) h->timed = 0; return 0; }
     if (!strcmp(name, "env_id_base")) {
         // the handle is shard [value, value + n) of a larger job: env e's default stream becomes
@@ -2309,38 +2197,7 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
     const bool pg = h->use_pg && lds && two_emit && autoreset;
     // the agent-group pipeline: state-independent (uniform-random) actions, LDS tables, pre-draw
     const bool ag = h->use_ag && h->use_pipe && !full && !staged && pg && action_mode == FJSP_ACTIONS_UNMASKED;
-    // k_step_ag's emit workgroups: one more block per core block, each on a CU of its own
-    const int ncore = (int)grid.x;
-    bool ewg = ag && h->use_emit_wg && h->num_cu > 0 && 2 * ncore <= h->num_cu;
-    const size_t snap_bytes = (size_t)K * (size_t)ncore * (SNAP_N / 2) * BLOCK * sizeof(uint64_t);
-    if (ewg && snap_bytes > h->ag_snap_bytes) {
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        HIPCHK(hipStreamIsCapturing(h->stream, &cs));
-        if (cs != hipStreamCaptureStatusNone) {
-            ewg = false;   // no allocation while a graph is being captured: emit in the core
-        } else {
-            if (h->ag_snap) {
-                HIPCHK(hipStreamSynchronize(h->stream));
-                HIPCHK(hipFree(h->ag_snap));
-                h->ag_snap = nullptr;
-                h->ag_snap_bytes = 0;
-            }
-            HIPCHK(hipMalloc(&h->ag_snap, snap_bytes));
-            h->ag_snap_bytes = snap_bytes;
-        }
-    }
-    AgEmit X{nullptr, nullptr, ncore, 0u};
-    if (ewg) {
-        if ((uint64_t)h->ag_base + (uint64_t)K + 1 >= (1ull << 31)) {   // restart the counts (rare)
-            HIPCHK(hipMemsetAsync(h->ag_count, 0, (size_t)ncore * AG_COUNT_STRIDE * sizeof(uint32_t), h->stream));
-            h->ag_base = 0;
-        }
-        X.snap = h->ag_snap;
-        X.count = h->ag_count;
-        X.base = h->ag_base + 1u;
-        h->ag_base += (uint32_t)K + 1u;
-    }
-    h->last_kernel = ag ? (ewg ? "k_step_ag<lds,predraw,emit-wg>" : "k_step_ag<lds,predraw>")
+    h->last_kernel = ag ? "k_step_ag<lds,predraw>"
                    : (h->use_pipe && !full && !staged)
                          ? (lds ? (two_emit ? (pg ? "k_step_pipe<lds,2emit,predraw>" : "k_step_pipe<lds,2emit>")
                                             : "k_step_pipe<lds,1emit>")
@@ -2349,8 +2206,8 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
                    : staged ? (lds ? "k_step_many<lds,staged>" : "k_step_many<staged>")
                    : (lds ? "k_step_many<lds>" : "k_step_many");
     if (ag) {
-        hipLaunchKernelGGL(k_step_ag, dim3(ewg ? 2 * ncore : ncore), dim3(AG_WAVES * BLOCK), 0, h->stream, h->S, h->dcfg,
-                           K, action_seed, env_gid0, step0, autoreset, o, X);
+        hipLaunchKernelGGL(k_step_ag, grid, dim3(AG_WAVES * BLOCK), 0, h->stream, h->S, h->dcfg,
+                           K, action_seed, env_gid0, step0, autoreset, o);
     } else if (h->use_pipe && !full && !staged) {
         // a second emit wave pays while the CUs are not full (N <= 16384 at 64 envs per CU)
         const bool two = two_emit;
@@ -2409,16 +2266,9 @@ extern "C" int fjsp_debug_stamps(unsigned long long* out) {
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)));
     return 0;
 }
-#ifdef FJSP_X_DEBUG
-extern "C" int fjsp_debug_dump(uint32_t* out) {
-    HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(uint32_t) * 8 * 64));
-    return 0;
-}
-#endif
 extern "C" int fjsp_debug_agstamps(unsigned long long* out) {   // out[16]: k_step_ag per wave busy / wait, epochs
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_agstamps), sizeof(unsigned long long) * 56));
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_agstamps), sizeof(unsigned long long) * 64));
     unsigned long long z[56] = {0};
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_agstamps), z, sizeof(z)));
     return 0;

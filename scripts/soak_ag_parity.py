@@ -1,4 +1,4 @@
-"""Soak: k_step_ag against k_step_pipe (and the emit-workgroup option) on larger and varied
+"""Soak: k_step_ag against k_step_pipe on larger and varied
 workloads than the unit tests: every lean output compared bit for bit, launch after launch.
 Prints one JSON line per case; exit status 1 on any mismatch."""
 import importlib, json, os, sys
@@ -18,11 +18,10 @@ CASES = [
 bad = 0
 for i, c in enumerate(CASES):
     runs = []
-    for agents, emit_wg in ((1, 0), (1, 1), (0, 0)):
+    for agents in (1, 0):
         env = G.make_env(c["n"], **c["cfg"])
         lib = G.native.lib()
         G.native.check(lib.fjsp_set_option(env.handle, b"agents", agents))
-        G.native.check(lib.fjsp_set_option(env.handle, b"emit_wg", emit_wg))
         env.reset(seeds=torch.arange(c["n"]) * 7 + i, num_orders=c["orders"])
         out, t = {k: [] for k in LEAN}, 0
         for k in c["chunks"]:

@@ -16,7 +16,6 @@ from tests import parity_util as P  # noqa: E402
 
 LEAN = ("obs_i32", "obs_i8", "obs_f32", "masks", "rewards", "term", "trunc", "status")
 AG = "k_step_ag<lds,predraw>"               # outputs from the core workgroup's emit waves (default)
-AG_EWG = "k_step_ag<lds,predraw,emit-wg>"   # outputs from emit workgroups (option "emit_wg")
 
 
 @pytest.fixture(scope="module")
@@ -27,12 +26,11 @@ def G():
     return gpu_util
 
 
-def _env(G, n, agents, pipeline=1, emit_wg=0, **cfg):
+def _env(G, n, agents, pipeline=1, **cfg):
     env = G.make_env(n, **cfg)
     lib = G.native.lib()
     G.native.check(lib.fjsp_set_option(env.handle, b"agents", agents))
     G.native.check(lib.fjsp_set_option(env.handle, b"pipeline", pipeline))
-    G.native.check(lib.fjsp_set_option(env.handle, b"emit_wg", emit_wg))
     return env
 
 
@@ -62,18 +60,17 @@ def _same_views(a, b):
 
 
 def test_agents_matches_other_kernels_and_oracle(G):
-    """1000 envs (a partial workgroup), 20 orders, launches of 1..200 steps: k_step_ag (outputs
-    from emit workgroups and from the core's emit waves) == k_step_pipe == k_step_many == the
+    """1000 envs (a partial workgroup), 20 orders, launches of 1..200 steps: k_step_ag == k_step_pipe == k_step_many == the
     oracle, and the state left behind is the same (a full-output step after it, the env views,
     the MT streams)."""
     n, seeds, chunks = 1000, np.arange(1000) * 3 + 1, [1, 37, 200, 5, 120, 2]
     runs = []
-    for agents, pipeline, emit_wg in ((1, 1, 0), (1, 1, 1), (0, 1, 0), (0, 0, 0)):
-        env = _env(G, n, agents, pipeline, emit_wg)
+    for agents, pipeline in ((1, 1), (0, 1), (0, 0)):
+        env = _env(G, n, agents, pipeline)
         env.reset(seeds=torch.from_numpy(seeds), num_orders=20)
         a = _chunks(G, env, chunks, seed=21)
         if agents:
-            assert env.last_kernel() == (AG_EWG if emit_wg else AG)
+            assert env.last_kernel() == AG
         tail = G.to_np(env.rollout(3, action_seed=21, step0=sum(chunks), policy="random", infos=True))
         runs.append((a, tail, _views(env, (0, 63, 64, 500, 999))))
     for a, tail, views in runs[1:]:
@@ -96,8 +93,8 @@ def test_agents_all_orders_done_resets(G):
     n, steps = 2048, 700
     seeds = np.arange(n) + 100
     runs = []
-    for agents, emit_wg in ((1, 0), (0, 0), (1, 1)):
-        env = _env(G, n, agents, emit_wg=emit_wg)
+    for agents in (1, 0):
+        env = _env(G, n, agents)
         env.reset(seeds=torch.from_numpy(seeds), num_orders=1)
         runs.append(_chunks(G, env, [300, 1, 399], seed=5))
     for r in runs[1:]:
@@ -160,17 +157,17 @@ def test_agents_staggered_masked_resets(G):
 
 
 def test_agents_full_size_invariants(G):
-    """The bench workload (4096 envs, 30 orders, 1000 steps in 200-step launches): emit
-    workgroups == the core's emit waves == k_step_pipe, plus sampled envs exact against the
+    """The bench workload (4096 envs, 30 orders, 1000 steps in 200-step launches):
+    k_step_ag == k_step_pipe, plus sampled envs exact against the
     oracle."""
     n = 4096
     runs = []
-    for agents, emit_wg in ((1, 0), (1, 1), (0, 0)):
-        env = _env(G, n, agents, emit_wg=emit_wg)
+    for agents in (1, 0):
+        env = _env(G, n, agents)
         env.reset(seeds=torch.arange(n), num_orders=30)
         runs.append(_chunks(G, env, [200] * 5, seed=0))
         if agents:
-            assert env.last_kernel() == (AG_EWG if emit_wg else AG)
+            assert env.last_kernel() == AG
     for r in runs[1:]:
         for k in LEAN:
             assert P.bits_equal(runs[0][k], r[k]), k
@@ -179,22 +176,6 @@ def test_agents_full_size_invariants(G):
         rec, _, _ = O.rollout(1, 1000, seeds=np.array([gid]), gid0=int(gid), num_orders=30, action_seed=0, policy=0)
         for k in ("obs_i32", "masks", "rewards"):
             assert P.bits_equal(runs[0][k][:, gid:gid + 1], rec[k]), (gid, k)
-
-
-def test_agents_emit_in_core_beyond_one_cu_per_block(G):
-    """Option emit_wg with more core workgroups than half the CUs (129 x 64 envs): no emit
-    workgroups (every block of the grid must have a CU of its own), the core's emit waves write
-    the outputs."""
-    n = 129 * 64
-    runs = []
-    for agents in (1, 0):
-        env = _env(G, n, agents, emit_wg=1)
-        env.reset(seeds=torch.arange(n) + 3, num_orders=5)
-        runs.append(_chunks(G, env, [40, 25], seed=2))
-        if agents:
-            assert env.last_kernel() == AG
-    for k in LEAN:
-        assert P.bits_equal(runs[0][k], runs[1][k]), k
 
 
 @pytest.mark.parametrize("n", [250, 1001])
