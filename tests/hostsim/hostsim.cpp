@@ -53,7 +53,7 @@ void* hs_create(const int32_t* c, int n) {
     return h;
 }
 void hs_destroy(void* p) {
-    HS* h = (HS*)p; free(h->E); free(h->orders); free(h->scode); free(h->snext); free(h->scstep); free(h->mt); free(h->mti); free(h);
+    HS* h = (HS*)p; free((void*)h->C.lut); free(h->E); free(h->orders); free(h->scode); free(h->snext); free(h->scstep); free(h->mt); free(h->mti); free(h);
 }
 static void reset_one(HS* h, int e, int num_orders) {
     Env& E = h->E[e]; Tables T = tabs(h, e);
