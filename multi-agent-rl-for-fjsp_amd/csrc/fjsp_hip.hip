@@ -234,10 +234,12 @@ __device__ __forceinline__ void env_reset_predrawn(Env& E, const Tables& T, cons
     E.set_mti((int)w3);
 }
 
-// Auto-reset inside the step kernels is a cold path (once per ~200 steps): a non-inlined call
-// keeps the MT reader's registers out of the hot loop's allocation.  Everything is passed and
-// returned by value so the env state never has its address taken (it stays in VGPRs).
-__device__ __attribute__((noinline))
+// Auto-reset inside the step kernels is a cold path (once per ~200 steps), taken in a branch.
+// Inlined: a call would need a stack frame in scratch memory (368 B per lane: the by-value
+// state and the callee-saved registers), and a kernel that uses scratch pays for its set-up
+// on every launch (measured: k_step 12.1 -> 7.9 us per launch in rocprof) and its allocation
+// raised every step kernel to 228+ VGPRs (157-233 inlined).
+__device__ __forceinline__
 Env env_reset_cold(Env E, Tables T, Cfg C, DevState S, int e, int num_orders, bool clear_pg = true) {
     env_reset(E, T, C, S, e, num_orders, clear_pg);
     return E;
@@ -492,20 +494,24 @@ __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t
     const uint64_t t_entry = __builtin_amdgcn_s_memtime();
 #endif
     __shared__ double s_lut[RLUT_SIZE];
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    const bool valid = e < S.n;
+    // the state and action loads are issued before the reward table's: one HBM round trip
+    Env E;
+    int act[NA];
+    if (valid) {
+        env_load(E, S.words, S.n, e);
+#pragma unroll
+        for (int a = 0; a < NA; a++) act[a] = actions[a * S.n + e];
+    }
     for (int i = threadIdx.x; i < RLUT_SIZE; i += BLOCK) s_lut[i] = C.lut[i];
     __syncthreads();
     C.lut = s_lut;
-    const int e = blockIdx.x * BLOCK + threadIdx.x;
-    if (e >= S.n) return;
+    if (!valid) return;
 #ifdef FJSP_STAMPS
     const uint64_t t_lut = __builtin_amdgcn_s_memtime();
 #endif
     Tables T = tables_of(S, e);
-    Env E;
-    env_load(E, S.words, S.n, e);
-    int act[NA];
-#pragma unroll
-    for (int a = 0; a < NA; a++) act[a] = actions[a * S.n + e];
     uint8_t order[NA];
 #pragma unroll
     for (int i = 0; i < NA; i++) order[i] = (uint8_t)(order_packed >> (8 * i));
@@ -705,7 +711,7 @@ constexpr int AG_PB = 4;   // words drawn per env per step in k_step_ag
 // each MT refill is loaded a step ahead: their latency hides behind the barrier instead of
 // the step (plain loads; an LDS DMA would be drained by the barrier's fence).  s_cp unused.
 template <int CR, int PB, bool FINAL_MB = false, bool ASYNC = false>
-__device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane, int e, bool valid,
+__device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane, int e, bool valid, size_t ebase,
                                              uint32_t (*s_mb)[2][BLOCK], uint4 (*s_cp)[3][BLOCK], uint32_t* s_nxt) {
     const uint32_t n = (uint32_t)S.n;
     // the pre-draw wave: 0 idle, 1 copying the live row, 2 drawing, 3 table ready
@@ -817,7 +823,7 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
                 const int pb = (k - 1) & 1;
 #pragma unroll
                 for (int r = 0; r < CR; r++) {
-                    const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls_prev[r];
+                    const size_t el = ebase + (size_t)ls_prev[r];
                     uint4* rd = reinterpret_cast<uint4*>(S.mt + ((size_t)(sl_prev[r] ^ 1u) * n + el) * MT_N);
                     rd[lane] = cp0;
                     rd[lane + 64] = cp1;
@@ -839,7 +845,7 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
                     ls_prev[r] = need ? __builtin_ctzll(need) : first;
                     need &= need - 1;
                     sl_prev[r] = (uint32_t)__builtin_amdgcn_readlane((int)src, ls_prev[r]);
-                    const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls_prev[r];
+                    const size_t el = ebase + (size_t)ls_prev[r];
                     const uint4* rs = reinterpret_cast<const uint4*>(S.mt + ((size_t)sl_prev[r] * n + el) * MT_N);
                     cp0 = rs[lane];
                     cp1 = rs[lane + 64];
@@ -858,7 +864,7 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
                 ls[r] = need ? __builtin_ctzll(need) : first;
                 need &= need - 1;
                 const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)src, ls[r]);
-                const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls[r];
+                const size_t el = ebase + (size_t)ls[r];
                 const uint4* rs = reinterpret_cast<const uint4*>(S.mt + ((size_t)sl * n + el) * MT_N);
 #pragma unroll
                 for (int i = 0; i < 3; i++)
@@ -871,7 +877,7 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
 #pragma unroll
             for (int r = 0; r < CR; r++) {
                 const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)src, ls[r]);
-                const size_t el = (size_t)blockIdx.x * BLOCK + (size_t)ls[r];
+                const size_t el = ebase + (size_t)ls[r];
                 uint4* rd = reinterpret_cast<uint4*>(S.mt + ((size_t)(sl ^ 1u) * n + el) * MT_N);
                 rd[lane] = s_cp[r][0][lane];
                 rd[lane + 64] = s_cp[r][1][lane];
@@ -1101,7 +1107,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
             for (int i = 0; i < 8; i++) atomicAdd((unsigned long long*)&g_stamps[i], (unsigned long long)E.st_acc[i]);
 #endif
     } else if (PG && wave == 1 + NEMIT) {
-        predraw_wave<CR, PB>(S, K, lane, e, valid, s_mb, s_cp, s_nxt);
+        predraw_wave<CR, PB>(S, K, lane, e, valid, (size_t)blockIdx.x * BLOCK, s_mb, s_cp, s_nxt);
     } else {
         // NEMIT == 2: two emit waves split the outputs: wave 1 rewards + int32 / float32
         // observation fields (+ the next step's uniform actions), wave 2 int8 fields, masks,
@@ -1366,8 +1372,12 @@ __device__ __forceinline__ void ag_spin(uint32_t* flag, uint32_t v) {
     while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
 }
 
+// EPW: envs per workgroup (64, 32 or 16; lanes >= EPW idle): fewer envs per CU spread N envs
+// over more CUs (every workgroup keeps its 150 KB of LDS, so one workgroup per CU).
+template <int EPW>
 __global__ void __launch_bounds__(AG_WAVES * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2)))
 k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0, int autoreset, fjsp_out out) {
+    static_assert(EPW == 64 || EPW == 32 || EPW == 16, "envs per workgroup");
 #ifdef FJSP_STAMPS
     const uint64_t t_entry = __builtin_amdgcn_s_memtime();
 #endif
@@ -1397,8 +1407,8 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     C.lut = s_lut;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / BLOCK);
     const int lane = threadIdx.x % BLOCK;
-    const int e = blockIdx.x * BLOCK + lane;
-    const bool valid = e < S.n;
+    const int e = blockIdx.x * EPW + lane;
+    const bool valid = lane < EPW && e < S.n;
     const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
     const Tables TL{s_orders + lane, s_code + lane, s_next + lane, s_cstep + lane, BLOCK};
 #ifdef FJSP_STAMPS
@@ -1434,32 +1444,53 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         // (copied in before the first barrier: K's first completions read them), copied by all
         // eight waves, rows r = wave (mod 8), loads batched: a per-lane loop with an LDS store
         // after each load waits out one HBM round trip per row (~30 µs per launch)
-        const uint32_t w0 = S.words[e], nslots = S.words[5 * n + e] >> 24, pg = S.words[(size_t)PGW * n + e];
-        const uint32_t no = (w0 >> 16) & 0xFFu, npd = (pg & 1u) ? (pg >> 24) & 0x7Fu : 0u;
+        // one round of loads: the state words and, speculatively, every order row, every
+        // pre-drawn row and the first 4 slot rows of this wave (all inside the allocations); a
+        // row is kept only if the words say it is live.  Slot rows past the first 32 follow in
+        // rounds of 8 per wave.
+        const uint32_t w0 = S.words[e], w5 = S.words[5 * n + e], pg = S.words[(size_t)PGW * n + e];
         uint32_t ov[MAX_ORDERS / AG_WAVES], pv[MAX_ORDERS / AG_WAVES];
 #pragma unroll
         for (int j = 0; j < MAX_ORDERS / AG_WAVES; j++) {
-            const uint32_t o = (uint32_t)(wave + AG_WAVES * j);
-            ov[j] = o < no ? S.orders[(size_t)o * n + e] : 0u;
-            pv[j] = o < npd ? S.nxt[(size_t)o * n + e] : 0u;
+            const size_t o = (size_t)(wave + AG_WAVES * j);
+            ov[j] = S.orders[o * n + e];
+            pv[j] = S.nxt[o * n + e];
         }
+        uint32_t cv[8], xv[8], tv[8];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const size_t q = (size_t)(wave + AG_WAVES * j);
+            cv[j] = S.scode[q * n + e];
+            xv[j] = S.snext[q * n + e];
+            tv[j] = S.scstep[q * n + e];
+        }
+        const uint32_t nslots = w5 >> 24;
+        const uint32_t no = (w0 >> 16) & 0xFFu, npd = (pg & 1u) ? (pg >> 24) & 0x7Fu : 0u;
 #pragma unroll
         for (int j = 0; j < MAX_ORDERS / AG_WAVES; j++) {
             const uint32_t o = (uint32_t)(wave + AG_WAVES * j);
             if (o < no) TL.orders[o * BLOCK] = ov[j];
             if (o < npd) s_nxt[o * BLOCK + lane] = pv[j];
         }
-        for (uint32_t q0 = (uint32_t)wave; q0 < nslots; q0 += 4 * AG_WAVES) {
-            uint32_t cv[4], xv[4], tv[4];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < 4; j++) {
+            const uint32_t q = (uint32_t)(wave + AG_WAVES * j);
+            if (q < nslots) {
+                TL.scode[q * BLOCK] = (uint16_t)cv[j];
+                TL.snext[q * BLOCK] = (uint8_t)xv[j];
+                TL.scstep[q * BLOCK] = (uint16_t)tv[j];
+            }
+        }
+        for (uint32_t q0 = (uint32_t)wave + 4 * AG_WAVES; q0 < nslots; q0 += 8 * AG_WAVES) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
                 const uint32_t q = q0 + (uint32_t)(AG_WAVES * j);
                 cv[j] = q < nslots ? S.scode[(size_t)q * n + e] : 0u;
                 xv[j] = q < nslots ? S.snext[(size_t)q * n + e] : 0u;
                 tv[j] = q < nslots ? S.scstep[(size_t)q * n + e] : 0u;
             }
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
+            for (int j = 0; j < 8; j++) {
                 const uint32_t q = q0 + (uint32_t)(AG_WAVES * j);
                 if (q < nslots) {
                     TL.scode[q * BLOCK] = (uint16_t)cv[j];
@@ -1743,7 +1774,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             AG_BARRIER();
         }
     } else if (wave == AG_PD) {
-        predraw_wave<CR, PB, true, true>(S, K, lane, e, valid, s_mb, s_cp, s_nxt);
+        predraw_wave<CR, PB, true, true>(S, K, lane, e, valid, (size_t)blockIdx.x * EPW, s_mb, s_cp, s_nxt);
     } else {
         // E0: step k+2's actions, rewards, the pickup's masks; E1: int32 and float32 fields; E2:
         // int8 fields, term, trunc, status, the AGV's pickup / drop masks; E3: step k+1's pickup
@@ -1895,6 +1926,7 @@ struct fjsp_handle {
     int use_pipe;    // two-wave pipelined k_step_many for lean outputs (FJSP_PIPE / fjsp_set_option)
     int use_pg;      // pre-draw wave in the pipelined kernel (FJSP_PREDRAW / fjsp_set_option "predraw")
     int use_ag;      // agent-group pipeline k_step_ag for uniform-random actions (FJSP_AGENTS / "agents")
+    int ag_epw;      // k_step_ag envs per workgroup: 64 / 32 / 16, 0 = auto (FJSP_AG_EPW / "ag_envs")
     const char* last_kernel;   // name of the last step kernel launched (fjsp_last_kernel)
     uint32_t env_id_base;      // global id of env 0 (fjsp_set_option "env_id_base")
 };
@@ -2017,6 +2049,8 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
         h->use_pg = pd ? atoi(pd) : 1;
         const char* ag = getenv("FJSP_AGENTS");
         h->use_ag = ag ? atoi(ag) : 1;
+        const char* ae = getenv("FJSP_AG_EPW");
+        h->ag_epw = ae ? atoi(ae) : 0;
     }
     h->dcfg.step_size = c.step_size;
     h->dcfg.max_steps = c.max_episode_steps;
@@ -2093,6 +2127,11 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
     if (!strcmp(name, "pipeline")) { h->use_pipe = value != 0; return 0; }
     if (!strcmp(name, "predraw")) { h->use_pg = value != 0; return 0; }
     if (!strcmp(name, "agents")) { h->use_ag = value != 0; return 0; }
+    if (!strcmp(name, "ag_envs")) {
+        if (value != 0 && value != 16 && value != 32 && value != 64) return fail("ag_envs must be 0, 16, 32 or 64");
+        h->ag_epw = (int)value;
+        return 0;
+    }
     if (!strcmp(name, "timing")) { h->timing = value != 0; if (!h->timing) h->timed = 0; return 0; }
     if (!strcmp(name, "env_id_base")) {
         // the handle is shard [value, value + n) of a larger job: env e's default stream becomes
@@ -2206,8 +2245,17 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
                    : staged ? (lds ? "k_step_many<lds,staged>" : "k_step_many<staged>")
                    : (lds ? "k_step_many<lds>" : "k_step_many");
     if (ag) {
-        hipLaunchKernelGGL(k_step_ag, grid, dim3(AG_WAVES * BLOCK), 0, h->stream, h->S, h->dcfg,
-                           K, action_seed, env_gid0, step0, autoreset, o);
+        // envs per workgroup: auto = the fewest that still give every workgroup a CU of its own
+        int epw = h->ag_epw;
+        if (epw == 0) epw = h->n <= 256 * 16 ? 16 : h->n <= 256 * 32 ? 32 : 64;
+        const dim3 agrid((h->n + epw - 1) / epw);
+        auto launch_ag = [&](auto kern) {
+            hipLaunchKernelGGL(kern, agrid, dim3(AG_WAVES * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed,
+                               env_gid0, step0, autoreset, o);
+        };
+        if (epw == 16) launch_ag(k_step_ag<16>);
+        else if (epw == 32) launch_ag(k_step_ag<32>);
+        else launch_ag(k_step_ag<64>);
     } else if (h->use_pipe && !full && !staged) {
         // a second emit wave pays while the CUs are not full (N <= 16384 at 64 envs per CU)
         const bool two = two_emit;

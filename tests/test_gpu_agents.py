@@ -191,3 +191,22 @@ def test_agents_byte_rows_not_quad_aligned(G, n):
             assert env.last_kernel() == AG
     for k in LEAN:
         assert P.bits_equal(runs[0][k], runs[1][k]), k
+
+
+@pytest.mark.parametrize("epw", [16, 32, 64])
+def test_agents_envs_per_workgroup(G, epw):
+    """k_step_ag with 16 / 32 / 64 envs per workgroup ("ag_envs"; 1000 envs leave a partial last
+    workgroup in each layout): the bytes of k_step_pipe, launch boundaries and end state included."""
+    n, seeds, chunks = 1000, np.arange(1000) * 5 + 2, [1, 37, 200, 5, 120]
+    runs = []
+    for agents in (1, 0):
+        env = _env(G, n, agents)
+        G.native.check(G.native.lib().fjsp_set_option(env.handle, b"ag_envs", epw))
+        env.reset(seeds=torch.from_numpy(seeds), num_orders=30)
+        a = _chunks(G, env, chunks, seed=9)
+        if agents:
+            assert env.last_kernel() == AG
+        runs.append((a, _views(env, (0, 15, 16, 31, 32, 63, 64, 999))))
+    for k in LEAN:
+        assert P.bits_equal(runs[0][0][k], runs[1][0][k]), k
+    _same_views(runs[0][1], runs[1][1])
