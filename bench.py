@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--batch-size", type=int, default=256, help="A2C batch (vector steps per update)")
     ap.add_argument("--no-a2c", action="store_true", help="skip the A2C training-loop leg of the step workload")
     ap.add_argument("--no-scale", action="store_true", help="skip the 16x-envs leg of the step workload")
+    ap.add_argument("--no-dedup", action="store_true",
+                    help="A2C update over every sample (no grouping of repeated inputs)")
     a = ap.parse_args()
     if a.steps is None:
         a.steps = 20 if a.workload == "step" else 4
@@ -140,11 +142,12 @@ def load_pmc(workload):
         return None
 
 
-def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=None, group=None):
+def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=None, group=None, dedup=True):
     """Batched A2C training loop (a2c_vec.VecMultiAgentA2C): env-steps/s over whole batches
-    (collect batch_size vector steps with the policy + GAE + one update)."""
+    (collect batch_size vector steps with the policy + GAE + one update).  dedup: the update
+    runs each network once per distinct input (A2CLosses; the same gradient)."""
     A = importlib.import_module("multi-agent-rl-for-fjsp_amd.a2c_vec")
-    learner = A.VecMultiAgentA2C(env, batch_size=batch_size, seed=0, group=group)
+    learner = A.VecMultiAgentA2C(env, batch_size=batch_size, seed=0, group=group, dedup=dedup)
     base = env.env_id_base
     learner.reset(seeds=torch.arange(base, base + N), num_orders=num_orders)
 
@@ -179,7 +182,7 @@ def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=
             "batch_size": batch_size, "envs_per_gpu": N, "ms_per_batch": elapsed * 1e3 / batches,
             "collect_ms_per_batch": tc * 1e3 / batches,
             "update_ms_per_batch": (elapsed - tc) * 1e3 / batches,
-            "critic_loss_last": learner.critic_loss_history[-1],
+            "critic_loss_last": learner.critic_loss_history[-1], "update_dedup": bool(dedup),
             "note": "predict (stacked-actor batched GEMMs + masked sampling) -> fjsp_step writing a2c "
                     "features in HBM -> fp64 GAE kernel -> full-batch update (8 actors + critic, Adam); "
                     "reference a2c.py loop: ~130 env-steps/s on one CPU core (SURVEY.md)"}
@@ -213,7 +216,7 @@ def main():
     env = vec_env.FJSPVecEnv(N, device=dev, env_id_base=base)
     if args.workload == "a2c":
         res = a2c_throughput(env, N, world, args.steps, args.warmup, args.batch_size, 25, dist,
-                             dist.group.WORLD if dist else None)
+                             dist.group.WORLD if dist else None, dedup=not args.no_dedup)
         if rank == 0:
             out = {"metric": "env-steps/sec of the A2C training loop (BASELINE configs 4/5)",
                    "value": res["value"], "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
@@ -355,7 +358,10 @@ def main():
             aenv = vec_env.FJSPVecEnv(N, device=dev)
             # two warm-up batches: the first collect / update carry one-time costs (graph
             # capture, allocator growth, library kernel selection: ~0.3 s / ~0.9 s)
-            a2c = a2c_throughput(aenv, N, 1, 3, 2, args.batch_size, 25)
+            a2c = a2c_throughput(aenv, N, 1, 3, 2, args.batch_size, 25, dedup=not args.no_dedup)
+            del aenv
+            aenv = vec_env.FJSPVecEnv(N, device=dev)
+            a2c["dense_update"] = a2c_throughput(aenv, N, 1, 3, 2, args.batch_size, 25, dedup=False)
             del aenv
         except Exception as e:   # the headline metric does not depend on this leg
             a2c = {"error": f"{type(e).__name__}: {e}"}

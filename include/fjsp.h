@@ -251,6 +251,12 @@ int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const fl
                     const uint64_t* seed, uint32_t env_gid0, uint32_t step, int32_t deterministic, uint8_t* actions,
                     float* values,
                     float* probs, void* stream);
+/* Grouping keys of the A2C update (a2c.py:647-703 _update over a batch; a2c_vec.A2CLosses
+ * dedup): feats f32 [T][38][n] (the rollout's a2c features) -> keys u64 [9][T * n], row a < 8
+ * a hash of actor a's padded input (its a2c.py:118-134 observation block, zero-padded to 13
+ * columns), row 8 of the critic's 38-column global state (a2c.py:153-166); equal inputs get
+ * equal keys (the caller verifies the grouping).  Stream-ordered on `stream`. */
+int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uint64_t* keys, void* stream);
 int fjsp_snapshot(fjsp_handle* h, void* dst);
 int fjsp_restore(fjsp_handle* h, const void* src);
 /* Kernel timing of the last fjsp_step_many / fjsp_step launch in ms (hipEvents on the

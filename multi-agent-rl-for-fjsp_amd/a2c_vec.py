@@ -96,6 +96,26 @@ class ActorStack(nn.Module):
     def forward(self, x):
         return torch.softmax(self.logits(x), dim=1)
 
+    def agent_probs(self, a, x):
+        """Actor a alone on x [13, B] -> probabilities [8, B] (the agent's slice of forward)."""
+        h = torch.relu(torch.addmm(self.b1[a], self.W1[a], x))
+        h = torch.relu(torch.addmm(self.b2[a], self.W2[a], h))
+        return torch.softmax(torch.addmm(self.b3[a], self.W3[a], h) + self.logit_pad[a], dim=0)
+
+    def forward_grouped(self, x, keys=None):
+        """forward on x [8, 13, S], each actor run once per distinct observation of its agent,
+        the probabilities gathered back per sample (A2CLosses dedup); keys [8, S] = row_keys(x)."""
+        if keys is None:
+            keys = row_keys(x)
+        out = []
+        for a in range(NA):
+            grp = group_columns(x[a], keys[a])
+            if grp is None:
+                out.append(self.agent_probs(a, x[a]))
+            else:
+                out.append(grp.gather(self.agent_probs(a, x[a][:, grp.first])))
+        return torch.stack(out)
+
     @torch.no_grad()
     def load_actor_nets(self, nets):
         for a, net in enumerate(nets):
@@ -221,6 +241,100 @@ def entropy_of(probs):
     return -(probs * torch.log(probs + 1e-10)).sum(dim=1)         # [8, B]
 
 
+# ---------------------------------------------------------------- duplicate observations
+_HASH_MUL = 0x100000001B3 * 0x9E37 + 1          # odd: a wrapping int64 multiply-add chain
+
+
+def row_keys(x):
+    """x f32 [..., C, S] -> int64 [..., S]: a hash of each column's C float bit patterns (equal
+    columns -> equal keys; unequal columns may collide, group_columns verifies)."""
+    bits = x.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    k = torch.zeros(bits.shape[:-2] + bits.shape[-1:], dtype=torch.int64, device=x.device)
+    for c in range(bits.shape[-2]):
+        k = _fmix64(k * _HASH_MUL + bits[..., c, :] + (c + 1))
+    return k
+
+
+def group_keys(feats):
+    """feats f32 [T, 38, N] -> int64 [9, T*N]: row a < 8 = row_keys of actor a's padded inputs
+    (actor_inputs), row 8 = row_keys of the critic's global state; on the GPU one pass of the
+    fjsp_a2c_group_keys kernel (the same hash)."""
+    T, _, N = feats.shape
+    if feats.is_cuda:
+        f = feats.contiguous()
+        keys = torch.empty(NA + 1, T * N, dtype=torch.int64, device=feats.device)
+        stream = torch.cuda.current_stream(feats.device).cuda_stream
+        nat.check(nat.lib().fjsp_a2c_group_keys(ctypes.c_void_p(f.data_ptr()), T, N, ctypes.c_void_p(keys.data_ptr()),
+                                                ctypes.c_void_p(stream)))
+        return keys
+    gidx = gather_index(feats.device)
+    return torch.cat([row_keys(actor_inputs(feats, gidx)),
+                      row_keys(feats.permute(1, 0, 2).reshape(GLOBAL_DIM, T * N))[None]])
+
+
+def group_columns(x, key=None):
+    """Distinct columns of x f32 [C, S] by one stable sort of their keys: a Groups (first [U] =
+    the first sample of each distinct column, inv [S] = each sample's distinct column, perm /
+    ends = the samples sorted by column and the end of each run), or None if a hash collision
+    merged two different columns (the caller then keeps the samples apart)."""
+    S = x.shape[-1]
+    if key is None:
+        key = row_keys(x)
+    sk, perm = torch.sort(key)
+    new = torch.ones(S, dtype=torch.bool, device=x.device)
+    new[1:] = sk[1:] != sk[:-1]
+    starts = torch.nonzero(new).view(-1)
+    seg = torch.cumsum(new, 0) - 1                                   # run of each sorted sample
+    inv = torch.empty(S, dtype=torch.int64, device=x.device)
+    inv[perm] = seg
+    first = perm[starts]                                             # a representative sample
+    ends = torch.cat([starts[1:], torch.tensor([S], device=x.device)])
+    if not bool((x[:, first][:, inv] == x).all()):
+        return None
+    return Groups(first, inv, perm, ends)
+
+
+class Groups:
+    __slots__ = ("first", "inv", "perm", "ends")
+
+    def __init__(self, first, inv, perm, ends):
+        self.first, self.inv, self.perm, self.ends = first, inv, perm, ends
+
+    def gather(self, y):
+        """y [..., U] -> y[..., inv] [..., S]; backward: per-run sums of the sample gradients."""
+        return _GatherRuns.apply(y, self)
+
+
+class _GatherRuns(torch.autograd.Function):
+    """Gather of per-group values to samples whose backward sums each group's sample gradients
+    by runs of the sorted order (an f64 prefix sum differenced at the run ends): deterministic
+    and free of the same-address atomic adds of index_select's backward (a station agent has
+    ~10 groups for ~10^6 samples)."""
+
+    @staticmethod
+    def forward(ctx, y, g):
+        ctx.g = g
+        return y[..., g.inv]
+
+    @staticmethod
+    def backward(ctx, gy):
+        g = ctx.g
+        cs = _prefix_sum(gy[..., g.perm].double())[..., g.ends - 1]
+        gu = torch.cat([cs[..., :1], cs[..., 1:] - cs[..., :-1]], dim=-1)
+        return gu.to(gy.dtype), None
+
+
+def _prefix_sum(w, block=1024):
+    """Inclusive prefix sum along the last dim, blocked so every scan runs over many short
+    rows (a scan over a few 10^6-long rows is one slow row per row)."""
+    *lead, S = w.shape
+    P = -(-S // block) * block
+    c = torch.nn.functional.pad(w, (0, P - S)).view(*lead, P // block, block).cumsum(-1)
+    tot = c[..., -1]
+    c = c + (tot.cumsum(-1) - tot)[..., None]
+    return c.view(*lead, P)[..., :S]
+
+
 class A2CLosses:
     """Loss sums for one (possibly sharded) batch; `count` = the GLOBAL sample count.
 
@@ -228,21 +342,33 @@ class A2CLosses:
     mean / unbiased std of agent a's advantages (calc_actor_loss, a2c.py:724-731); critic =
     mean over (agent, sample) of (V - R)^2 (calc_critic_loss, a2c.py:713-722).  With shards,
     every rank passes the global statistics and count, so summing the per-rank gradients
-    (all_reduce) gives the single-learner gradient."""
+    (all_reduce) gives the single-learner gradient.
+
+    dedup: every network runs once per DISTINCT input of the batch and its outputs are gathered
+    per sample.  An agent's observation repeats across steps and envs (in a 256 x 1024
+    masked-random batch the six station agents see <= 28 distinct observations, the pickup
+    station 1 225, the AGV 16 % of the samples, the critic's global state 75 %).  The losses
+    are built from the gathered outputs exactly as without dedup, so the gather's backward sums
+    each sample's gradient into its distinct input: the same gradient, summed in another order."""
 
     @staticmethod
     def compute(actors, critic, feats, masks, actions, returns, adv, gidx, midx, entropy_coef,
-                adv_mean, adv_std, count):
+                adv_mean, adv_std, count, dedup=False):
         x = actor_inputs(feats, gidx)                                # [8, 13, S]
-        probs = actors(x)                                            # [8, 8, S]
+        keys = group_keys(feats if feats.dim() == 3 else feats[None]) if dedup else None
+        probs = actors.forward_grouped(x, keys[:NA]) if dedup else actors(x)    # [8, 8, S]
         ent = entropy_of(probs)                                      # [8, S]
         pm = masked_probs(probs, agent_masks(masks, midx))
         logp = categorical_log_prob(pm, actions)                     # [8, S]
         adv_n = (adv - adv_mean[:, None]) / (adv_std[:, None] + 1e-8) if count > 1 else adv
         actor_losses = -(adv_n * logp).sum(dim=1) / count - entropy_coef * ent.sum(dim=1) / count
         S = feats.shape[0] * feats.shape[-1] if feats.dim() == 3 else feats.shape[-1]
-        g = feats.permute(0, 2, 1).reshape(S, GLOBAL_DIM) if feats.dim() == 3 else feats.t()
-        v = critic(g).reshape(-1)                                    # [S]
+        gt = feats.permute(1, 0, 2).reshape(GLOBAL_DIM, S) if feats.dim() == 3 else feats   # [38, S]
+        grp = group_columns(gt, keys[NA]) if dedup else None
+        if grp is not None:
+            v = grp.gather(critic(gt[:, grp.first].t()).reshape(-1))    # [S]
+        else:
+            v = critic(gt.t()).reshape(-1)
         critic_loss = ((v[None, :] - returns) ** 2).sum() / (NA * count)
         return actor_losses, critic_loss
 
@@ -307,7 +433,7 @@ def init_networks(seed=None, hidden=256, device="cpu"):
 
 
 def update_step(actors, critic, optim_actor, optim_critic, feats, masks, actions, ret, adv, gidx, midx,
-                entropy_coef, max_grad_norm, group=None):
+                entropy_coef, max_grad_norm, group=None, dedup=False):
     """One _update (a2c.py:647-703) on a [T, ., N] batch (this rank's shard of it).
 
     feats f32 [T, 38, N], masks int8 [T, 29, N], actions u8 [T, 8, N], ret / adv f64 [T, 8, N].
@@ -322,7 +448,7 @@ def update_step(actors, critic, optim_actor, optim_critic, feats, masks, actions
     optim_actor.zero_grad(set_to_none=True)
     optim_critic.zero_grad(set_to_none=True)
     actor_losses, critic_loss = A2CLosses.compute(actors, critic, feats, masks, acts, ret32, adv32, gidx, midx,
-                                                  entropy_coef, mean, std, count)
+                                                  entropy_coef, mean, std, count, dedup)
     (actor_losses.sum() + critic_loss).backward()
     D.allreduce_grads(list(actors.parameters()) + list(critic.parameters()), group)
     clip_per_agent_(actors, max_grad_norm)
@@ -360,7 +486,7 @@ class VecMultiAgentA2C:
 
     def __init__(self, env, batch_size=256, gamma=0.99, lamb=0.95, lr_actor=3e-4, lr_critic=1e-3,
                  use_gae=True, entropy_coef=0.01, max_grad_norm=0.5, hidden=256, seed=None, group=None,
-                 use_graph=True, fused_policy=True, exchange="allreduce"):
+                 use_graph=True, fused_policy=True, exchange="allreduce", dedup=True):
         self.env = env
         self.device = env.device
         self.N = env.num_envs
@@ -373,6 +499,7 @@ class VecMultiAgentA2C:
         if exchange not in ("allreduce", "gather"):
             raise ValueError("exchange must be 'allreduce' or 'gather'")
         self.exchange = exchange
+        self.dedup = bool(dedup)   # networks once per distinct input in the update (A2CLosses)
         self.possible_agents = list(AGENTS)
         self.obs_dims = dict(zip(AGENTS, OBS_DIMS))
         self.act_dims = dict(zip(AGENTS, N_ACTIONS))
@@ -561,7 +688,7 @@ class VecMultiAgentA2C:
             T = self.batch_size
             al, cl = update_step(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
                                  b["masks"][:T], b["actions"], ret, adv, self.gidx, self.midx, self.entropy_coef,
-                                 self.max_grad_norm, self.group)
+                                 self.max_grad_norm, self.group, self.dedup)
         for a, x in zip(AGENTS, al):
             self.actor_loss_history[a].append(x)
         self.critic_loss_history.append(cl)
@@ -587,7 +714,7 @@ class VecMultiAgentA2C:
             ret, adv = batch_advantages(g["rewards"], g["values"], g["done"], self.gamma, self.lamb, self.use_gae)
             al, cl = update_step(self.actors, self.critic, self.optim_actor, self.optim_critic, g["feats"], g["masks"],
                                  g["actions"], ret, adv, self.gidx, self.midx, self.entropy_coef,
-                                 self.max_grad_norm, D.LOCAL)
+                                 self.max_grad_norm, D.LOCAL, self.dedup)
             stats.copy_(torch.tensor(al + [cl], dtype=torch.float32))
         D.broadcast_flat(params + [stats], src=0, group=self.group)
         v = stats.cpu().tolist()

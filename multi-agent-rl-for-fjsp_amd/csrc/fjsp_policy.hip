@@ -232,9 +232,62 @@ __global__ void __launch_bounds__(256, 2) k_policy(const float* __restrict__ fea
     }
 }
 
+// Keys of the A2C update's grouping of repeated inputs (a2c_vec.row_keys, the same hash): per
+// sample s = t * n + e of feats f32 [T][38][n], key a < 8 over actor a's 13 padded input columns
+// (its OBS_DIMS[a] a2c features, then zeros), key 8 over all 38; k = fmix64(k * MUL + bits(x_c)
+// + c + 1) from k = 0.  One lane per sample, each column a coalesced load.
+constexpr uint64_t GK_MUL = 0x100000001B3ull * 0x9E37ull + 1ull;
+__device__ __forceinline__ uint64_t gk_fmix(uint64_t z) {
+    z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27; z *= 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ void __launch_bounds__(256) k_group_keys(const float* __restrict__ feats, int T, int n,
+                                                    uint64_t* __restrict__ keys) {
+    const size_t S = (size_t)T * n;
+    const size_t s = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= S) return;
+    const size_t t = s / (size_t)n, e = s - t * (size_t)n;
+    const float* x = feats + t * 38 * (size_t)n + e;
+    constexpr int offs[NAG + 1] = {0, 7, 20, 23, 26, 29, 32, 35, 38};
+    uint64_t kc = 0;
+    uint64_t ka[NAG];
+#pragma unroll
+    for (int a = 0; a < NAG; a++) ka[a] = 0;
+#pragma unroll
+    for (int c = 0; c < 38; c++) {
+        const uint64_t b = (uint64_t)__float_as_uint(x[(size_t)c * n]);
+        kc = gk_fmix(kc * GK_MUL + b + (uint64_t)(c + 1));
+#pragma unroll
+        for (int a = 0; a < NAG; a++)
+            if (c >= offs[a] && c < offs[a + 1]) ka[a] = gk_fmix(ka[a] * GK_MUL + b + (uint64_t)(c - offs[a] + 1));
+    }
+#pragma unroll
+    for (int a = 0; a < NAG; a++) {   // the zero padding up to 13 columns
+#pragma unroll
+        for (int c = offs[a + 1] - offs[a]; c < 13; c++) ka[a] = gk_fmix(ka[a] * GK_MUL + (uint64_t)(c + 1));
+        keys[(size_t)a * S + s] = ka[a];
+    }
+    keys[(size_t)NAG * S + s] = kc;
+}
+
 }  // namespace
 
 int fjsp_internal_fail(const char* msg);   // fjsp_hip.hip: sets fjsp_last_error()
+
+extern "C" int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uint64_t* keys, void* stream) {
+    if (T <= 0 || n <= 0) return fjsp_internal_fail("fjsp_a2c_group_keys: T and n must be > 0");
+    if (!feats || !keys) return fjsp_internal_fail("fjsp_a2c_group_keys: null buffer");
+    const size_t S = (size_t)T * (size_t)n;
+    hipLaunchKernelGGL(k_group_keys, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, feats, T, n,
+                       keys);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
+}
 
 extern "C" int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const float* actor_w,
                                const float* critic_w, const uint64_t* seed, uint32_t env_gid0, uint32_t step,

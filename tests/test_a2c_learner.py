@@ -88,8 +88,9 @@ def _replay_obs(actions, seed=0, num_orders=25):
     return feats, masks, rew, done
 
 
+@pytest.mark.parametrize("dedup", [False, True])
 @pytest.mark.parametrize("case", ["greedy", "replay"])
-def test_predict_and_update_match_reference(gold, case):
+def test_predict_and_update_match_reference(gold, case, dedup):
     acts = gold[f"{case}_actions"]
     T = len(acts)
     feats, masks, rew, done = _replay_obs(acts)
@@ -123,7 +124,8 @@ def test_predict_and_update_match_reference(gold, case):
     oc = torch.optim.Adam(critic.parameters(), lr=HP["lr_critic"])
     al, cl = A.update_step(actors, critic, oa, oc, torch.from_numpy(feats[:T]), torch.from_numpy(masks[:T]),
                            torch.from_numpy(acts[:, :, None].copy()), torch.from_numpy(ret[:, :, None]),
-                           torch.from_numpy(adv[:, :, None]), gidx, midx, HP["entropy_coef"], HP["max_grad_norm"])
+                           torch.from_numpy(adv[:, :, None]), gidx, midx, HP["entropy_coef"], HP["max_grad_norm"],
+                           dedup=dedup)
     assert np.allclose(al, gold[f"{case}_actor_loss"], rtol=1e-4, atol=1e-6), (al, gold[f"{case}_actor_loss"])
     assert cl == pytest.approx(float(gold[f"{case}_critic_loss"]), rel=1e-4)
     after = _params(actors, critic)
@@ -211,3 +213,46 @@ def test_log_prob_matches_torch_categorical():
     a = torch.randint(0, 8, (8, 300))
     ref = torch.distributions.Categorical(probs=p.permute(0, 2, 1)).log_prob(a)
     assert torch.equal(A.categorical_log_prob(p, a), ref)
+
+
+def test_grouped_update_equals_dense_update():
+    """dedup (each network once per distinct input, outputs gathered per sample) gives the
+    losses and gradients of the dense update on a batch with many repeated observations: the
+    same sums in another order (f32 tolerance)."""
+    torch.manual_seed(3)
+    T, N = 16, 64
+    gen = torch.Generator().manual_seed(5)
+    feats = torch.randint(0, 3, (T, A.GLOBAL_DIM, N), generator=gen).float()
+    feats[:, 5:9] = torch.randint(0, 40, (T, 4, N), generator=gen).float()   # AGV / pickup: more values
+    feats[:, 21] = torch.rand(T, N, generator=gen).round(decimals=1)       # a float progress field
+    masks = torch.randint(0, 2, (T, 29, N), generator=gen).to(torch.int8)
+    masks[:, A.MASK_OFFS] = 1                                                # IDLE is always valid
+    acts = torch.stack([torch.randint(0, n, (T, N), generator=gen) for n in A.N_ACTIONS], 1).to(torch.uint8)
+    ret = torch.randn(T, A.NA, N, generator=gen, dtype=torch.float64)
+    adv = torch.randn(T, A.NA, N, generator=gen, dtype=torch.float64)
+    gidx, midx = A.gather_index("cpu"), A.mask_index("cpu")
+    res = []
+    for dedup in (False, True):
+        actors, critic = A.init_networks(seed=11)
+        oa = torch.optim.SGD(actors.parameters(), lr=1.0)
+        oc = torch.optim.SGD(critic.parameters(), lr=1.0)
+        before = [p.detach().clone() for p in list(actors.parameters()) + list(critic.parameters())]
+        al, cl = A.update_step(actors, critic, oa, oc, feats, masks, acts, ret, adv, gidx, midx, 0.01, 1e9,
+                               dedup=dedup)
+        after = [p.detach().clone() for p in list(actors.parameters()) + list(critic.parameters())]
+        res.append((al, cl, [b - a for a, b in zip(after, before)]))
+    (al0, cl0, g0), (al1, cl1, g1) = res
+    assert np.allclose(al0, al1, rtol=1e-5, atol=1e-6)
+    assert cl1 == pytest.approx(cl0, rel=1e-5)
+    for a, b in zip(g0, g1):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-6)
+    # the grouping itself: repeated columns share an index, a collision is detected
+    x = feats.permute(1, 0, 2).reshape(A.GLOBAL_DIM, -1)[:7]
+    g = A.group_columns(x)
+    assert torch.equal(x[:, g.first][:, g.inv], x) and g.first.numel() < x.shape[1]
+    y = torch.randn(3, g.first.numel(), dtype=torch.float32, requires_grad=True)
+    w = torch.randn(3, x.shape[1])
+    (g.gather(y) * w).sum().backward()
+    ref = torch.zeros(3, g.first.numel()).index_add_(1, g.inv, w)
+    assert torch.allclose(y.grad, ref, rtol=1e-5, atol=1e-5)
+    assert A.group_columns(x, torch.zeros(x.shape[1], dtype=torch.int64)) is None

@@ -188,3 +188,55 @@ def test_eager_and_fused_draws_share_the_counter_hash(M):
     u_shard = A.counter_uniform(learner._rng_host, torch.arange(3 * n, 4 * n), 7, "cpu")
     u_big = A.counter_uniform(learner._rng_host, torch.arange(0, 4 * n), 7, "cpu")
     assert torch.equal(u_shard, u_big[..., 3 * n:])
+
+
+def test_a2c_4096_envs_grouped_update(M):
+    """A 4096-env x 64-step batch (BASELINE config 4's env count): sampled actions respect the
+    masks, three sampled envs replay on the oracle, the group-key kernel equals the host hash,
+    and the grouped update (dedup: each network once per distinct input) moves every parameter
+    as the dense update does, with finite losses."""
+    A, V, spec = M["A"], M["V"], M["spec"]
+    n, T = 4096, 64
+    env = V.FJSPVecEnv(n)
+    learner = A.VecMultiAgentA2C(env, batch_size=T, seed=4)
+    learner.reset(seeds=torch.arange(n) + 7, num_orders=25)
+    learner.collect()
+    b = learner._bufs
+    acts = b["actions"].long()
+    for a in range(8):
+        chosen = b["masks"][:T, A.MASK_OFFS[a]:A.MASK_OFFS[a] + A.N_ACTIONS[a], :].gather(1, acts[:, a:a + 1, :])
+        assert bool((chosen == 1).all()), a
+    idx = spec.a2c_feature_index()
+    feats, masks, rew = b["feats"].cpu().numpy(), b["masks"].cpu().numpy(), b["rewards"].cpu().numpy()
+    an = acts.cpu().numpy()
+    for e in (0, 2049, 4095):
+        o = O.OracleEnv()
+        r = o.reset(seed=7 + e, num_orders=25)
+        for t in range(T):
+            flat = np.concatenate([r["obs_i32"], r["obs_i8"], r["obs_f32"]]).astype(np.float32)
+            assert P.bits_equal(feats[t, :, e], flat[idx]), (e, t)
+            assert P.bits_equal(masks[t, :, e], r["masks"]), (e, t)
+            r = o.step(an[t, :, e])
+            assert P.bits_equal(rew[t, :, e], r["rewards"]), (e, t)
+            if r["term"] or r["trunc"]:
+                r = o.reset(num_orders=25)
+    keys = A.group_keys(b["feats"][:T])
+    assert torch.equal(keys.cpu(), A.group_keys(b["feats"][:T].cpu()))
+    ret, adv = learner.advantages()
+    res = []
+    for dedup in (False, True):
+        actors, critic = A.init_networks(seed=9, device="cuda")
+        oa = torch.optim.SGD(actors.parameters(), lr=1.0)
+        oc = torch.optim.SGD(critic.parameters(), lr=1.0)
+        before = [p.detach().clone() for p in list(actors.parameters()) + list(critic.parameters())]
+        al, cl = A.update_step(actors, critic, oa, oc, b["feats"][:T], b["masks"][:T], b["actions"], ret, adv,
+                               learner.gidx, learner.midx, 0.01, 1e9, dedup=dedup)
+        assert np.all(np.isfinite(al)) and np.isfinite(cl)
+        res.append((al, cl, [(bb - p.detach()) for bb, p in zip(before, list(actors.parameters()) +
+                                                                 list(critic.parameters()))]))
+    (al0, cl0, g0), (al1, cl1, g1) = res
+    assert np.allclose(al0, al1, rtol=1e-4, atol=1e-6)
+    assert cl1 == pytest.approx(cl0, rel=1e-4)
+    for x, y in zip(g0, g1):
+        scale = float(x.abs().max()) + 1e-12
+        assert float((x - y).abs().max()) <= 1e-3 * scale
