@@ -67,6 +67,40 @@ class CriticNet(nn.Module):
         return self.net(x)
 
 
+class _LinearSplitK(torch.autograd.Function):
+    """y = x W^T + b whose weight gradient over a long batch is a batched GEMM over batch chunks
+    summed afterwards (split-K): one [out, in] GEMM with K = 10^5..10^6 samples leaves most of
+    the chip idle (a few dozen output tiles)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        return torch.addmm(b, x, W.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W = ctx.saved_tensors
+        B = x.shape[0]
+        c = max(1, min(64, B // 8192))
+        bc = -(-B // c)
+        pad = c * bc - B
+        xp = torch.nn.functional.pad(x, (0, 0, 0, pad)).view(c, bc, -1)
+        gp = torch.nn.functional.pad(gy, (0, 0, 0, pad)).view(c, bc, -1)
+        gW = torch.bmm(gp.transpose(1, 2), xp).sum(0)
+        return gy @ W, gW, gy.sum(0)
+
+
+def mlp_forward(seq, x):
+    """An nn.Sequential of Linear / ReLU on x [B, in] with split-K weight gradients for long
+    batches (the same parameters, the same math)."""
+    for m in seq:
+        if isinstance(m, nn.Linear):
+            x = _LinearSplitK.apply(x, m.weight, m.bias) if x.shape[0] >= 65536 else m(x)
+        else:
+            x = m(x)
+    return x
+
+
 class ActorStack(nn.Module):
     """The 8 ActorNetworks as stacked, padded weights; forward is 3 batched GEMMs.
 
@@ -102,19 +136,36 @@ class ActorStack(nn.Module):
         h = torch.relu(torch.addmm(self.b2[a], self.W2[a], h))
         return torch.softmax(torch.addmm(self.b3[a], self.W3[a], h) + self.logit_pad[a], dim=0)
 
+    def forward_rows(self, x, g):
+        """The actors on their agents' distinct inputs: x [8, 13, S], g = RowGroups of the
+        agents' keys -> probabilities [8, 8, Umax] per group.  The agent with the most groups
+        runs alone and the others stacked on the second-largest count (padding columns are
+        computed and never gathered)."""
+        U = g.U
+        big = max(range(NA), key=lambda a: U[a])
+        rest = [a for a in range(NA) if a != big]
+        u2 = max(U[a] for a in rest)
+        ridx = torch.tensor(rest, device=x.device)
+        fr = g.first[ridx, :u2]
+        xr = torch.gather(x[ridx], 2, fr[:, None, :].expand(NA - 1, x.shape[1], u2))
+        h = torch.relu(torch.baddbmm(self.b1[ridx], self.W1[ridx], xr))
+        h = torch.relu(torch.baddbmm(self.b2[ridx], self.W2[ridx], h))
+        pr = torch.softmax(torch.baddbmm(self.b3[ridx], self.W3[ridx], h) + self.logit_pad[ridx], dim=1)
+        pb = self.agent_probs(big, x[big][:, g.first[big, :U[big]]])
+        umax = g.first.shape[1]
+        out = [None] * NA
+        out[big] = torch.nn.functional.pad(pb, (0, umax - U[big]))
+        for i, a in enumerate(rest):
+            out[a] = torch.nn.functional.pad(pr[i], (0, umax - u2))
+        return torch.stack(out)
+
     def forward_grouped(self, x, keys=None):
         """forward on x [8, 13, S], each actor run once per distinct observation of its agent,
         the probabilities gathered back per sample (A2CLosses dedup); keys [8, S] = row_keys(x)."""
-        if keys is None:
-            keys = row_keys(x)
-        out = []
-        for a in range(NA):
-            grp = group_columns(x[a], keys[a])
-            if grp is None:
-                out.append(self.agent_probs(a, x[a]))
-            else:
-                out.append(grp.gather(self.agent_probs(a, x[a][:, grp.first])))
-        return torch.stack(out)
+        g = RowGroups(row_keys(x) if keys is None else keys)
+        if not bool((torch.gather(x, 2, g.rep[:, None, :].expand_as(x)) == x).all()):
+            return self(x)
+        return g.gather(self.forward_rows(x, g))
 
     @torch.no_grad()
     def load_actor_nets(self, nets):
@@ -272,37 +323,47 @@ def group_keys(feats):
                       row_keys(feats.permute(1, 0, 2).reshape(GLOBAL_DIM, T * N))[None]])
 
 
-def group_columns(x, key=None):
-    """Distinct columns of x f32 [C, S] by one stable sort of their keys: a Groups (first [U] =
-    the first sample of each distinct column, inv [S] = each sample's distinct column, perm /
-    ends = the samples sorted by column and the end of each run), or None if a hash collision
-    merged two different columns (the caller then keeps the samples apart)."""
-    S = x.shape[-1]
-    if key is None:
-        key = row_keys(x)
-    sk, perm = torch.sort(key)
-    new = torch.ones(S, dtype=torch.bool, device=x.device)
-    new[1:] = sk[1:] != sk[:-1]
-    starts = torch.nonzero(new).view(-1)
-    seg = torch.cumsum(new, 0) - 1                                   # run of each sorted sample
-    inv = torch.empty(S, dtype=torch.int64, device=x.device)
-    inv[perm] = seg
-    first = perm[starts]                                             # a representative sample
-    ends = torch.cat([starts[1:], torch.tensor([S], device=x.device)])
-    if not bool((x[:, first][:, inv] == x).all()):
-        return None
-    return Groups(first, inv, perm, ends)
+class RowGroups:
+    """Distinct values of each row of keys int64 [R, S] (one segmented sort for all rows):
+    U[r] groups in row r; inv [R, S] = each sample's group, first [R, Umax] = a representative
+    sample of each group (padding: any sample), rep [R, S] = the representative of each
+    sample's group, perm [R, S] / ends [R, Umax] = the samples sorted by group and the end of
+    each group's run (padding: S)."""
 
-
-class Groups:
-    __slots__ = ("first", "inv", "perm", "ends")
-
-    def __init__(self, first, inv, perm, ends):
-        self.first, self.inv, self.perm, self.ends = first, inv, perm, ends
+    def __init__(self, keys):
+        R, S = keys.shape
+        dev = keys.device
+        # one flat sort for all rows: the row in bits 60..62 above 60 bits of the key (the
+        # grouping is verified by the caller, so a shorter key only risks a dense fallback)
+        flat = (keys & ((1 << 60) - 1)) | (torch.arange(R, device=dev, dtype=torch.int64)[:, None] << 60)
+        sk, fperm = torch.sort(flat.view(-1))
+        sk = sk.view(R, S)
+        perm = (fperm.view(R, S) - torch.arange(R, device=dev, dtype=torch.int64)[:, None] * S)
+        new = torch.ones(R, S, dtype=torch.bool, device=dev)
+        new[:, 1:] = sk[:, 1:] != sk[:, :-1]
+        seg = _prefix_sum(new.to(torch.int64)) - 1
+        self.U = (seg[:, -1] + 1).tolist()                        # the one host sync
+        umax = max(self.U)
+        idx = torch.where(new, seg, torch.full_like(seg, umax))
+        pos = torch.arange(S, device=dev).expand(R, S)
+        starts = torch.full((R, umax + 1), S, dtype=torch.int64, device=dev).scatter_(1, idx, pos)[:, :umax]
+        self.ends = torch.cat([starts[:, 1:], torch.full((R, 1), S, dtype=torch.int64, device=dev)], 1)
+        self.first = torch.gather(perm, 1, starts.clamp(max=S - 1))
+        self.inv = torch.empty_like(perm).scatter_(1, perm, seg)
+        self.rep = torch.gather(self.first, 1, self.inv)
+        self.perm = perm
 
     def gather(self, y):
-        """y [..., U] -> y[..., inv] [..., S]; backward: per-run sums of the sample gradients."""
+        """y [R, C, Umax] per group -> [R, C, S] per sample; backward: each group's sample
+        gradients summed (runs of the sorted order)."""
         return _GatherRuns.apply(y, self)
+
+
+def group_columns(x, key=None):
+    """Single-row RowGroups of the columns of x f32 [C, S], or None if a hash collision merged
+    two different columns."""
+    g = RowGroups((row_keys(x) if key is None else key)[None])
+    return g if bool((x[:, g.rep[0]] == x).all()) else None
 
 
 class _GatherRuns(torch.autograd.Function):
@@ -314,13 +375,16 @@ class _GatherRuns(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, g):
         ctx.g = g
-        return y[..., g.inv]
+        R, C, _ = y.shape
+        return torch.gather(y, 2, g.inv[:, None, :].expand(R, C, g.inv.shape[1]))
 
     @staticmethod
     def backward(ctx, gy):
         g = ctx.g
-        cs = _prefix_sum(gy[..., g.perm].double())[..., g.ends - 1]
-        gu = torch.cat([cs[..., :1], cs[..., 1:] - cs[..., :-1]], dim=-1)
+        R, C, S = gy.shape
+        cs = _prefix_sum(torch.gather(gy, 2, g.perm[:, None, :].expand(R, C, S)).double())
+        ce = torch.gather(cs, 2, (g.ends - 1)[:, None, :].expand(R, C, g.ends.shape[1]))
+        gu = torch.cat([ce[..., :1], ce[..., 1:] - ce[..., :-1]], dim=-1)
         return gu.to(gy.dtype), None
 
 
@@ -355,20 +419,30 @@ class A2CLosses:
     def compute(actors, critic, feats, masks, actions, returns, adv, gidx, midx, entropy_coef,
                 adv_mean, adv_std, count, dedup=False):
         x = actor_inputs(feats, gidx)                                # [8, 13, S]
-        keys = group_keys(feats if feats.dim() == 3 else feats[None]) if dedup else None
-        probs = actors.forward_grouped(x, keys[:NA]) if dedup else actors(x)    # [8, 8, S]
+        S = x.shape[-1]
+        gt = feats.permute(1, 0, 2).reshape(GLOBAL_DIM, S) if feats.dim() == 3 else feats   # [38, S]
+        ga = gc = None
+        if dedup:
+            keys = group_keys(feats if feats.dim() == 3 else feats[None])
+            ga, gc = RowGroups(keys[:NA]), RowGroups(keys[NA:])
+            ok = torch.stack([(torch.gather(x, 2, ga.rep[:, None, :].expand_as(x)) == x).all(),
+                              (gt[:, gc.rep[0]] == gt).all()])
+            if not bool(ok.all()):                                   # a hash collision: dense
+                ga = gc = None
+        if ga is not None:
+            probs = ga.gather(actors.forward_rows(x, ga))            # [8, 8, S]
+        else:
+            probs = actors(x)                                        # [8, 8, S]
         ent = entropy_of(probs)                                      # [8, S]
         pm = masked_probs(probs, agent_masks(masks, midx))
         logp = categorical_log_prob(pm, actions)                     # [8, S]
         adv_n = (adv - adv_mean[:, None]) / (adv_std[:, None] + 1e-8) if count > 1 else adv
         actor_losses = -(adv_n * logp).sum(dim=1) / count - entropy_coef * ent.sum(dim=1) / count
-        S = feats.shape[0] * feats.shape[-1] if feats.dim() == 3 else feats.shape[-1]
-        gt = feats.permute(1, 0, 2).reshape(GLOBAL_DIM, S) if feats.dim() == 3 else feats   # [38, S]
-        grp = group_columns(gt, keys[NA]) if dedup else None
-        if grp is not None:
-            v = grp.gather(critic(gt[:, grp.first].t()).reshape(-1))    # [S]
+        if gc is not None:
+            vu = mlp_forward(critic.net, gt[:, gc.first[0]].t()).reshape(1, 1, -1)
+            v = gc.gather(vu).reshape(-1)                            # [S]
         else:
-            v = critic(gt.t()).reshape(-1)
+            v = mlp_forward(critic.net, gt.t()).reshape(-1)
         critic_loss = ((v[None, :] - returns) ** 2).sum() / (NA * count)
         return actor_losses, critic_loss
 

@@ -13,7 +13,7 @@ env = G.make_env(N)
 env.reset(seeds=torch.arange(N))
 b = G.vec_env.Buffers(200, N, env.device, infos=False)
 env.rollout(200, buffers=b); torch.cuda.synchronize()
-ag = (ctypes.c_ulonglong * 56)(); pg = (ctypes.c_ulonglong * 8)()
+ag = (ctypes.c_ulonglong * 64)(); pg = (ctypes.c_ulonglong * 8)()
 L.fjsp_debug_agstamps(ag); L.fjsp_debug_pgstamps(pg)
 env.rollout(200, step0=200, buffers=b); torch.cuda.synchronize()
 L.fjsp_debug_agstamps(ag); L.fjsp_debug_pgstamps(pg)

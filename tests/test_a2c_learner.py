@@ -249,10 +249,11 @@ def test_grouped_update_equals_dense_update():
     # the grouping itself: repeated columns share an index, a collision is detected
     x = feats.permute(1, 0, 2).reshape(A.GLOBAL_DIM, -1)[:7]
     g = A.group_columns(x)
-    assert torch.equal(x[:, g.first][:, g.inv], x) and g.first.numel() < x.shape[1]
-    y = torch.randn(3, g.first.numel(), dtype=torch.float32, requires_grad=True)
-    w = torch.randn(3, x.shape[1])
+    assert torch.equal(x[:, g.rep[0]], x) and g.U[0] < x.shape[1]
+    assert torch.equal(x[:, g.first[0]][:, g.inv[0]], x)
+    y = torch.randn(1, 3, g.U[0], dtype=torch.float32, requires_grad=True)
+    w = torch.randn(1, 3, x.shape[1])
     (g.gather(y) * w).sum().backward()
-    ref = torch.zeros(3, g.first.numel()).index_add_(1, g.inv, w)
-    assert torch.allclose(y.grad, ref, rtol=1e-5, atol=1e-5)
+    ref = torch.zeros(3, g.U[0]).index_add_(1, g.inv[0], w[0])
+    assert torch.allclose(y.grad[0], ref, rtol=1e-5, atol=1e-5)
     assert A.group_columns(x, torch.zeros(x.shape[1], dtype=torch.int64)) is None
