@@ -26,7 +26,8 @@ def launches(path, kernel, grid):
     out = []
     with open(path) as f:
         for row in csv.DictReader(f):
-            if row["Kernel_Name"] == kernel and int(row["Grid_Size"]) == grid:
+            name = row["Kernel_Name"]
+            if (name == kernel or name.startswith(kernel + "<")) and int(row["Grid_Size"]) == grid:
                 out.append((float(row["Counter_Value"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
     return out
 
@@ -50,7 +51,7 @@ def summarize(a, dst, kernel, variant, grid, workload, steps_per_launch, algo_pe
     hbm = (2.0 * fk + wk) * 1024.0
     env_steps = a.envs * steps_per_launch
     algo = algo_per_env_step * env_steps
-    k = stats.get(kernel, {})
+    k = next((v for n, v in stats.items() if n == kernel or n.startswith(kernel + "<")), {})
     pmc = {
         "workload": workload,
         "envs": a.envs,
@@ -84,6 +85,7 @@ def main():
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--steps-per-launch", type=int, default=1024)
     ap.add_argument("--variant", default="k_step_ag<lds,predraw>", help="fjsp_last_kernel name of the fused launch")
+    ap.add_argument("--epw", type=int, default=16, help="k_step_ag envs per workgroup (option ag_envs; auto at 4096 envs: 16)")
     a = ap.parse_args()
     dst = os.path.join(REPO, "profiles", a.round)
     os.makedirs(dst, exist_ok=True)
@@ -101,7 +103,7 @@ def main():
         for row in csv.DictReader(f):
             stats[row["Name"]] = row
     rel = os.path.relpath(dst, REPO)
-    grid_ag = (a.envs + 63) // 64 * 64 * 8          # k_step_ag: 8 waves per 64-env workgroup
+    grid_ag = (a.envs + a.epw - 1) // a.epw * 64 * 8   # k_step_ag: 8 waves per workgroup of epw envs
     grid_1 = (a.envs + 63) // 64 * 64
     out = {
         "fused": summarize(a, dst, "k_step_ag", a.variant, grid_ag, f"fjsp_step_{a.envs}envs", a.steps_per_launch,
