@@ -164,7 +164,9 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
  * table ahead on a fourth wave, so auto-resets need no MT draws on the critical path; the
  * results are identical either way); "agents" (0/1, default 1: uniform-random actions with LDS
  * tables and the pre-draw run k_step_ag, the env's agents split over eight wavefronts of its
- * workgroup; identical results); "env_id_base" (0..2^32-1, default 0: the handle is the shard [value, value + N) of a
+ * workgroup; identical results); "ag_envs" (0/16/32/64, default 0 = auto: envs per k_step_ag
+ * workgroup, lanes >= ag_envs idle; auto = 64 for launches of fewer than 64 steps, else the
+ * fewest that give every workgroup a CU of its own; identical results); "env_id_base" (0..2^32-1, default 0: the handle is the shard [value, value + N) of a
  * larger job — every env's MT19937 stream is re-seeded to np.random.seed(value + e), exactly
  * the stream env value + e of one big handle starts from; stream-ordered). */
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value);

@@ -6,7 +6,7 @@
 // action draw (inverse CDF over the masked probabilities, or argmax) and the centralised
 // critic (networks.CentralizedCriticNetwork: 38 -> 256 -> 256 -> 128 -> 1).
 //
-// Grid: blockIdx.y = role (0..7 actor of agent y, 8 critic), blockIdx.x = tile of 64 envs;
+// Grid: blockIdx.y = role (0 critic, 1..8 actor of agent y - 1), blockIdx.x = tile of 64 envs;
 // 256 threads = 4 wavefronts.  The hidden activations never leave LDS:
 //   x   [40][64]  inputs of the tile (feature rows of the kernel-written [38][N] slab)
 //   h   [256][64] layer 1, then layer 2, then the critic's layer 3 (in place: results stay in
@@ -146,7 +146,10 @@ __global__ void __launch_bounds__(256, 2) k_policy(const float* __restrict__ fea
     __shared__ float s_h[HID * TILE];                        // h1, then h2 (then critic h3)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int role = blockIdx.y;
+    // the critic (the heaviest role: 848 MFMAs per wave against 544) first: 576 workgroups run
+    // on 512 two-per-CU slots, and the ones left for the second round should be the short ones
+    // (measured: 83.8 -> 75.0 us per launch at 4 096 envs)
+    const int role = blockIdx.y == 0 ? NAG : (int)blockIdx.y - 1;
     const int e0 = blockIdx.x * TILE;
     const bool critic = role == NAG;
     const int din = critic ? 38 : c_obs_dim[role];
