@@ -1787,6 +1787,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             if (part == 3 && k + 1 < K) {   // step k+1's pickup station, from P's AGV result of step k
                 const bool fresh = ag_fresh(k, valid, s_p1, s_kpost, lane, C, autoreset);
                 if (__ballot(valid && fresh) != 0) ag_spin(&s_flag1, (uint32_t)(k + 1));
+                AG_MARK(3);
                 if (valid) {
                     Env Ep;
 #pragma unroll
@@ -1803,6 +1804,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                     }
                     const int act0 = (int)(s_act[(k + 1) % 3][0][lane] & 0xFFu);
                     const uint32_t r0 = (pickup_execute(Ep, TL, C, act0) & 0xFFu) | ((uint32_t)act0 << 8);
+                    AG_MARK(4);
                     s_pk[lane] = make_uint4(Ep.w[0], Ep.w[4], Ep.w[5], Ep.w[7]);
                     s_pkr[lane] = make_uint2(r0, Ep.w[2]);
                     __hip_atomic_store(&s_uflag, (uint32_t)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1868,8 +1870,10 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         }
         if (wave == AG_P)
             for (int i = 0; i < 6; i++) atomicAdd(&g_agstamps[33 + i], (unsigned long long)amt[i]);
-        if (wave == AG_E3 || wave == AG_E2)   // after the pickup post (E3), the snapshot, the stores
-            for (int i = 0; i < 4; i++) atomicAdd(&g_agstamps[(wave == AG_E3 ? 40 : 46) + i], (unsigned long long)amt[i]);
+        if (wave == AG_E3)   // after the pickup post, the snapshot, the stores, the fresh wait, the pickup
+            for (int i = 0; i < 6; i++) atomicAdd(&g_agstamps[40 + i], (unsigned long long)amt[i]);
+        if (wave == AG_E2)   // top, the snapshot, the stores
+            for (int i = 0; i < 4; i++) atomicAdd(&g_agstamps[46 + i], (unsigned long long)amt[i]);
     }
 #endif
 }
