@@ -6,11 +6,11 @@
 // action draw (inverse CDF over the masked probabilities, or argmax) and the centralised
 // critic (networks.CentralizedCriticNetwork: 38 -> 256 -> 256 -> 128 -> 1).
 //
-// Grid: blockIdx.y = role (0 critic, 1..8 actor of agent y - 1), blockIdx.x = tile of 64 envs;
+// Grid: blockIdx.y = role (0 critic, 1..8 actor of agent y - 1), blockIdx.x = tile of 32 envs;
 // 256 threads = 4 wavefronts.  The hidden activations never leave LDS:
-//   x   [40][64]  inputs of the tile (feature rows of the kernel-written [38][N] slab)
-//   h   [256][64] layer 1, then layer 2, then the critic's layer 3 (in place: results stay in
-//                 registers across a barrier), so two workgroups fit a CU (74 KB of LDS each)
+//   x   [40][TILE]  inputs of the tile (feature rows of the kernel-written [38][N] slab)
+//   h   [256][TILE] layer 1, then layer 2, then the critic's layer 3 (in place: results stay in
+//                   registers across a barrier), so four workgroups fit a CU (37 KB of LDS each)
 // Every layer with K >= 16 runs on v_mfma_f32_32x32x2_f32 (exact f32 fma chains): each wave
 // owns 64 output rows = 2 x 2 tiles of 32 x 32 (the critic's 128-row layer 3: one tile row).
 // The actor's 256 -> n_a logits and the critic's 128 -> 1 value are VALU dot products.
@@ -28,7 +28,12 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int TILE = 64;       // envs per workgroup
+// 32 envs per workgroup: 37 KB of LDS and 113 VGPRs, so four workgroups share a CU and the 1 152
+// workgroups of a 4 096-env step run in 1.1 rounds of 1 024 slots (64-env tiles: 576 workgroups
+// in 1.1 rounds of 512, two waves per SIMD to hide the weight loads; measured 77.8 -> 68.2 us)
+constexpr int TILE = 32;              // envs per workgroup
+constexpr int NCOL = TILE / 32;       // 32-column MFMA tiles per row tile
+constexpr int WGS_PER_CU = 4;
 constexpr int HID = 256;
 constexpr int NAG = 8;
 constexpr int KS2 = HID / 2;   // k-steps of 2 for a 256-wide contraction
@@ -48,10 +53,10 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t z) {
 // MFMA A operands are packed per row tile t in groups of 4 k-steps: element (t, q, l, j) =
 // W[32 t + (l & 31)][2 (4 q + j) + (l >> 5)], so one 16-byte load per lane fetches the A
 // fragments of 4 consecutive k-steps (a coalesced 1 KB per wave instruction).
-// acc[i][j] += W(row tile rt0 + i) . act(col tile j); act = LDS [K][64] (rows = k), KS = K / 2.
+// acc[i][j] += W(row tile rt0 + i) . act(col tile j); act = LDS [K][TILE] (rows = k), KS = K / 2.
 template <int NT, int KS>
 __device__ __forceinline__ void mfma_rows(const float* __restrict__ wp, int rt0, const float* act, int lane,
-                                          f32x16 acc[NT][2]) {
+                                          f32x16 acc[NT][NCOL]) {
     static_assert(KS % 4 == 0, "k-steps come in groups of 4");
     constexpr int NQ = KS / 4;
     const float4* a[NT];
@@ -76,29 +81,30 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ wp, int rt0,
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int k = 2 * (4 * q + j) + kr;
-            const float b0 = act[k * TILE + cl];
-            const float b1 = act[k * TILE + 32 + cl];
+            float b[NCOL];
+#pragma unroll
+            for (int c = 0; c < NCOL; c++) b[c] = act[k * TILE + 32 * c + cl];
 #pragma unroll
             for (int i = 0; i < NT; i++) {
                 const float fa = j == 0 ? cur[i].x : j == 1 ? cur[i].y : j == 2 ? cur[i].z : cur[i].w;
-                acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, b0, acc[i][0], 0, 0, 0);
-                acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, b1, acc[i][1], 0, 0, 0);
+#pragma unroll
+                for (int c = 0; c < NCOL; c++) acc[i][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, b[c], acc[i][c], 0, 0, 0);
             }
         }
     }
 }
 
 template <int NT>
-__device__ __forceinline__ void zero_acc(f32x16 acc[NT][2]) {
+__device__ __forceinline__ void zero_acc(f32x16 acc[NT][NCOL]) {
 #pragma unroll
     for (int i = 0; i < NT; i++)
 #pragma unroll
-        for (int j = 0; j < 2; j++)
+        for (int j = 0; j < NCOL; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] = 0.0f;
 }
 
-// relu(acc + bias) -> out LDS [rows][64]; C/D layout of the 32x32 f32 MFMA: col = lane & 31,
+// relu(acc + bias) -> out LDS [rows][TILE]; C/D layout of the 32x32 f32 MFMA: col = lane & 31,
 // row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
 __device__ __forceinline__ void store_tile(const f32x16& acc, int row0, int col0, const float* __restrict__ bias,
                                            float* out, int lane) {
@@ -110,22 +116,22 @@ __device__ __forceinline__ void store_tile(const f32x16& acc, int row0, int col0
     }
 }
 template <int NT>
-__device__ __forceinline__ void store_rows(const f32x16 acc[NT][2], int row0, const float* __restrict__ bias, float* out,
+__device__ __forceinline__ void store_rows(const f32x16 acc[NT][NCOL], int row0, const float* __restrict__ bias, float* out,
                                            int lane) {
 #pragma unroll
     for (int i = 0; i < NT; i++)
 #pragma unroll
-        for (int j = 0; j < 2; j++) store_tile(acc[i][j], row0 + 32 * i, 32 * j, bias, out, lane);
+        for (int j = 0; j < NCOL; j++) store_tile(acc[i][j], row0 + 32 * i, 32 * j, bias, out, lane);
 }
 
-// Hidden layers 1 and 2 of a 256-wide MLP on the tile (x in s_x [DPAD][64]) -> s_h [256][64].
+// Hidden layers 1 and 2 of a 256-wide MLP on the tile (x in s_x [DPAD][TILE]) -> s_h [256][TILE].
 template <int DPAD>
 __device__ __forceinline__ void hidden256(const float* __restrict__ W, const float* s_x, float* s_h, int wave, int lane) {
     const float* W1 = W;                         // packed [8][DPAD/8][64][4]
     const float* B1 = W1 + 256 * DPAD;           // [256]
     const float* W2 = B1 + 256;                  // packed [8][32][64][4]
     const float* B2 = W2 + 256 * 256;            // [256]
-    f32x16 acc[2][2];
+    f32x16 acc[2][NCOL];
     zero_acc<2>(acc);
     mfma_rows<2, DPAD / 2>(W1, 2 * wave, s_x, lane, acc);
     store_rows<2>(acc, 64 * wave, B1, s_h, lane);
@@ -137,12 +143,12 @@ __device__ __forceinline__ void hidden256(const float* __restrict__ W, const flo
     __syncthreads();
 }
 
-__global__ void __launch_bounds__(256, 2) k_policy(const float* __restrict__ feats, const int8_t* __restrict__ masks,
+__global__ void __launch_bounds__(256, WGS_PER_CU) k_policy(const float* __restrict__ feats, const int8_t* __restrict__ masks,
                                                    int n, const float* __restrict__ actor_w,
                                                    const float* __restrict__ critic_w, const uint64_t* __restrict__ seedp,
                                                    uint32_t gid0, uint32_t step, int deterministic, uint8_t* __restrict__ actions,
                                                    float* __restrict__ values, float* __restrict__ probs_out) {
-    __shared__ float s_x[FJSP_POLICY_CRITIC_DPAD * TILE];   // inputs; later the logits [8][64]
+    __shared__ float s_x[FJSP_POLICY_CRITIC_DPAD * TILE];   // inputs; later the logits [8][TILE]
     __shared__ float s_h[HID * TILE];                        // h1, then h2 (then critic h3)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -166,7 +172,7 @@ __global__ void __launch_bounds__(256, 2) k_policy(const float* __restrict__ fea
         const float* B3 = W3 + 128 * HID;                  // [128]
         const float* W4 = B3 + 128;                        // [128]
         const float* B4 = W4 + 128;                        // [1]
-        f32x16 acc[1][2];
+        f32x16 acc[1][NCOL];
         zero_acc<1>(acc);
         mfma_rows<1, 128>(W3, wave, s_h, lane, acc);
         __syncthreads();
@@ -185,7 +191,7 @@ __global__ void __launch_bounds__(256, 2) k_policy(const float* __restrict__ fea
     const float* W3 = W + 256 * FJSP_POLICY_ACTOR_DPAD + 256 + 256 * 256 + 256;   // [8][256]
     const float* B3 = W3 + 8 * HID;                                                // [8]
     float* s_logit = s_x;
-    {
+    if (lane < TILE) {
         const int c = lane, r0 = 2 * wave;
         float l0 = B3[r0], l1 = B3[r0 + 1];
         for (int k = 0; k < HID; k++) {
