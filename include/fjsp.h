@@ -259,6 +259,15 @@ int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const fl
  * columns), row 8 of the critic's 38-column global state (a2c.py:153-166); equal inputs get
  * equal keys (the caller verifies the grouping).  Stream-ordered on `stream`. */
 int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uint64_t* keys, void* stream);
+/* The actor loss head of the grouped update (a2c.py:204-220 masked probabilities, :705-731
+ * entropy and calc_actor_loss): pu f32 [8][8][umax] = each agent's action probabilities per
+ * distinct input, inv int64 [8][T * n] = each sample's distinct input, masks int8 [T][29][n],
+ * actions int64 [8][T * n], adv_n f32 [8][T * n] (normalised advantages).  Out: grad f32
+ * [8][8][T * n] = d(sum_a actor_loss_a) / d(sample probabilities), and sums f64 [8][2] +=
+ * (sum adv_n * logp, sum entropy) per agent (the caller zeroes them).  Stream-ordered. */
+int fjsp_a2c_actor_head(const float* pu, int32_t umax, const int64_t* inv, int32_t T, int32_t n, const int8_t* masks,
+                        const int64_t* actions, const float* adv_n, float inv_count, float ent_coef, float* grad,
+                        double* sums, void* stream);
 int fjsp_snapshot(fjsp_handle* h, void* dst);
 int fjsp_restore(fjsp_handle* h, const void* src);
 /* Kernel timing of the last fjsp_step_many / fjsp_step launch in ms (hipEvents on the

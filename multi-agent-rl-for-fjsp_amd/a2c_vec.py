@@ -380,12 +380,43 @@ class _GatherRuns(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        g = ctx.g
-        R, C, S = gy.shape
-        cs = _prefix_sum(torch.gather(gy, 2, g.perm[:, None, :].expand(R, C, S)).double())
-        ce = torch.gather(cs, 2, (g.ends - 1)[:, None, :].expand(R, C, g.ends.shape[1]))
-        gu = torch.cat([ce[..., :1], ce[..., 1:] - ce[..., :-1]], dim=-1)
-        return gu.to(gy.dtype), None
+        return _run_sums(ctx.g, gy), None
+
+
+def _run_sums(g, gy):
+    """gy [R, C, S] per sample -> [R, C, Umax] per group of the RowGroups g: runs of the sorted
+    order summed (an f64 prefix sum differenced at the run ends)."""
+    R, C, S = gy.shape
+    cs = _prefix_sum(torch.gather(gy, 2, g.perm[:, None, :].expand(R, C, S)).double())
+    ce = torch.gather(cs, 2, (g.ends - 1)[:, None, :].expand(R, C, g.ends.shape[1]))
+    return torch.cat([ce[..., :1], ce[..., 1:] - ce[..., :-1]], dim=-1).to(gy.dtype)
+
+
+class _ActorHead(torch.autograd.Function):
+    """Per-agent actor losses of A2CLosses from the agents' per-group probabilities pu [8, 8,
+    Umax] (RowGroups g), computed with their per-sample gradient by one HIP kernel; backward:
+    the per-sample gradients summed per group (_run_sums)."""
+
+    @staticmethod
+    def forward(ctx, pu, g, masks, actions, adv_n, count, coef):
+        T, _, n = masks.shape
+        S = T * n
+        grad = torch.empty(NA, 8, S, dtype=torch.float32, device=pu.device)
+        sums = torch.zeros(NA, 2, dtype=torch.float64, device=pu.device)
+        pu_c = pu.detach().contiguous()
+        stream = torch.cuda.current_stream(pu.device).cuda_stream
+        V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        nat.check(nat.lib().fjsp_a2c_actor_head(V(pu_c), int(pu_c.shape[2]), V(g.inv), T, n, V(masks), V(actions),
+                                                V(adv_n), 1.0 / count, coef, V(grad), V(sums),
+                                                ctypes.c_void_p(stream)))
+        ctx.g = g
+        ctx.save_for_backward(grad)
+        return ((-sums[:, 0] - coef * sums[:, 1]) / count).float()
+
+    @staticmethod
+    def backward(ctx, gl):
+        (grad,) = ctx.saved_tensors
+        return _run_sums(ctx.g, grad * gl.to(grad.dtype)[:, None, None]), None, None, None, None, None, None
 
 
 def _prefix_sum(w, block=1024):
@@ -429,15 +460,21 @@ class A2CLosses:
                               (gt[:, gc.rep[0]] == gt).all()])
             if not bool(ok.all()):                                   # a hash collision: dense
                 ga = gc = None
-        if ga is not None:
-            probs = ga.gather(actors.forward_rows(x, ga))            # [8, 8, S]
-        else:
-            probs = actors(x)                                        # [8, 8, S]
-        ent = entropy_of(probs)                                      # [8, S]
-        pm = masked_probs(probs, agent_masks(masks, midx))
-        logp = categorical_log_prob(pm, actions)                     # [8, S]
         adv_n = (adv - adv_mean[:, None]) / (adv_std[:, None] + 1e-8) if count > 1 else adv
-        actor_losses = -(adv_n * logp).sum(dim=1) / count - entropy_coef * ent.sum(dim=1) / count
+        if ga is not None and x.is_cuda:
+            # the loss head and its gradient in one kernel (fjsp_a2c_actor_head)
+            m3 = (masks if masks.dim() == 3 else masks[None]).contiguous()
+            actor_losses = _ActorHead.apply(actors.forward_rows(x, ga), ga, m3, actions.contiguous(),
+                                            adv_n.float().contiguous(), float(count), float(entropy_coef))
+        else:
+            if ga is not None:
+                probs = ga.gather(actors.forward_rows(x, ga))        # [8, 8, S]
+            else:
+                probs = actors(x)                                    # [8, 8, S]
+            ent = entropy_of(probs)                                  # [8, S]
+            pm = masked_probs(probs, agent_masks(masks, midx))
+            logp = categorical_log_prob(pm, actions)                 # [8, S]
+            actor_losses = -(adv_n * logp).sum(dim=1) / count - entropy_coef * ent.sum(dim=1) / count
         if gc is not None:
             vu = mlp_forward(critic.net, gt[:, gc.first[0]].t()).reshape(1, 1, -1)
             v = gc.gather(vu).reshape(-1)                            # [S]

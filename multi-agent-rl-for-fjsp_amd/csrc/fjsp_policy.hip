@@ -280,9 +280,107 @@ __global__ void __launch_bounds__(256) k_group_keys(const float* __restrict__ fe
     keys[(size_t)NAG * S + s] = kc;
 }
 
+// The actor loss head of the grouped A2C update for one (agent, sample): the reference's
+// entropy, masked renormalisation / uniform fallback, Categorical log-prob and actor loss
+// (a2c.py:204-220, 705-731; a2c_vec.A2CLosses) and its gradient with respect to the sample's
+// eight probabilities, which are read from the agent's distinct-input outputs through inv.
+// L = sum over agents of -(sum adv_n logp) / count - c (sum entropy) / count; per (a, s):
+//   grad[a][j][s] = dL / dp_j;  sums[a] += (adv_n logp, entropy)  (f64 atomics per wave).
+__global__ void __launch_bounds__(256) k_actor_head(const float* __restrict__ pu, int umax,
+                                                    const int64_t* __restrict__ inv, int T, int n,
+                                                    const int8_t* __restrict__ masks,
+                                                    const int64_t* __restrict__ actions,
+                                                    const float* __restrict__ adv_n, float inv_count, float ent_coef,
+                                                    float* __restrict__ grad, double* __restrict__ sums) {
+    const int a = blockIdx.y;
+    const size_t S = (size_t)T * n;
+    const size_t s = (size_t)blockIdx.x * 256 + threadIdx.x;
+    double sl = 0.0, se = 0.0;
+    if (s < S) {
+        const size_t t = s / (size_t)n, e = s - t * (size_t)n;
+        const size_t u = (size_t)inv[(size_t)a * S + s];
+        const int na = c_nact[a], mo = c_mask_off[a];
+        const int act = (int)actions[(size_t)a * S + s];
+        const float adv = adv_n[(size_t)a * S + s];
+        float p[8], m[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            p[j] = pu[((size_t)a * 8 + j) * umax + u];
+            m[j] = j < na ? (float)masks[(t * 29 + mo + j) * n + e] : 0.0f;
+        }
+        // entropy and its gradient
+        float ent = 0.0f, g[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const float pe = p[j] + 1e-10f;
+            ent += p[j] * logf(pe);
+            g[j] = -ent_coef * inv_count * -(logf(pe) + p[j] / pe);
+        }
+        ent = -ent;
+        // masked probabilities: p m / sum(p m), or m / sum(m) when nothing valid is left
+        float sr = 0.0f, sm = 0.0f, pm[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) { sr += p[j] * m[j]; sm += m[j]; }
+#pragma unroll
+        for (int j = 0; j < 8; j++) pm[j] = sr > 0.0f ? (p[j] * m[j]) / sr : m[j] / sm;
+        float s2 = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; j++) s2 += pm[j];
+        float qa = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; j++) qa = j == act ? pm[j] / s2 : qa;
+        const float eps = 1.1920928955078125e-07f;
+        const float qc = fminf(fmaxf(qa, eps), 1.0f - eps);
+        const float logp = logf(qc);
+        // d L / d logp = -adv / count; through clamp (inclusive), q = pm / s2, pm = p m / sr
+        const float gq = (qa >= eps && qa <= 1.0f - eps) ? (-adv * inv_count) / qc : 0.0f;
+        if (sr > 0.0f) {
+            float gpm[8], dot = 0.0f;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                gpm[j] = (j == act ? gq / s2 : 0.0f) - gq * qa / s2;   // d q_act / d pm_j
+                dot += gpm[j] * (p[j] * m[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) g[j] += m[j] * (gpm[j] / sr - dot / (sr * sr));
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) grad[((size_t)a * 8 + j) * S + s] = g[j];
+        sl = (double)(adv * logp);
+        se = (double)ent;
+    }
+    // per-wave sums, one atomic pair per wave
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        sl += __shfl_xor(sl, off);
+        se += __shfl_xor(se, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&sums[2 * a], sl);
+        atomicAdd(&sums[2 * a + 1], se);
+    }
+}
+
 }  // namespace
 
 int fjsp_internal_fail(const char* msg);   // fjsp_hip.hip: sets fjsp_last_error()
+
+extern "C" int fjsp_a2c_actor_head(const float* pu, int32_t umax, const int64_t* inv, int32_t T, int32_t n,
+                                   const int8_t* masks, const int64_t* actions, const float* adv_n, float inv_count,
+                                   float ent_coef, float* grad, double* sums, void* stream) {
+    if (T <= 0 || n <= 0 || umax <= 0) return fjsp_internal_fail("fjsp_a2c_actor_head: T, n and umax must be > 0");
+    if (!pu || !inv || !masks || !actions || !adv_n || !grad || !sums)
+        return fjsp_internal_fail("fjsp_a2c_actor_head: null buffer");
+    const size_t S = (size_t)T * (size_t)n;
+    hipLaunchKernelGGL(k_actor_head, dim3((unsigned)((S + 255) / 256), NAG), dim3(256), 0, (hipStream_t)stream, pu, umax,
+                       inv, T, n, masks, actions, adv_n, inv_count, ent_coef, grad, sums);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
+}
 
 extern "C" int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uint64_t* keys, void* stream) {
     if (T <= 0 || n <= 0) return fjsp_internal_fail("fjsp_a2c_group_keys: T and n must be > 0");
