@@ -402,13 +402,14 @@ class _ActorHead(torch.autograd.Function):
         T, _, n = masks.shape
         S = T * n
         grad = torch.empty(NA, 8, S, dtype=torch.float32, device=pu.device)
-        sums = torch.zeros(NA, 2, dtype=torch.float64, device=pu.device)
+        part = torch.empty(NA, -(-S // 256), 2, dtype=torch.float64, device=pu.device)
         pu_c = pu.detach().contiguous()
         stream = torch.cuda.current_stream(pu.device).cuda_stream
         V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         nat.check(nat.lib().fjsp_a2c_actor_head(V(pu_c), int(pu_c.shape[2]), V(g.inv), T, n, V(masks), V(actions),
-                                                V(adv_n), 1.0 / count, coef, V(grad), V(sums),
+                                                V(adv_n), 1.0 / count, coef, V(grad), V(part),
                                                 ctypes.c_void_p(stream)))
+        sums = part.sum(1)
         ctx.g = g
         ctx.save_for_backward(grad)
         return ((-sums[:, 0] - coef * sums[:, 1]) / count).float()
@@ -424,7 +425,8 @@ def _prefix_sum(w, block=1024):
     rows (a scan over a few 10^6-long rows is one slow row per row)."""
     *lead, S = w.shape
     P = -(-S // block) * block
-    c = torch.nn.functional.pad(w, (0, P - S)).view(*lead, P // block, block).cumsum(-1)
+    wp = w if P == S else torch.nn.functional.pad(w, (0, P - S))
+    c = wp.reshape(*lead, P // block, block).cumsum(-1)
     tot = c[..., -1]
     c = c + (tot.cumsum(-1) - tot)[..., None]
     return c.view(*lead, P)[..., :S]

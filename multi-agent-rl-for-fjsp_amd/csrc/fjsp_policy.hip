@@ -285,7 +285,7 @@ __global__ void __launch_bounds__(256) k_group_keys(const float* __restrict__ fe
 // (a2c.py:204-220, 705-731; a2c_vec.A2CLosses) and its gradient with respect to the sample's
 // eight probabilities, which are read from the agent's distinct-input outputs through inv.
 // L = sum over agents of -(sum adv_n logp) / count - c (sum entropy) / count; per (a, s):
-//   grad[a][j][s] = dL / dp_j;  sums[a] += (adv_n logp, entropy)  (f64 atomics per wave).
+//   grad[a][j][s] = dL / dp_j;  sums[a][block] = the workgroup's (adv_n logp, entropy) sums.
 __global__ void __launch_bounds__(256) k_actor_head(const float* __restrict__ pu, int umax,
                                                     const int64_t* __restrict__ inv, int T, int n,
                                                     const int8_t* __restrict__ masks,
@@ -349,15 +349,19 @@ __global__ void __launch_bounds__(256) k_actor_head(const float* __restrict__ pu
         sl = (double)(adv * logp);
         se = (double)ent;
     }
-    // per-wave sums, one atomic pair per wave
+    // the workgroup's sums, one partial pair per workgroup (no atomics: ~16 000 workgroups per
+    // agent adding into one address serialise)
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         sl += __shfl_xor(sl, off);
         se += __shfl_xor(se, off);
     }
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&sums[2 * a], sl);
-        atomicAdd(&sums[2 * a + 1], se);
+    __shared__ double s_part[4][2];
+    if ((threadIdx.x & 63) == 0) { s_part[threadIdx.x >> 6][0] = sl; s_part[threadIdx.x >> 6][1] = se; }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const double v = s_part[0][threadIdx.x] + s_part[1][threadIdx.x] + s_part[2][threadIdx.x] + s_part[3][threadIdx.x];
+        sums[((size_t)a * gridDim.x + blockIdx.x) * 2 + threadIdx.x] = v;
     }
 }
 
