@@ -1278,12 +1278,11 @@ constexpr uint32_t K_WORDS = (1u << 1) | (0xFu << 13) | (0x3FFu << 20);
 // masks per emit wave: pickup [0,3) | the AGV's pickup / drop [9,11) | the AGV's moves [3,9),
 // machines [11,17), packaging [17,29)
 // (other splits of the fields over the emit waves measured within 1 %)
-#ifndef FJSP_AG_E0ST
-#define FJSP_AG_E0ST 2   // station masks (3 per station, from field 11) moved from E3 to E0 (E3 arrived
-                         // last at the barrier in 92 % of the steps; 0 / 2 / 4 / 6 stations: 1.212 / 1.183 /
-                         // 1.186 / 1.210 us per step at 16 envs per workgroup)
-#endif
-constexpr uint32_t AG_E0ST_BITS = ((1u << (3 * FJSP_AG_E0ST)) - 1u) << 11;
+// station masks (3 per station, from field 11) emitted by E0 instead of E3: E3 arrived last at
+// the barrier in 92 % of the steps; 0 / 2 / 4 / 6 stations: 1.212 / 1.183 / 1.186 / 1.210 us per
+// step at 16 envs per workgroup (profiles/r02/experiments/e3_masks_to_e0_*.json)
+constexpr int AG_E0ST = 2;
+constexpr uint32_t AG_E0ST_BITS = ((1u << (3 * AG_E0ST)) - 1u) << 11;
 constexpr uint32_t AG_MASKS_E0 = 0x7u | AG_E0ST_BITS, AG_MASKS_E2 = 0x3u << 9,
                    AG_MASKS_E3 = ((0x3Fu << 3) | (0x3FFFFu << 11)) & ~AG_E0ST_BITS;
 static_assert((AG_MASKS_E0 | AG_MASKS_E2 | AG_MASKS_E3) == (1u << NMASK) - 1u && !(AG_MASKS_E0 & AG_MASKS_E2) &&
