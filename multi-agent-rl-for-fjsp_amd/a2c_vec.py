@@ -324,7 +324,7 @@ def group_keys(feats):
 
 
 class RowGroups:
-    """Distinct values of each row of keys int64 [R, S] (one segmented sort for all rows):
+    """Distinct values of each row of keys int64 [R, S] (one flat sort for all rows):
     U[r] groups in row r; inv [R, S] = each sample's group, first [R, Umax] = a representative
     sample of each group (padding: any sample), rep [R, S] = the representative of each
     sample's group, perm [R, S] / ends [R, Umax] = the samples sorted by group and the end of
@@ -332,6 +332,7 @@ class RowGroups:
 
     def __init__(self, keys):
         R, S = keys.shape
+        assert R <= 8, "the row id lives in bits 60..62 of the sort key"
         dev = keys.device
         # one flat sort for all rows: the row in bits 60..62 above 60 bits of the key (the
         # grouping is verified by the caller, so a shorter key only risks a dense fallback)
