@@ -259,6 +259,12 @@ int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const fl
  * columns), row 8 of the critic's 38-column global state (a2c.py:153-166); equal inputs get
  * equal keys (the caller verifies the grouping).  Stream-ordered on `stream`. */
 int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uint64_t* keys, void* stream);
+/* The check of that grouping: rep_a int64 [8][T * n] / rep_c int64 [T * n] = the representative
+ * sample of each sample's actor-input / global-state group.  bad int32 [ceil(T * n / 256)] = 1
+ * for a block of 256 samples holding one whose inputs differ bitwise from its representative's
+ * (a hash collision: the caller falls back to the dense update), else 0.  Stream-ordered. */
+int fjsp_a2c_group_verify(const float* feats, int32_t T, int32_t n, const int64_t* rep_a, const int64_t* rep_c,
+                          int32_t* bad, void* stream);
 /* The actor loss head of the grouped update (a2c.py:204-220 masked probabilities, :705-731
  * entropy and calc_actor_loss): pu f32 [8][8][umax] = each agent's action probabilities per
  * distinct input, inv int64 [8][T * n] = each sample's distinct input, masks int8 [T][29][n],

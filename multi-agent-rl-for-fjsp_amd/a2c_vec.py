@@ -68,36 +68,50 @@ class CriticNet(nn.Module):
 
 
 class _LinearSplitK(torch.autograd.Function):
-    """y = x W^T + b whose weight gradient over a long batch is a batched GEMM over batch chunks
-    summed afterwards (split-K): one [out, in] GEMM with K = 10^5..10^6 samples leaves most of
-    the chip idle (a few dozen output tiles)."""
+    """y = x W^T + b (relu: max(y, 0) in the GEMM's epilogue) whose weight gradient over a long
+    batch is a batched GEMM over batch chunks summed afterwards (split-K): one [out, in] GEMM
+    with K = 10^5..10^6 samples leaves most of the chip idle (a few dozen output tiles).  The
+    input gradient is skipped when x needs none (the first layer)."""
 
     @staticmethod
-    def forward(ctx, x, W, b):
-        ctx.save_for_backward(x, W)
-        return torch.addmm(b, x, W.t())
+    def forward(ctx, x, W, b, relu):
+        y = torch._addmm_activation(b, x, W.t()) if relu else torch.addmm(b, x, W.t())
+        ctx.relu = relu
+        ctx.save_for_backward(x, W, y if relu else None)
+        return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, W = ctx.saved_tensors
+        x, W, y = ctx.saved_tensors
+        if ctx.relu:
+            gy = torch.ops.aten.threshold_backward(gy, y, 0.0)      # relu' from the output
         B = x.shape[0]
         c = max(1, min(64, B // 8192))
-        bc = -(-B // c)
-        pad = c * bc - B
-        xp = torch.nn.functional.pad(x, (0, 0, 0, pad)).view(c, bc, -1)
-        gp = torch.nn.functional.pad(gy, (0, 0, 0, pad)).view(c, bc, -1)
-        gW = torch.bmm(gp.transpose(1, 2), xp).sum(0)
-        return gy @ W, gW, gy.sum(0)
+        bc = B // c
+        # c chunks of bc rows as strided views (no padded copies), the B - c*bc tail apart
+        xc = x[:c * bc].reshape(c, bc, -1)
+        gc = gy[:c * bc].reshape(c, bc, -1)
+        gW = torch.bmm(gc.transpose(1, 2), xc).sum(0)
+        if c * bc < B:
+            gW += gy[c * bc:].t() @ x[c * bc:]
+        gx = gy @ W if ctx.needs_input_grad[0] else None
+        return gx, gW, gy.sum(0), None
 
 
 def mlp_forward(seq, x):
-    """An nn.Sequential of Linear / ReLU on x [B, in] with split-K weight gradients for long
-    batches (the same parameters, the same math)."""
-    for m in seq:
-        if isinstance(m, nn.Linear):
-            x = _LinearSplitK.apply(x, m.weight, m.bias) if x.shape[0] >= 65536 else m(x)
+    """An nn.Sequential of Linear / ReLU on x [B, in] with split-K weight gradients and the
+    ReLU fused into the GEMM for long batches (the same parameters, the same math)."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, nn.Linear) and x.shape[0] >= 65536:
+            relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
+            x = _LinearSplitK.apply(x, m.weight, m.bias, relu)
+            i += 2 if relu else 1
         else:
             x = m(x)
+            i += 1
     return x
 
 
@@ -136,22 +150,28 @@ class ActorStack(nn.Module):
         h = torch.relu(torch.addmm(self.b2[a], self.W2[a], h))
         return torch.softmax(torch.addmm(self.b3[a], self.W3[a], h) + self.logit_pad[a], dim=0)
 
-    def forward_rows(self, x, g):
+    def forward_rows(self, x, g, cols=None):
         """The actors on their agents' distinct inputs: x [8, 13, S], g = RowGroups of the
         agents' keys -> probabilities [8, 8, Umax] per group.  The agent with the most groups
         runs alone and the others stacked on the second-largest count (padding columns are
-        computed and never gathered)."""
+        computed and never gathered).  cols(agents, idx [k, u]) -> [k, 13, u] may stand in for x
+        (the inputs of just the representatives)."""
         U = g.U
         big = max(range(NA), key=lambda a: U[a])
         rest = [a for a in range(NA) if a != big]
         u2 = max(U[a] for a in rest)
-        ridx = torch.tensor(rest, device=x.device)
+        ridx = torch.tensor(rest, device=g.first.device)
         fr = g.first[ridx, :u2]
-        xr = torch.gather(x[ridx], 2, fr[:, None, :].expand(NA - 1, x.shape[1], u2))
+        if cols is None:
+            xr = torch.gather(x[ridx], 2, fr[:, None, :].expand(NA - 1, x.shape[1], u2))
+            xb = x[big][:, g.first[big, :U[big]]]
+        else:
+            xr = cols(ridx, fr)
+            xb = cols(torch.tensor([big], device=ridx.device), g.first[big:big + 1, :U[big]])[0]
         h = torch.relu(torch.baddbmm(self.b1[ridx], self.W1[ridx], xr))
         h = torch.relu(torch.baddbmm(self.b2[ridx], self.W2[ridx], h))
         pr = torch.softmax(torch.baddbmm(self.b3[ridx], self.W3[ridx], h) + self.logit_pad[ridx], dim=1)
-        pb = self.agent_probs(big, x[big][:, g.first[big, :U[big]]])
+        pb = self.agent_probs(big, xb)
         umax = g.first.shape[1]
         out = [None] * NA
         out[big] = torch.nn.functional.pad(pb, (0, umax - U[big]))
@@ -367,6 +387,24 @@ def group_columns(x, key=None):
     return g if bool((x[:, g.rep[0]] == x).all()) else None
 
 
+def group_verify(feats, ga, gc, x=None, gt=None):
+    """True when no hash collision merged different inputs in the groupings ga (actor inputs,
+    RowGroups of group_keys rows 0..7) and gc (global states, row 8) of feats f32 [T, 38, N]:
+    every sample's inputs equal those of its group's representative.  On the GPU one pass of the
+    fjsp_a2c_group_verify kernel (bitwise); else x [8, 13, S] / gt [38, S] compared in torch."""
+    if feats.is_cuda:
+        T, _, n = feats.shape
+        bad = torch.empty(-(-(T * n) // 256), dtype=torch.int32, device=feats.device)
+        stream = torch.cuda.current_stream(feats.device).cuda_stream
+        V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        nat.check(nat.lib().fjsp_a2c_group_verify(V(feats), T, n, V(ga.rep), V(gc.rep), V(bad),
+                                                  ctypes.c_void_p(stream)))
+        return not bool(bad.any())
+    ok = torch.stack([(torch.gather(x, 2, ga.rep[:, None, :].expand_as(x)) == x).all(),
+                      (gt[:, gc.rep[0]] == gt).all()])
+    return bool(ok.all())
+
+
 class _GatherRuns(torch.autograd.Function):
     """Gather of per-group values to samples whose backward sums each group's sample gradients
     by runs of the sorted order (an f64 prefix sum differenced at the run ends): deterministic
@@ -452,26 +490,35 @@ class A2CLosses:
     @staticmethod
     def compute(actors, critic, feats, masks, actions, returns, adv, gidx, midx, entropy_coef,
                 adv_mean, adv_std, count, dedup=False):
-        x = actor_inputs(feats, gidx)                                # [8, 13, S]
-        S = x.shape[-1]
-        gt = feats.permute(1, 0, 2).reshape(GLOBAL_DIM, S) if feats.dim() == 3 else feats   # [38, S]
+        f3 = feats if feats.dim() == 3 else feats[None]
+        T, _, n = f3.shape
+        S = T * n
+        gt = f3.permute(1, 0, 2).reshape(GLOBAL_DIM, S)                # [38, S]
+        x = None if dedup and feats.is_cuda else actor_inputs(feats, gidx)   # [8, 13, S]
         ga = gc = None
         if dedup:
-            keys = group_keys(feats if feats.dim() == 3 else feats[None])
+            f3 = f3.contiguous()
+            keys = group_keys(f3)
             ga, gc = RowGroups(keys[:NA]), RowGroups(keys[NA:])
-            ok = torch.stack([(torch.gather(x, 2, ga.rep[:, None, :].expand_as(x)) == x).all(),
-                              (gt[:, gc.rep[0]] == gt).all()])
-            if not bool(ok.all()):                                   # a hash collision: dense
+            if not group_verify(f3, ga, gc, x, gt):                 # a hash collision: dense
                 ga = gc = None
+                if x is None:
+                    x = actor_inputs(feats, gidx)
+
+        def cols(agents, idx):                                       # [k, 13, u] from gt
+            k, u = idx.shape
+            c = gt[:, idx.reshape(-1)].view(GLOBAL_DIM, k, u)
+            c = torch.cat([c, c.new_zeros(1, k, u)])
+            return c[gidx[agents], torch.arange(k, device=idx.device)[:, None], :]
         adv_n = (adv - adv_mean[:, None]) / (adv_std[:, None] + 1e-8) if count > 1 else adv
-        if ga is not None and x.is_cuda:
+        if ga is not None and feats.is_cuda:
             # the loss head and its gradient in one kernel (fjsp_a2c_actor_head)
             m3 = (masks if masks.dim() == 3 else masks[None]).contiguous()
-            actor_losses = _ActorHead.apply(actors.forward_rows(x, ga), ga, m3, actions.contiguous(),
+            actor_losses = _ActorHead.apply(actors.forward_rows(x, ga, cols), ga, m3, actions.contiguous(),
                                             adv_n.float().contiguous(), float(count), float(entropy_coef))
         else:
             if ga is not None:
-                probs = ga.gather(actors.forward_rows(x, ga))        # [8, 8, S]
+                probs = ga.gather(actors.forward_rows(x, ga, cols))  # [8, 8, S]
             else:
                 probs = actors(x)                                    # [8, 8, S]
             ent = entropy_of(probs)                                  # [8, S]

@@ -365,6 +365,48 @@ __global__ void __launch_bounds__(256) k_actor_head(const float* __restrict__ pu
     }
 }
 
+// The grouping check of the A2C update (a2c_vec.A2CLosses, replaces the torch gather-and-compare
+// of every input with its group's representative): sample s is bad when any of actor a's input
+// columns differs bitwise from those of rep_a[a][s], or any of its 38 global-state columns from
+// those of rep_c[s] (a hash collision merged two different inputs).  Samples that represent
+// their own group are skipped.  bad[block] = 1 if any sample of the workgroup is bad, else 0.
+__global__ void __launch_bounds__(256) k_group_verify(const float* __restrict__ feats, int T, int n,
+                                                      const int64_t* __restrict__ rep_a,
+                                                      const int64_t* __restrict__ rep_c, int32_t* __restrict__ bad) {
+    const size_t S = (size_t)T * n;
+    const size_t s = (size_t)blockIdx.x * 256 + threadIdx.x;
+    int diff = 0;
+    if (s < S) {
+        constexpr int offs[NAG + 1] = {0, 7, 20, 23, 26, 29, 32, 35, 38};
+        const size_t t = s / (size_t)n, e = s - t * (size_t)n;
+        const uint32_t* x = reinterpret_cast<const uint32_t*>(feats) + t * 38 * (size_t)n + e;
+        uint32_t v[38];
+#pragma unroll
+        for (int c = 0; c < 38; c++) v[c] = x[(size_t)c * n];
+        auto col = [&](size_t r) {
+            const size_t tr = r / (size_t)n, er = r - tr * (size_t)n;
+            return reinterpret_cast<const uint32_t*>(feats) + tr * 38 * (size_t)n + er;
+        };
+        const size_t rc = (size_t)rep_c[s];
+        if (rc != s) {
+            const uint32_t* y = col(rc);
+#pragma unroll
+            for (int c = 0; c < 38; c++) diff |= (int)(y[(size_t)c * n] != v[c]);
+        }
+#pragma unroll
+        for (int a = 0; a < NAG; a++) {
+            const size_t ra = (size_t)rep_a[(size_t)a * S + s];
+            if (ra != s) {
+                const uint32_t* y = col(ra);
+#pragma unroll
+                for (int c = offs[a]; c < offs[a + 1]; c++) diff |= (int)(y[(size_t)c * n] != v[c]);
+            }
+        }
+    }
+    diff = __syncthreads_or(diff);
+    if (threadIdx.x == 0) bad[blockIdx.x] = diff ? 1 : 0;
+}
+
 }  // namespace
 
 int fjsp_internal_fail(const char* msg);   // fjsp_hip.hip: sets fjsp_last_error()
@@ -392,6 +434,21 @@ extern "C" int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uin
     const size_t S = (size_t)T * (size_t)n;
     hipLaunchKernelGGL(k_group_keys, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, feats, T, n,
                        keys);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int fjsp_a2c_group_verify(const float* feats, int32_t T, int32_t n, const int64_t* rep_a,
+                                     const int64_t* rep_c, int32_t* bad, void* stream) {
+    if (T <= 0 || n <= 0) return fjsp_internal_fail("fjsp_a2c_group_verify: T and n must be > 0");
+    if (!feats || !rep_a || !rep_c || !bad) return fjsp_internal_fail("fjsp_a2c_group_verify: null buffer");
+    const size_t S = (size_t)T * (size_t)n;
+    hipLaunchKernelGGL(k_group_verify, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, feats, T,
+                       n, rep_a, rep_c, bad);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

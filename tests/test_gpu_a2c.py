@@ -240,3 +240,43 @@ def test_a2c_4096_envs_grouped_update(M):
     for x, y in zip(g0, g1):
         scale = float(x.abs().max()) + 1e-12
         assert float((x - y).abs().max()) <= 1e-3 * scale
+
+
+def test_group_verify_kernel_flags_collisions(M):
+    """fjsp_a2c_group_verify accepts a true grouping (equal to the torch comparison) and flags
+    a forged one: an actor representative or a global-state representative whose inputs
+    differ from the sample's (what a hash collision would produce)."""
+    A = M["A"]
+    T, n = 3, 700
+    g = torch.Generator().manual_seed(5)
+    base = torch.randint(0, 4, (T, 38, n), generator=g).float()
+    base[:, :, n // 2:] = base[:, :, :n - n // 2]              # duplicated columns
+    f = base.cuda()
+    keys = A.group_keys(f)
+    ga, gc = A.RowGroups(keys[:A.NA]), A.RowGroups(keys[A.NA:])
+    x = A.actor_inputs(f, A.gather_index(f.device))
+    gt = f.permute(1, 0, 2).reshape(A.GLOBAL_DIM, -1)
+    assert A.group_verify(f, ga, gc)
+    assert bool((torch.gather(x, 2, ga.rep[:, None, :].expand_as(x)) == x).all())
+    S = T * n
+    s = 1234
+    other = int((gt[:, s + 1:] != gt[:, s:s + 1]).any(0).nonzero()[0]) + s + 1   # a column unlike s
+    bad_c = _copy(gc)
+    bad_c.rep = gc.rep.clone()
+    bad_c.rep[0, s] = other
+    assert not A.group_verify(f, ga, bad_c)
+    for a in (0, 1, 7):
+        cols = A.gather_index(f.device)[a, :A.OBS_DIMS[a]]
+        o = int((gt[cols, :] != gt[cols, s:s + 1]).any(0).nonzero()[0])
+        bad_a = _copy(ga)
+        bad_a.rep = ga.rep.clone()
+        bad_a.rep[a, s] = o
+        assert not A.group_verify(f, bad_a, gc), a
+    assert S == gt.shape[1]
+
+
+def _copy(g):
+    """A shallow copy of RowGroups g (its rep replaced by the caller)."""
+    c = type(g).__new__(type(g))
+    c.__dict__.update(g.__dict__)
+    return c
