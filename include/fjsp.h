@@ -269,7 +269,8 @@ int fjsp_a2c_group_verify(const float* feats, int32_t T, int32_t n, const int64_
  * entropy and calc_actor_loss): pu f32 [8][8][umax] = each agent's action probabilities per
  * distinct input, inv int64 [8][T * n] = each sample's distinct input, masks int8 [T][29][n],
  * actions int64 [8][T * n], adv_n f32 [8][T * n] (normalised advantages).  Out: grad f32
- * [8][8][T * n] = d(sum_a actor_loss_a) / d(sample probabilities), and sums f64
+ * [29][T * n] = d(sum_a actor_loss_a) / d(sample probabilities), row mask_off[a] + j for agent
+ * a's valid action j (the 29 action-mask columns' order), and sums f64
  * [8][ceil(T * n / 256)][2] = per agent and block of 256 samples (sum adv_n * logp, sum
  * entropy); the caller adds the blocks.  Stream-ordered. */
 int fjsp_a2c_actor_head(const float* pu, int32_t umax, const int64_t* inv, int32_t T, int32_t n, const int8_t* masks,

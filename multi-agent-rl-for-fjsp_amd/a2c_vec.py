@@ -38,6 +38,7 @@ NA = 8
 OBS_DIMS = [7, 13, 3, 3, 3, 3, 3, 3]          # _get_obs_dim per agent (a2c.py:118-134)
 OBS_OFFS = [0, 7, 20, 23, 26, 29, 32, 35]      # agent blocks of the 38-dim global state
 MASK_OFFS = [0, 3, 11, 14, 17, 20, 23, 26]     # agent blocks of the 29 mask bytes
+MASK_DIM = 29
 GLOBAL_DIM = 38
 DPAD, APAD = 13, 8
 
@@ -434,13 +435,15 @@ def _run_sums(g, gy):
 class _ActorHead(torch.autograd.Function):
     """Per-agent actor losses of A2CLosses from the agents' per-group probabilities pu [8, 8,
     Umax] (RowGroups g), computed with their per-sample gradient by one HIP kernel; backward:
-    the per-sample gradients summed per group (_run_sums)."""
+    the per-sample gradients summed per group (runs of the sorted order) for the 29 valid
+    (agent, action) rows only: a padded action's probability is an exact 0 out of the softmax,
+    so its gradient is never used (left 0)."""
 
     @staticmethod
     def forward(ctx, pu, g, masks, actions, adv_n, count, coef):
         T, _, n = masks.shape
         S = T * n
-        grad = torch.empty(NA, 8, S, dtype=torch.float32, device=pu.device)
+        grad = torch.empty(MASK_DIM, S, dtype=torch.float32, device=pu.device)
         part = torch.empty(NA, -(-S // 256), 2, dtype=torch.float64, device=pu.device)
         pu_c = pu.detach().contiguous()
         stream = torch.cuda.current_stream(pu.device).cuda_stream
@@ -456,7 +459,35 @@ class _ActorHead(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gl):
         (grad,) = ctx.saved_tensors
-        return _run_sums(ctx.g, grad * gl.to(grad.dtype)[:, None, None]), None, None, None, None, None, None
+        g = ctx.g
+        S = grad.shape[1]
+        umax = g.ends.shape[1]
+        # each agent's rows in its sorted sample order, scaled by the agent's loss gradient
+        srt = torch.empty_like(grad)
+        for a in range(NA):
+            o, k = MASK_OFFS[a], N_ACTIONS[a]
+            torch.gather(grad[o:o + k], 1, g.perm[a].expand(k, S), out=srt[o:o + k])
+        row_agent = torch.repeat_interleave(torch.arange(NA, device=grad.device),
+                                            torch.tensor(N_ACTIONS, device=grad.device))
+        srt.mul_(gl.to(grad.dtype)[row_agent, None])
+        cs = _prefix_sum(srt.double())
+        ce = torch.gather(cs, 1, (g.ends - 1)[row_agent])
+        rs = torch.cat([ce[:, :1], ce[:, 1:] - ce[:, :-1]], dim=1).to(grad.dtype)    # [29, Umax]
+        out = torch.zeros(NA * 8, umax, dtype=grad.dtype, device=grad.device)
+        out[_valid_rows(grad.device)] = rs
+        return out.view(NA, 8, umax), None, None, None, None, None, None
+
+
+_VALID_ROWS = {}
+
+
+def _valid_rows(device):
+    """Rows a * 8 + j (j < N_ACTIONS[a]) of [8 * 8, .]: the 29 valid (agent, action) pairs in
+    action-mask order."""
+    if device not in _VALID_ROWS:
+        _VALID_ROWS[device] = torch.tensor([a * 8 + j for a in range(NA) for j in range(N_ACTIONS[a])],
+                                           device=device)
+    return _VALID_ROWS[device]
 
 
 def _prefix_sum(w, block=1024):

@@ -285,7 +285,9 @@ __global__ void __launch_bounds__(256) k_group_keys(const float* __restrict__ fe
 // (a2c.py:204-220, 705-731; a2c_vec.A2CLosses) and its gradient with respect to the sample's
 // eight probabilities, which are read from the agent's distinct-input outputs through inv.
 // L = sum over agents of -(sum adv_n logp) / count - c (sum entropy) / count; per (a, s):
-//   grad[a][j][s] = dL / dp_j;  sums[a][block] = the workgroup's (adv_n logp, entropy) sums.
+//   grad[mask_off[a] + j][s] = dL / dp_j for the agent's valid actions j < nact[a] (29 rows: a
+//   padded action's probability is an exact 0 out of the softmax, its gradient is never used);
+//   sums[a][block] = the workgroup's (adv_n logp, entropy) sums.
 __global__ void __launch_bounds__(256) k_actor_head(const float* __restrict__ pu, int umax,
                                                     const int64_t* __restrict__ inv, int T, int n,
                                                     const int8_t* __restrict__ masks,
@@ -345,7 +347,8 @@ __global__ void __launch_bounds__(256) k_actor_head(const float* __restrict__ pu
             for (int j = 0; j < 8; j++) g[j] += m[j] * (gpm[j] / sr - dot / (sr * sr));
         }
 #pragma unroll
-        for (int j = 0; j < 8; j++) grad[((size_t)a * 8 + j) * S + s] = g[j];
+        for (int j = 0; j < 8; j++)
+            if (j < na) grad[(size_t)(mo + j) * S + s] = g[j];   // valid actions only (rows mo..mo+na)
         sl = (double)(adv * logp);
         se = (double)ent;
     }
