@@ -18,6 +18,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "fjsp_stamps.h"
+
 #ifndef FJSP_DEV
 #define FJSP_DEV __device__ __forceinline__
 #endif
@@ -137,37 +139,7 @@ constexpr uint32_t ST_DIVERGED = 0x1u, ST_OBS_OVERFLOW = 0x2u, ST_PKG_WAIT = 0x4
 // Number of packed u32 words of Env in the SoA state buffer.
 constexpr int NWORDS = 40;   // rows of the HBM state buffer (30 used)
 
-// Diagnostic build only (-DFJSP_STAMPS): per-wave s_memtime deltas per step phase.
-// -DFJSP_STAMPS_FINE splits the action phase per agent: slots 0 synth, 1 pickup, 2 AGV,
-// 3 machines, 4 packaging, 5 run, 6 rewards + observe + stores, 7 auto-reset.
-#ifdef FJSP_STAMPS
-#define FJSP_STAMP_AT(E, i)                                \
-    do {                                                   \
-        uint64_t _t = __builtin_amdgcn_s_memtime();        \
-        (E).st_acc[i] += _t - (E).st_t0;                   \
-        (E).st_t0 = _t;                                    \
-    } while (0)
-#ifdef FJSP_STAMPS_FINE
-#define FJSP_STAMP(E, i)                                                          \
-    do {                                                                          \
-        constexpr int _m[7] = {0, -1, 5, 6, 6, 6, 7};                             \
-        if (_m[i] >= 0) FJSP_STAMP_AT(E, _m[i]);                                  \
-    } while (0)
-#define FJSP_STAMP_AGENT(E, a)                                                    \
-    do {                                                                          \
-        if ((a) == 0) FJSP_STAMP_AT(E, 1);                                        \
-        if ((a) == 1) FJSP_STAMP_AT(E, 2);                                        \
-        if ((a) == 3) FJSP_STAMP_AT(E, 3);                                        \
-        if ((a) == 7) FJSP_STAMP_AT(E, 4);                                        \
-    } while (0)
-#else
-#define FJSP_STAMP(E, i) FJSP_STAMP_AT(E, i)
-#define FJSP_STAMP_AGENT(E, a) ((void)0)
-#endif
-#else
-#define FJSP_STAMP(E, i) ((void)0)
-#define FJSP_STAMP_AGENT(E, a) ((void)0)
-#endif
+// Diagnostic phase stamps: fjsp_stamps.h (FJSP_STAMP, FJSP_STAMP_AGENT; nothing in the product build).
 
 // Per-env register state: 30 packed u32 words, bit-identical to the HBM `words` rows, so
 // loading / storing an env is a plain copy and the live state costs 30 VGPRs instead of ~95.
@@ -188,9 +160,7 @@ constexpr int NSTATE = 30;
 
 struct Env {
     uint32_t w[NSTATE];
-#ifdef FJSP_STAMPS
-    uint64_t st_acc[8], st_t0;
-#endif
+    FJSP_DIAG(uint64_t st_acc[8], st_t0;)
     FJSP_DEV uint32_t bf(int i, int o, int b) const { return (w[i] >> o) & ((1u << b) - 1u); }
     FJSP_DEV void sbf(int i, int o, int b, uint32_t v) {
         const uint32_t m = ((1u << b) - 1u) << o;

@@ -22,6 +22,7 @@
 #include <type_traits>
 
 #include "fjsp_env.h"
+#include "fjsp_stamps.h"
 #include "../../include/fjsp.h"
 
 using namespace fjsp;
@@ -30,17 +31,11 @@ namespace {
 
 constexpr int BLOCK = 64;
 constexpr int MT_N = 624;
-#ifdef FJSP_STAMPS
-__device__ unsigned long long g_stamps[8];
-__device__ unsigned long long g_pgstamps[4];   // pre-draw wave: busy cycles, active steps, busy in active steps, steps
-__device__ unsigned long long g_emitstamps[4];   // emit waves 1, 2: busy cycles, steps
-__device__ unsigned long long g_agstamps[64];   // k_step_ag (scripts/diag_ag_stamps.py)   // k_step_ag: per wave [busy, wait] cycles, epochs
-#define AG_T0() const uint64_t _ag_t0 = __builtin_amdgcn_s_memtime()
-#define AG_ACC(v) ((v) += __builtin_amdgcn_s_memtime() - _ag_t0)
-#else
-#define AG_T0() ((void)0)
-#define AG_ACC(v) ((void)0)
-#endif
+// diagnostic builds only (fjsp_stamps.h)
+FJSP_DIAG(__device__ unsigned long long g_stamps[8];
+          __device__ unsigned long long g_pgstamps[4];     // pre-draw wave: busy cycles, active steps, busy in active steps, steps
+          __device__ unsigned long long g_emitstamps[4];   // emit waves 1, 2: busy cycles, steps
+          __device__ unsigned long long g_agstamps[64];)   // k_step_ag per wave [busy, wait] cycles, marks (scripts/diag_ag_stamps.py)
 
 struct DevState {
     uint32_t* words;
@@ -490,9 +485,9 @@ __device__ __forceinline__ void step_and_emit(Env& E, const Tables& T, const Cfg
 template <bool CANON>
 __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t* __restrict__ actions, uint64_t order_packed,
                                                 int autoreset, fjsp_out out) {
-#ifdef FJSP_STAMPS
+    FJSP_DIAG(
     const uint64_t t_entry = __builtin_amdgcn_s_memtime();
-#endif
+    )
     __shared__ double s_lut[RLUT_SIZE];
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     const bool valid = e < S.n;
@@ -508,29 +503,30 @@ __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t
     __syncthreads();
     C.lut = s_lut;
     if (!valid) return;
-#ifdef FJSP_STAMPS
+    FJSP_DIAG(
     const uint64_t t_lut = __builtin_amdgcn_s_memtime();
-#endif
+    )
     Tables T = tables_of(S, e);
     uint8_t order[NA];
 #pragma unroll
     for (int i = 0; i < NA; i++) order[i] = (uint8_t)(order_packed >> (8 * i));
-#ifdef FJSP_STAMPS   // slots: 0 entry -> LUT -> state + action loads landed, 1 action phase, 2 run,
+                     // slots: 0 entry -> LUT -> state + action loads landed, 1 action phase, 2 run,
+                     FJSP_DIAG(
                      // 3 rewards, 4 observe, 5 term / trunc / status, 6 auto-reset + next obs, 7 state store drained
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (int i = 0; i < 8; i++) E.st_acc[i] = 0;
     E.st_t0 = __builtin_amdgcn_s_memtime();
     E.st_acc[0] = E.st_t0 - t_entry;
     (void)t_lut;
-#endif
+                     )
     step_and_emit<CANON>(E, T, C, S, e, act, order, autoreset, out, 0);
     env_store(E, S.words, S.n, e);
-#ifdef FJSP_STAMPS
+    FJSP_DIAG(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     FJSP_STAMP_AT(E, 7);
     if (threadIdx.x == 0)
         for (int i = 0; i < 8; i++) atomicAdd((unsigned long long*)&g_stamps[i], (unsigned long long)E.st_acc[i]);
-#endif
+    )
 }
 
 // The env's order table and used tray-slot prefix into LDS tables (one lane per env): the
@@ -599,10 +595,10 @@ __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, u
     } else {
         T = tables_of(S, e);
     }
-#ifdef FJSP_STAMPS
+    FJSP_DIAG(
     for (int i = 0; i < 8; i++) E.st_acc[i] = 0;
     E.st_t0 = __builtin_amdgcn_s_memtime();
-#endif
+    )
     for (int k = 0; k < K; k++) {
         int act[NA];
         synth_actions(seed, gid0 + (uint32_t)e, step0 + (uint32_t)k, mode, E, T, C, act);
@@ -621,10 +617,10 @@ __global__ void __launch_bounds__(BLOCK) k_step_many(DevState S, Cfg C, int K, u
         }
     }
     env_store(E, S.words, S.n, e);
-#ifdef FJSP_STAMPS
+    FJSP_DIAG(
     if (lane == 0)
         for (int i = 0; i < 8; i++) atomicAdd((unsigned long long*)&g_stamps[i], (unsigned long long)E.st_acc[i]);
-#endif
+    )
 }
 
 // K fused steps, pipelined over 2 or 3 wavefronts per 64-env workgroup (lean outputs only).
@@ -742,14 +738,14 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
             src = ((pg >> 21) & 1u) ^ (nord > 0 ? 1u : 0u);
         }
     }
-#ifdef FJSP_STAMPS
+    FJSP_DIAG(
     uint64_t pg_busy = 0, pg_act = 0, pg_busy_act = 0, pg_ph[3] = {0, 0, 0};
-#endif
+    )
     for (int k = 0; k <= K; k++) {
-#ifdef FJSP_STAMPS
+        FJSP_DIAG(
         const uint64_t pt0 = __builtin_amdgcn_s_memtime();
         bool pg_active = false;
-#endif
+        )
         if (valid) {
             const uint32_t si = s_mb[0][k & 1][lane];
             if ((si & 0xFFu) != my) {   // a new episode: start over from its stream position
@@ -802,23 +798,23 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
                 }
             }
         };
-#ifdef FJSP_STAMPS
+        FJSP_DIAG(
         const uint64_t pt1 = __builtin_amdgcn_s_memtime();
-#endif
+        )
         const int promote = ph;   // ASYNC: ph == 4 lanes become drawable after this step's draw
         uint64_t need = __ballot(valid && ph == 1);
-#ifdef FJSP_STAMPS
+        FJSP_DIAG(
         pg_active = need != 0 || __ballot(valid && ph == 2) != 0;
-#endif
+        )
         if (ASYNC) {
             // the draw first (its runs were loaded two steps ago), then last step's rows (loaded
             // after that step's prefetches), then this step's row loads: each wait is for loads
             // a step old, never for the ones just issued (vmcnt counts in order)
             draw_step();
-#ifdef FJSP_STAMPS
+            FJSP_DIAG(
             const uint64_t pt2 = __builtin_amdgcn_s_memtime();
             if (pg_active) { pg_ph[0] += pt1 - pt0; pg_ph[1] += pt2 - pt1; }
-#endif
+            )
             if (ASYNC && inflight) {   // last step's row DMAs: store them, the lanes draw from the next step on
                 const int pb = (k - 1) & 1;
 #pragma unroll
@@ -892,18 +888,18 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
             s_mb[2][(k + 1) & 1][lane] = (ph == 3 ? 1u : 0u) | (my << 1) | ((uint32_t)nord << 9);
             s_mb[3][(k + 1) & 1][lane] = (uint32_t)pos | ((uint32_t)g << 16) | (wrow << 31);
         }
-#ifdef FJSP_STAMPS
+        FJSP_DIAG(
         {
             const uint64_t dt = __builtin_amdgcn_s_memtime() - pt0;
             pg_busy += dt;
             if (pg_active) { pg_act += 1; pg_busy_act += dt; }
             (void)pg_ph;
         }
-#endif
+        )
         __syncthreads();
     }
     if (ASYNC) __builtin_amdgcn_s_waitcnt(0x0F70);   // no LDS DMA outlives the workgroup
-#ifdef FJSP_STAMPS
+    FJSP_DIAG(
     if (lane == 0) {
         atomicAdd(&g_pgstamps[0], (unsigned long long)pg_busy);
         atomicAdd(&g_pgstamps[1], (unsigned long long)pg_act);
@@ -911,7 +907,7 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
         atomicAdd(&g_pgstamps[3], (unsigned long long)(K + 1));
         if (ASYNC) { atomicAdd(&g_agstamps[52], (unsigned long long)pg_ph[0]); atomicAdd(&g_agstamps[53], (unsigned long long)pg_ph[1]); }
     }
-#endif
+    )
     if (valid) {
         uint32_t pg = 0;
         if (FINAL_MB && (s_mb[0][(K + 1) & 1][lane] & 0xFFu) != my) ph = 0;   // reset in the final epoch
@@ -1001,10 +997,10 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
             T.stride = BLOCK;
             if (valid) tables_copy_in(S, T, e, E.norders(), E.slot_next());
         }
-#ifdef FJSP_STAMPS
+        FJSP_DIAG(
         for (int i = 0; i < 8; i++) E.st_acc[i] = 0;
         E.st_t0 = __builtin_amdgcn_s_memtime();
-#endif
+        )
         int epi = 0;   // episodes started in this launch (mod 256), the pre-draw tag
         bool fresh = true;   // this step's pickup runs here (first step of the launch / after a reset)
         for (int k = 0; k <= K; k++) {
@@ -1102,10 +1098,10 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
             }
             env_store(E, S.words, S.n, e);
         }
-#ifdef FJSP_STAMPS
+        FJSP_DIAG(
         if (lane == 0)
             for (int i = 0; i < 8; i++) atomicAdd((unsigned long long*)&g_stamps[i], (unsigned long long)E.st_acc[i]);
-#endif
+        )
     } else if (PG && wave == 1 + NEMIT) {
         predraw_wave<CR, PB>(S, K, lane, e, valid, (size_t)blockIdx.x * BLOCK, s_mb, s_cp, s_nxt);
     } else {
@@ -1113,13 +1109,13 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
         // observation fields (+ the next step's uniform actions), wave 2 int8 fields, masks,
         // term, trunc, status.  NEMIT == 1 (many envs: the CUs are already full): one wave.
         const int part = wave - 1;
-#ifdef FJSP_STAMPS
+        FJSP_DIAG(
         uint64_t em_busy = 0;
-#endif
+        )
         for (int k = 0; k <= K; k++) {
-#ifdef FJSP_STAMPS
+            FJSP_DIAG(
             const uint64_t et0 = __builtin_amdgcn_s_memtime();
-#endif
+            )
             // order within a step (PG): wave 1 first draws step k + 1's actions, writes step
             // k - 1's rewards and runs step k + 1's pickup as soon as the sim wave posts (early
             // in step k), then the observation fields; wave 2 writes its fields, then runs step
@@ -1220,17 +1216,17 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
                     }
                 }
             }
-#ifdef FJSP_STAMPS
+            FJSP_DIAG(
             em_busy += __builtin_amdgcn_s_memtime() - et0;
-#endif
+            )
             __syncthreads();
         }
-#ifdef FJSP_STAMPS
+        FJSP_DIAG(
         if (lane == 0 && part < 2) {
             atomicAdd(&g_emitstamps[2 * part], (unsigned long long)em_busy);
             atomicAdd(&g_emitstamps[2 * part + 1], (unsigned long long)(K + 1));
         }
-#endif
+        )
     }
 }
 
@@ -1384,9 +1380,9 @@ template <int EPW>
 __global__ void __launch_bounds__(AG_WAVES * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2)))
 k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0, int autoreset, fjsp_out out) {
     static_assert(EPW == 64 || EPW == 32 || EPW == 16, "envs per workgroup");
-#ifdef FJSP_STAMPS
+    FJSP_DIAG(
     const uint64_t t_entry = __builtin_amdgcn_s_memtime();
-#endif
+    )
     // pre-draw work per step: the draw costs more than its loads' latency here (PD shares its
     // SIMD with E0), so four words per step (~33 steps for 30 orders) beat eight (measured)
     constexpr int CR = PG_CR, PB = AG_PB;
@@ -1417,25 +1413,9 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     const bool valid = lane < EPW && e < S.n;
     const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
     const Tables TL{s_orders + lane, s_code + lane, s_next + lane, s_cstep + lane, BLOCK};
-#ifdef FJSP_STAMPS
-    uint64_t ag_busy = 0, ag_wait = 0;   // per step: busy until the barrier; AM: until post 1, K / P: spinning
-    uint64_t amt[6] = {0, 0, 0, 0, 0, 0};   // AM: cycles into the step at its phase marks
-    uint64_t ag_last = 0;                    // steps this wave arrived last at the barrier
-#define AG_BARRIER()                                                        \
-    do {                                                                    \
-        const uint64_t _b0 = __builtin_amdgcn_s_memtime();                 \
-        __syncthreads();                                                    \
-        ag_last += (__builtin_amdgcn_s_memtime() - _b0) < 200 ? 1 : 0;     \
-    } while (0)
-#define AG_SPIN_T0() const uint64_t _ag_w0 = __builtin_amdgcn_s_memtime()
-#define AG_SPIN_ACC() (ag_wait += __builtin_amdgcn_s_memtime() - _ag_w0)
-#define AG_MARK(i) (amt[i] += __builtin_amdgcn_s_memtime() - _ag_t0)
-#else
-#define AG_BARRIER() __syncthreads()
-#define AG_SPIN_T0() ((void)0)
-#define AG_SPIN_ACC() ((void)0)
-#define AG_MARK(i) ((void)0)
-#endif
+    FJSP_DIAG(uint64_t ag_busy = 0, ag_wait = 0;   // per step: busy until the barrier; AM: until post 1, K / P: spinning
+              uint64_t amt[6] = {0, 0, 0, 0, 0, 0};   // AM: cycles into the step at its phase marks
+              uint64_t ag_last = 0;)                   // steps this wave arrived last at the barrier
     if (wave == AG_P) {   // the first two steps' actions
         for (int j = 0; j < 2 && j < K; j++) {
             int act[NA];
@@ -1515,18 +1495,19 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         }
     }
     __syncthreads();
-#ifdef FJSP_STAMPS   // [56] launch prologue (entry -> tables in LDS), summed over workgroups
+    // [56] launch prologue (entry -> tables in LDS), summed over workgroups
+    FJSP_DIAG(
     if (threadIdx.x == 0) atomicAdd(&g_agstamps[56], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_entry));
-#endif
+    )
     if (wave == AG_AM) {
         __builtin_amdgcn_s_setprio(3);   // the machines -> AGV chain is the critical path
         Env E;
         if (valid) env_load(E, S.words, S.n, e);
         int epi = 0;
         bool fresh = true, trunc_prev = false;
-#ifdef FJSP_STAMPS
+        FJSP_DIAG(
         const uint64_t loop_t0 = __builtin_amdgcn_s_memtime();
-#endif
+        )
         for (int k = 0; k <= K; k++) {
             AG_T0();
             AG_MARK(0);
@@ -1620,9 +1601,9 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             AG_ACC(ag_busy);
             AG_BARRIER();
         }
-#ifdef FJSP_STAMPS
+        FJSP_DIAG(
         if (lane == 0) atomicAdd(&g_agstamps[24], (unsigned long long)(__builtin_amdgcn_s_memtime() - loop_t0));
-#endif
+        )
         if (valid) {
             s_act[0][0][lane] = (uint32_t)E.norders();   // for the copy-out by all waves below
             s_act[0][1][lane] = (uint32_t)E.slot_next();
@@ -1827,9 +1808,9 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 const uint32_t t = (uint32_t)(k - 1);
                 uint32_t v[SNAP_N];
                 snap_get(snap[(k - 1) & 1], lane, v);
-#ifdef FJSP_STAMPS
+                FJSP_DIAG(
                 __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the snapshot arrived
-#endif
+                )
                 AG_MARK(1);
                 ag_emit(part, v, t, n, ue, C, out);
             }
@@ -1839,9 +1820,9 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         }
     }
     __syncthreads();
-#ifdef FJSP_STAMPS
+    FJSP_DIAG(
     const uint64_t t_out = __builtin_amdgcn_s_memtime();
-#endif
+    )
     if (valid) {   // the order table and the used slot prefix back to HBM, rows r = wave (mod 8)
         const uint32_t no = s_act[0][0][lane], ns = s_act[0][1][lane];
         for (uint32_t o = (uint32_t)wave; o < no; o += AG_WAVES) S.orders[(size_t)o * n + e] = TL.orders[o * BLOCK];
@@ -1851,7 +1832,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             S.scstep[(size_t)q * n + e] = TL.scstep[q * BLOCK];
         }
     }
-#ifdef FJSP_STAMPS
+    FJSP_DIAG(
     // stamp slots by role: AM 0, E0 1, K 2, E1 3, P 4, PD 5, E2 6, E3 7 (scripts/diag_ag_stamps.py):
     // [2 slot] busy, [2 slot + 1] wait, [16] steps, [17] SIMD map, [18..23] AM marks, [24] AM wall,
     // [25 + slot] last arrivals
@@ -1881,7 +1862,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         if (wave == AG_E2)   // top, the snapshot, the stores
             for (int i = 0; i < 4; i++) atomicAdd(&g_agstamps[46 + i], (unsigned long long)amt[i]);
     }
-#endif
+    )
 }
 
 // transition_memory.py:83-105 over a [T][M] rollout buffer; column m = a*N + e
@@ -2330,7 +2311,7 @@ extern "C" int fjsp_debug_stamps(unsigned long long* out) {
 extern "C" int fjsp_debug_agstamps(unsigned long long* out) {   // out[16]: k_step_ag per wave busy / wait, epochs
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_agstamps), sizeof(unsigned long long) * 64));
-    unsigned long long z[56] = {0};
+    unsigned long long z[64] = {0};
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_agstamps), z, sizeof(z)));
     return 0;
 }
