@@ -697,8 +697,9 @@ class VecMultiAgentA2C:
         self.act_dims = dict(zip(AGENTS, N_ACTIONS))
         self.global_obs_dim = GLOBAL_DIM
         self.actors, self.critic = init_networks(seed, hidden, self.device)
-        self.optim_actor = torch.optim.Adam(self.actors.parameters(), lr=lr_actor)
-        self.optim_critic = torch.optim.Adam(self.critic.parameters(), lr=lr_critic)
+        fused = self.device.type == "cuda"      # one multi-tensor kernel per step (same Adam math)
+        self.optim_actor = torch.optim.Adam(self.actors.parameters(), lr=lr_actor, fused=fused)
+        self.optim_critic = torch.optim.Adam(self.critic.parameters(), lr=lr_critic, fused=fused)
         self.gidx = gather_index(self.device)
         self.midx = mask_index(self.device)
         self.actor_loss_history = {a: [] for a in AGENTS}

@@ -27,6 +27,7 @@ L.collect()
 ret, adv = L.advantages()
 b = L._bufs
 T = L.batch_size
+print("optimizer defaults:", L.optim_actor.defaults.get("fused"), file=sys.stderr)
 feats, masks, actions = b["feats"][:T], b["masks"][:T], b["actions"]
 
 
