@@ -276,6 +276,13 @@ int fjsp_a2c_group_verify(const float* feats, int32_t T, int32_t n, const int64_
 int fjsp_a2c_actor_head(const float* pu, int32_t umax, const int64_t* inv, int32_t T, int32_t n, const int8_t* masks,
                         const int64_t* actions, const float* adv_n, float inv_count, float ent_coef, float* grad,
                         double* sums, void* stream);
+/* ReLU backward fused with the bias gradient (the critic backward of the A2C update,
+ * a2c.py:713-722 calc_critic_loss through the 256-256-128 ReLU layers): gy, y f32 [rows][cols]
+ * (y = the layer's ReLU output), cols 128 or 256.  Out: g f32 [rows][cols] = gy where y > 0
+ * else 0, part f32 [ceil(rows / 128)][cols] = column sums of g per block of 128 rows (the
+ * caller adds the blocks).  Stream-ordered. */
+int fjsp_a2c_relu_bias_grad(const float* gy, const float* y, int64_t rows, int32_t cols, float* g, float* part,
+                            void* stream);
 int fjsp_snapshot(fjsp_handle* h, void* dst);
 int fjsp_restore(fjsp_handle* h, const void* src);
 /* Kernel timing of the last fjsp_step_many / fjsp_step launch in ms (hipEvents on the

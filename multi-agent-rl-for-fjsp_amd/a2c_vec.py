@@ -84,7 +84,10 @@ class _LinearSplitK(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, W, y = ctx.saved_tensors
-        if ctx.relu:
+        gb = None
+        if ctx.relu and gy.is_cuda and W.shape[0] in (128, 256):
+            gy, gb = _relu_bias_grad(gy.contiguous(), y)            # one pass (HIP kernel)
+        elif ctx.relu:
             gy = torch.ops.aten.threshold_backward(gy, y, 0.0)      # relu' from the output
         B = x.shape[0]
         c = max(1, min(64, B // 8192))
@@ -96,7 +99,19 @@ class _LinearSplitK(torch.autograd.Function):
         if c * bc < B:
             gW += gy[c * bc:].t() @ x[c * bc:]
         gx = gy @ W if ctx.needs_input_grad[0] else None
-        return gx, gW, gy.sum(0), None
+        return gx, gW, gy.sum(0) if gb is None else gb, None
+
+
+def _relu_bias_grad(gy, y):
+    """(gy where y > 0 else 0, its column sums) for y [B, C] = a ReLU output, gy [B, C]
+    contiguous f32 on the GPU: fjsp_a2c_relu_bias_grad."""
+    B, C = y.shape
+    g = torch.empty_like(gy)
+    part = torch.empty(-(-B // 128), C, dtype=torch.float32, device=gy.device)
+    stream = torch.cuda.current_stream(gy.device).cuda_stream
+    V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    nat.check(nat.lib().fjsp_a2c_relu_bias_grad(V(gy), V(y), B, C, V(g), V(part), ctypes.c_void_p(stream)))
+    return g, part.sum(0)
 
 
 def mlp_forward(seq, x):

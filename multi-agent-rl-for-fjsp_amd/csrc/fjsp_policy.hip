@@ -410,6 +410,41 @@ __global__ void __launch_bounds__(256) k_group_verify(const float* __restrict__ 
     if (threadIdx.x == 0) bad[blockIdx.x] = diff ? 1 : 0;
 }
 
+// ReLU backward fused with the bias gradient of the layer under it (the critic's split-K
+// backward, a2c_vec._LinearSplitK): g = gy where y > 0 else 0 for y = relu(x W^T + b) [rows][C],
+// and part[block][c] = sum of g[r][c] over the workgroup's RB rows (the caller sums the
+// blocks).  One pass over gy and y instead of a threshold pass plus a column reduction.
+// 256 threads = (256 / (C / 4)) rows x (C / 4) float4 columns.
+template <int C>
+__global__ void __launch_bounds__(256) k_relu_bias_grad(const float* __restrict__ gy, const float* __restrict__ y,
+                                                        int64_t rows, float* __restrict__ g,
+                                                        float* __restrict__ part) {
+    constexpr int Q = C / 4, RP = 256 / Q, RB = 128;
+    const int q = threadIdx.x % Q, rr = threadIdx.x / Q;
+    const int64_t r0 = (int64_t)blockIdx.x * RB;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = rr; i < RB; i += RP) {
+        const int64_t r = r0 + i;
+        if (r >= rows) break;
+        const float4 a = reinterpret_cast<const float4*>(gy + r * C)[q];
+        const float4 v = reinterpret_cast<const float4*>(y + r * C)[q];
+        const float4 o = make_float4(v.x > 0.f ? a.x : 0.f, v.y > 0.f ? a.y : 0.f, v.z > 0.f ? a.z : 0.f,
+                                     v.w > 0.f ? a.w : 0.f);
+        reinterpret_cast<float4*>(g + r * C)[q] = o;
+        acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+    }
+    __shared__ float4 s_acc[256];
+    s_acc[threadIdx.x] = acc;
+    __syncthreads();
+    if (rr == 0) {
+        for (int k = 1; k < RP; k++) {
+            const float4 b = s_acc[k * Q + q];
+            acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
+        }
+        reinterpret_cast<float4*>(part + (size_t)blockIdx.x * C)[q] = acc;
+    }
+}
+
 }  // namespace
 
 int fjsp_internal_fail(const char* msg);   // fjsp_hip.hip: sets fjsp_last_error()
@@ -452,6 +487,24 @@ extern "C" int fjsp_a2c_group_verify(const float* feats, int32_t T, int32_t n, c
     const size_t S = (size_t)T * (size_t)n;
     hipLaunchKernelGGL(k_group_verify, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, feats, T,
                        n, rep_a, rep_c, bad);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int fjsp_a2c_relu_bias_grad(const float* gy, const float* y, int64_t rows, int32_t cols, float* g,
+                                       float* part, void* stream) {
+    if (rows <= 0) return fjsp_internal_fail("fjsp_a2c_relu_bias_grad: rows must be > 0");
+    if (cols != 128 && cols != 256) return fjsp_internal_fail("fjsp_a2c_relu_bias_grad: cols must be 128 or 256");
+    if (!gy || !y || !g || !part) return fjsp_internal_fail("fjsp_a2c_relu_bias_grad: null buffer");
+    const dim3 grid((unsigned)((rows + 127) / 128));
+    if (cols == 256)
+        hipLaunchKernelGGL(k_relu_bias_grad<256>, grid, dim3(256), 0, (hipStream_t)stream, gy, y, rows, g, part);
+    else
+        hipLaunchKernelGGL(k_relu_bias_grad<128>, grid, dim3(256), 0, (hipStream_t)stream, gy, y, rows, g, part);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));
