@@ -368,11 +368,11 @@ class RowGroups:
 
     def __init__(self, keys):
         R, S = keys.shape
-        assert R <= 8, "the row id lives in bits 60..62 of the sort key"
+        assert R <= 16, "the row id lives in bits 59..62 of the sort key"
         dev = keys.device
-        # one flat sort for all rows: the row in bits 60..62 above 60 bits of the key (the
+        # one flat sort for all rows: the row in bits 59..62 above 59 bits of the key (the
         # grouping is verified by the caller, so a shorter key only risks a dense fallback)
-        flat = (keys & ((1 << 60) - 1)) | (torch.arange(R, device=dev, dtype=torch.int64)[:, None] << 60)
+        flat = (keys & ((1 << 59) - 1)) | (torch.arange(R, device=dev, dtype=torch.int64)[:, None] << 59)
         sk, fperm = torch.sort(flat.view(-1))
         sk = sk.view(R, S)
         perm = (fperm.view(R, S) - torch.arange(R, device=dev, dtype=torch.int64)[:, None] * S)
@@ -389,6 +389,15 @@ class RowGroups:
         self.inv = torch.empty_like(perm).scatter_(1, perm, seg)
         self.rep = torch.gather(self.first, 1, self.inv)
         self.perm = perm
+
+    def rows(self, lo, hi):
+        """The groupings of rows lo..hi-1 alone (views; Umax = their own largest count)."""
+        g = RowGroups.__new__(RowGroups)
+        g.U = self.U[lo:hi]
+        um = max(g.U)
+        g.first, g.ends = self.first[lo:hi, :um], self.ends[lo:hi, :um]
+        g.inv, g.rep, g.perm = self.inv[lo:hi], self.rep[lo:hi], self.perm[lo:hi]
+        return g
 
     def gather(self, y):
         """y [R, C, Umax] per group -> [R, C, S] per sample; backward: each group's sample
@@ -544,8 +553,8 @@ class A2CLosses:
         ga = gc = None
         if dedup:
             f3 = f3.contiguous()
-            keys = group_keys(f3)
-            ga, gc = RowGroups(keys[:NA]), RowGroups(keys[NA:])
+            gr = RowGroups(group_keys(f3))                          # 8 actor rows + the critic's
+            ga, gc = gr.rows(0, NA), gr.rows(NA, NA + 1)
             if not group_verify(f3, ga, gc, x, gt):                 # a hash collision: dense
                 ga = gc = None
                 if x is None:

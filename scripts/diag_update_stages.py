@@ -52,10 +52,9 @@ def run(st):
     mark("critic_T")
     keys = A.group_keys(f3)
     mark("group_keys")
-    ga = A.RowGroups(keys[:A.NA])
-    mark("RowGroups_actors")
-    gc = A.RowGroups(keys[A.NA:])
-    mark("RowGroups_critic")
+    gr = A.RowGroups(keys)
+    ga, gc = gr.rows(0, A.NA), gr.rows(A.NA, A.NA + 1)
+    mark("RowGroups")
     assert A.group_verify(f3, ga, gc)
     mark("verify")
 
