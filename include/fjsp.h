@@ -283,6 +283,14 @@ int fjsp_a2c_actor_head(const float* pu, int32_t umax, const int64_t* inv, int32
  * caller adds the blocks).  Stream-ordered. */
 int fjsp_a2c_relu_bias_grad(const float* gy, const float* y, int64_t rows, int32_t cols, float* g, float* part,
                             void* stream);
+/* Backward of the critic's last two layers (a2c.py:153-166 critic 256 -> 128 ReLU -> 1):
+ * y f32 [rows][128] = the 128-wide ReLU output, gv f32 [rows] = d loss / d value, w4 f32 [128]
+ * = the value head's weights.  Out: g f32 [rows][128] = gv w4 where y > 0 else 0 (the gradient
+ * at the 128-wide layer's pre-activation), part f32 [ceil(rows / 128)][260] per block of 128
+ * rows: [0, 128) column sums of g (bias gradient), [128, 256) sums of gv y (w4's gradient),
+ * [256] sum of gv (the value bias's gradient), [257, 260) zero.  Stream-ordered. */
+int fjsp_a2c_value_head_grad(const float* y, const float* gv, const float* w4, int64_t rows, float* g, float* part,
+                             void* stream);
 int fjsp_snapshot(fjsp_handle* h, void* dst);
 int fjsp_restore(fjsp_handle* h, const void* src);
 /* Kernel timing of the last fjsp_step_many / fjsp_step launch in ms (hipEvents on the

@@ -89,17 +89,57 @@ class _LinearSplitK(torch.autograd.Function):
             gy, gb = _relu_bias_grad(gy.contiguous(), y)            # one pass (HIP kernel)
         elif ctx.relu:
             gy = torch.ops.aten.threshold_backward(gy, y, 0.0)      # relu' from the output
-        B = x.shape[0]
-        c = max(1, min(64, B // 8192))
-        bc = B // c
-        # c chunks of bc rows as strided views (no padded copies), the B - c*bc tail apart
-        xc = x[:c * bc].reshape(c, bc, -1)
-        gc = gy[:c * bc].reshape(c, bc, -1)
-        gW = torch.bmm(gc.transpose(1, 2), xc).sum(0)
-        if c * bc < B:
-            gW += gy[c * bc:].t() @ x[c * bc:]
-        gx = gy @ W if ctx.needs_input_grad[0] else None
+        gW = _splitk_wgrad(gy, x)
+        gx = None
+        if ctx.needs_input_grad[0]:
+            # one output (the value head): an outer product, elementwise (a K = 1 GEMM is slow)
+            gx = gy * W if W.shape[0] == 1 else gy @ W
         return gx, gW, gy.sum(0) if gb is None else gb, None
+
+
+def _splitk_wgrad(gy, x):
+    """gy^T x over a long batch B: c chunks of B // c rows as strided views (no padded copies)
+    in one batched GEMM, summed; the B - c * (B // c) tail apart."""
+    B = x.shape[0]
+    c = max(1, min(64, B // 8192))
+    bc = B // c
+    xc = x[:c * bc].reshape(c, bc, -1)
+    gc = gy[:c * bc].reshape(c, bc, -1)
+    if x.stride(0) == 1:   # x a transposed [in, B] slab (the first layer): (x^T g)^T, both operands natural
+        gW = torch.bmm(xc.transpose(1, 2), gc).sum(0).t()
+    else:
+        gW = torch.bmm(gc.transpose(1, 2), xc).sum(0)
+    if c * bc < B:
+        gW += gy[c * bc:].t() @ x[c * bc:]
+    return gW
+
+
+class _ValueHead(torch.autograd.Function):
+    """The critic's last two layers v = relu(h W3^T + b3) w4^T + b4 over a long batch on the
+    GPU; backward: layer 3's ReLU and bias gradient, the value head's weight and bias gradient
+    and the gradient into layer 3 in one pass over the 128-wide activations
+    (fjsp_a2c_value_head_grad), then layer 3's split-K weight gradient."""
+
+    @staticmethod
+    def forward(ctx, h, W3, b3, W4, b4):
+        y = torch._addmm_activation(b3, h, W3.t())
+        ctx.save_for_backward(h, W3, y, W4)
+        return torch.addmm(b4, y, W4.t())
+
+    @staticmethod
+    def backward(ctx, gv):
+        h, W3, y, W4 = ctx.saved_tensors
+        B, C = y.shape
+        gvc = gv.reshape(-1).contiguous()
+        w4 = W4.reshape(-1).contiguous()
+        g = torch.empty_like(y)
+        part = torch.empty(-(-B // 128), 2 * C + 4, dtype=torch.float32, device=y.device)
+        stream = torch.cuda.current_stream(y.device).cuda_stream
+        V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        nat.check(nat.lib().fjsp_a2c_value_head_grad(V(y), V(gvc), V(w4), B, V(g), V(part), ctypes.c_void_p(stream)))
+        ps = part.sum(0)
+        gh = g @ W3 if ctx.needs_input_grad[0] else None
+        return gh, _splitk_wgrad(g, h), ps[:C], ps[C:2 * C].view(1, C), ps[2 * C:2 * C + 1]
 
 
 def _relu_bias_grad(gy, y):
@@ -121,6 +161,10 @@ def mlp_forward(seq, x):
     i = 0
     while i < len(mods):
         m = mods[i]
+        if (x.is_cuda and x.shape[0] >= 65536 and i + 3 == len(mods) and isinstance(m, nn.Linear)
+                and isinstance(mods[i + 1], nn.ReLU) and isinstance(mods[i + 2], nn.Linear)
+                and mods[i + 2].out_features == 1 and m.out_features == 128):
+            return _ValueHead.apply(x, m.weight, m.bias, mods[i + 2].weight, mods[i + 2].bias)
         if isinstance(m, nn.Linear) and x.shape[0] >= 65536:
             relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
             x = _LinearSplitK.apply(x, m.weight, m.bias, relu)
@@ -161,7 +205,14 @@ class ActorStack(nn.Module):
         return torch.softmax(self.logits(x), dim=1)
 
     def agent_probs(self, a, x):
-        """Actor a alone on x [13, B] -> probabilities [8, B] (the agent's slice of forward)."""
+        """Actor a alone on x [13, B] -> probabilities [8, B] (the agent's slice of forward);
+        a long batch through the split-K layers (a weight gradient with K = B and a [256, 13]
+        output is a handful of GEMM tiles)."""
+        if x.shape[1] >= 16384:
+            h = _LinearSplitK.apply(x.t(), self.W1[a], self.b1[a, :, 0], True)
+            h = _LinearSplitK.apply(h, self.W2[a], self.b2[a, :, 0], True)
+            z = _LinearSplitK.apply(h, self.W3[a], self.b3[a, :, 0], False)
+            return torch.softmax(z.t() + self.logit_pad[a], dim=0)
         h = torch.relu(torch.addmm(self.b1[a], self.W1[a], x))
         h = torch.relu(torch.addmm(self.b2[a], self.W2[a], h))
         return torch.softmax(torch.addmm(self.b3[a], self.W3[a], h) + self.logit_pad[a], dim=0)

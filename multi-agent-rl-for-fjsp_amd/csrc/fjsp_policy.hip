@@ -423,15 +423,19 @@ __global__ void __launch_bounds__(256) k_relu_bias_grad(const float* __restrict_
     const int q = threadIdx.x % Q, rr = threadIdx.x / Q;
     const int64_t r0 = (int64_t)blockIdx.x * RB;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = rr; i < RB; i += RP) {
-        const int64_t r = r0 + i;
-        if (r >= rows) break;
+    auto row = [&](int64_t r) {
         const float4 a = reinterpret_cast<const float4*>(gy + r * C)[q];
         const float4 v = reinterpret_cast<const float4*>(y + r * C)[q];
         const float4 o = make_float4(v.x > 0.f ? a.x : 0.f, v.y > 0.f ? a.y : 0.f, v.z > 0.f ? a.z : 0.f,
                                      v.w > 0.f ? a.w : 0.f);
         reinterpret_cast<float4*>(g + r * C)[q] = o;
         acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+    };
+    if (r0 + RB <= rows) {   // a full block: fixed trip count, loads batched by the unroll
+#pragma unroll 8
+        for (int i = rr; i < RB; i += RP) row(r0 + i);
+    } else {
+        for (int i = rr; i < RB && r0 + i < rows; i += RP) row(r0 + i);
     }
     __shared__ float4 s_acc[256];
     s_acc[threadIdx.x] = acc;
@@ -442,6 +446,59 @@ __global__ void __launch_bounds__(256) k_relu_bias_grad(const float* __restrict_
             acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
         }
         reinterpret_cast<float4*>(part + (size_t)blockIdx.x * C)[q] = acc;
+    }
+}
+
+// Backward of the critic's last two layers, y = relu(h W3^T + b3) [rows][128], v = y w4 + b4,
+// from the value gradient gv [rows] in one pass over y (a2c_vec._ValueHead): g = gv w4 where
+// y > 0 else 0 (the gradient into layer 3's pre-activation), and per block of 128 rows the
+// partial sums part[block][0..127] = sum g (layer 3's bias gradient), [128..255] = sum gv y
+// (w4's gradient), [256] = sum gv (b4's gradient), [257..259] = 0.
+__global__ void __launch_bounds__(256) k_value_head_grad(const float* __restrict__ y, const float* __restrict__ gv,
+                                                         const float* __restrict__ w4, int64_t rows,
+                                                         float* __restrict__ g, float* __restrict__ part) {
+    constexpr int C = 128, Q = C / 4, RP = 256 / Q, RB = 128, PW = 2 * C + 4;
+    const int q = threadIdx.x % Q, rr = threadIdx.x / Q;
+    const int64_t r0 = (int64_t)blockIdx.x * RB;
+    const float4 w = reinterpret_cast<const float4*>(w4)[q];
+    float4 ab = make_float4(0.f, 0.f, 0.f, 0.f), aw = ab;
+    float av = 0.f;
+    auto row = [&](int64_t r) {
+        const float gr = gv[r];
+        const float4 v = reinterpret_cast<const float4*>(y + r * C)[q];
+        const float4 o = make_float4(v.x > 0.f ? gr * w.x : 0.f, v.y > 0.f ? gr * w.y : 0.f,
+                                     v.z > 0.f ? gr * w.z : 0.f, v.w > 0.f ? gr * w.w : 0.f);
+        reinterpret_cast<float4*>(g + r * C)[q] = o;
+        ab.x += o.x; ab.y += o.y; ab.z += o.z; ab.w += o.w;
+        aw.x += gr * v.x; aw.y += gr * v.y; aw.z += gr * v.z; aw.w += gr * v.w;
+        av += gr;
+    };
+    if (r0 + RB <= rows) {
+#pragma unroll 8
+        for (int i = rr; i < RB; i += RP) row(r0 + i);
+    } else {
+        for (int i = rr; i < RB && r0 + i < rows; i += RP) row(r0 + i);
+    }
+    __shared__ float4 s_b[256], s_w[256];
+    __shared__ float s_v[256];
+    s_b[threadIdx.x] = ab;
+    s_w[threadIdx.x] = aw;
+    s_v[threadIdx.x] = q == 0 ? av : 0.f;
+    __syncthreads();
+    float* out = part + (size_t)blockIdx.x * PW;
+    if (rr == 0) {
+        for (int k = 1; k < RP; k++) {
+            const float4 b = s_b[k * Q + q], c = s_w[k * Q + q];
+            ab.x += b.x; ab.y += b.y; ab.z += b.z; ab.w += b.w;
+            aw.x += c.x; aw.y += c.y; aw.z += c.z; aw.w += c.w;
+        }
+        reinterpret_cast<float4*>(out)[q] = ab;
+        reinterpret_cast<float4*>(out + C)[q] = aw;
+    }
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int k = 0; k < RP; k++) t += s_v[k * Q];
+        reinterpret_cast<float4*>(out + 2 * C)[0] = make_float4(t, 0.f, 0.f, 0.f);
     }
 }
 
@@ -505,6 +562,20 @@ extern "C" int fjsp_a2c_relu_bias_grad(const float* gy, const float* y, int64_t 
         hipLaunchKernelGGL(k_relu_bias_grad<256>, grid, dim3(256), 0, (hipStream_t)stream, gy, y, rows, g, part);
     else
         hipLaunchKernelGGL(k_relu_bias_grad<128>, grid, dim3(256), 0, (hipStream_t)stream, gy, y, rows, g, part);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int fjsp_a2c_value_head_grad(const float* y, const float* gv, const float* w4, int64_t rows, float* g,
+                                        float* part, void* stream) {
+    if (rows <= 0) return fjsp_internal_fail("fjsp_a2c_value_head_grad: rows must be > 0");
+    if (!y || !gv || !w4 || !g || !part) return fjsp_internal_fail("fjsp_a2c_value_head_grad: null buffer");
+    hipLaunchKernelGGL(k_value_head_grad, dim3((unsigned)((rows + 127) / 128)), dim3(256), 0, (hipStream_t)stream, y,
+                       gv, w4, rows, g, part);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));
