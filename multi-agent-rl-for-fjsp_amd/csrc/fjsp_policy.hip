@@ -6,13 +6,14 @@
 // action draw (inverse CDF over the masked probabilities, or argmax) and the centralised
 // critic (networks.CentralizedCriticNetwork: 38 -> 256 -> 256 -> 128 -> 1).
 //
-// Grid: blockIdx.y = role (0 critic, 1..8 actor of agent y - 1), blockIdx.x = tile of 32 envs;
-// 256 threads = 4 wavefronts.  The hidden activations never leave LDS:
+// Grid: blockIdx.y = role (0 critic, 1..8 actor of agent y - 1), blockIdx.x = tile of 64 envs;
+// 512 threads = 8 wavefronts.  The hidden activations never leave LDS:
 //   x   [40][TILE]  inputs of the tile (feature rows of the kernel-written [38][N] slab)
 //   h   [256][TILE] layer 1, then layer 2, then the critic's layer 3 (in place: results stay in
-//                   registers across a barrier), so four workgroups fit a CU (37 KB of LDS each)
+//                   registers across a barrier), so two workgroups fit a CU (74 KB of LDS each)
 // Every layer with K >= 16 runs on v_mfma_f32_32x32x2_f32 (exact f32 fma chains): each wave
-// owns 64 output rows = 2 x 2 tiles of 32 x 32 (the critic's 128-row layer 3: one tile row).
+// owns 32 output rows x the tile's 64 envs = two 32 x 32 tiles sharing one weight fragment (the
+// critic's 128-row layer 3: waves 0..3).
 // The actor's 256 -> n_a logits and the critic's 128 -> 1 value are VALU dot products.
 // MFMA A operands (weights) are pre-packed on the host per (row tile, k-step) in lane order
 // (fjsp_pack_policy_weights layout below), so each k-step's A fragment is one coalesced
@@ -28,12 +29,15 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// 32 envs per workgroup: 37 KB of LDS and 113 VGPRs, so four workgroups share a CU and the 1 152
-// workgroups of a 4 096-env step run in 1.1 rounds of 1 024 slots (64-env tiles: 576 workgroups
-// in 1.1 rounds of 512, two waves per SIMD to hide the weight loads; measured 77.8 -> 68.2 us)
-constexpr int TILE = 32;              // envs per workgroup
+// 64 envs per workgroup on 8 waves: each weight fragment loaded from L2 feeds two MFMAs (one
+// per 32-env column tile), half the weight traffic of 32-env tiles at the same waves per CU
+// (two 74 KB workgroups = 16 waves).  The weight loads, one 256-byte A fragment per MFMA with
+// 32-env tiles, are what bounds this kernel: 4 SIMDs x 256 B per 16-cycle MFMA = the CU's
+// 64 B/clk vector-memory path.
+constexpr int TILE = 64;              // envs per workgroup
 constexpr int NCOL = TILE / 32;       // 32-column MFMA tiles per row tile
-constexpr int WGS_PER_CU = 4;
+constexpr int NWAVE = 8;
+constexpr int NTHR = 64 * NWAVE;
 constexpr int HID = 256;
 constexpr int NAG = 8;
 constexpr int KS2 = HID / 2;   // k-steps of 2 for a 256-wide contraction
@@ -131,19 +135,19 @@ __device__ __forceinline__ void hidden256(const float* __restrict__ W, const flo
     const float* B1 = W1 + 256 * DPAD;           // [256]
     const float* W2 = B1 + 256;                  // packed [8][32][64][4]
     const float* B2 = W2 + 256 * 256;            // [256]
-    f32x16 acc[2][NCOL];
-    zero_acc<2>(acc);
-    mfma_rows<2, DPAD / 2>(W1, 2 * wave, s_x, lane, acc);
-    store_rows<2>(acc, 64 * wave, B1, s_h, lane);
+    f32x16 acc[1][NCOL];
+    zero_acc<1>(acc);
+    mfma_rows<1, DPAD / 2>(W1, wave, s_x, lane, acc);
+    store_rows<1>(acc, 32 * wave, B1, s_h, lane);
     __syncthreads();
-    zero_acc<2>(acc);
-    mfma_rows<2, 128>(W2, 2 * wave, s_h, lane, acc);
+    zero_acc<1>(acc);
+    mfma_rows<1, 128>(W2, wave, s_h, lane, acc);
     __syncthreads();                             // every wave has read h1
-    store_rows<2>(acc, 64 * wave, B2, s_h, lane);
+    store_rows<1>(acc, 32 * wave, B2, s_h, lane);
     __syncthreads();
 }
 
-__global__ void __launch_bounds__(256, WGS_PER_CU) k_policy(const float* __restrict__ feats, const int8_t* __restrict__ masks,
+__global__ void __launch_bounds__(NTHR, 4) k_policy(const float* __restrict__ feats, const int8_t* __restrict__ masks,
                                                    int n, const float* __restrict__ actor_w,
                                                    const float* __restrict__ critic_w, const uint64_t* __restrict__ seedp,
                                                    uint32_t gid0, uint32_t step, int deterministic, uint8_t* __restrict__ actions,
@@ -161,7 +165,7 @@ __global__ void __launch_bounds__(256, WGS_PER_CU) k_policy(const float* __restr
     const int din = critic ? 38 : c_obs_dim[role];
     const int off = critic ? 0 : c_obs_off[role];
     const int dpad = critic ? FJSP_POLICY_CRITIC_DPAD : FJSP_POLICY_ACTOR_DPAD;
-    for (int i = tid; i < dpad * TILE; i += 256) {
+    for (int i = tid; i < dpad * TILE; i += NTHR) {
         const int k = i / TILE, c = i % TILE;
         s_x[i] = (k < din && e0 + c < n) ? feats[(size_t)(off + k) * n + e0 + c] : 0.0f;
     }
@@ -173,10 +177,12 @@ __global__ void __launch_bounds__(256, WGS_PER_CU) k_policy(const float* __restr
         const float* W4 = B3 + 128;                        // [128]
         const float* B4 = W4 + 128;                        // [1]
         f32x16 acc[1][NCOL];
-        zero_acc<1>(acc);
-        mfma_rows<1, 128>(W3, wave, s_h, lane, acc);
+        if (wave < 4) {                                    // 128 rows = 4 row tiles
+            zero_acc<1>(acc);
+            mfma_rows<1, 128>(W3, wave, s_h, lane, acc);
+        }
         __syncthreads();
-        store_rows<1>(acc, 32 * wave, B3, s_h, lane);      // h3 [128][64]
+        if (wave < 4) store_rows<1>(acc, 32 * wave, B3, s_h, lane);   // h3 [128][TILE]
         __syncthreads();
         if (tid < TILE && e0 + tid < n) {
             float v = B4[0];
@@ -187,20 +193,16 @@ __global__ void __launch_bounds__(256, WGS_PER_CU) k_policy(const float* __restr
     }
     const float* W = actor_w + (size_t)role * FJSP_POLICY_ACTOR_FLOATS;
     hidden256<FJSP_POLICY_ACTOR_DPAD>(W, s_x, s_h, wave, lane);
-    // layer 3: logits [8][64]; thread -> (action pair, env); weights wave-uniform
+    // layer 3: logits [8][TILE]; wave -> action row, lane -> env; weights wave-uniform
     const float* W3 = W + 256 * FJSP_POLICY_ACTOR_DPAD + 256 + 256 * 256 + 256;   // [8][256]
     const float* B3 = W3 + 8 * HID;                                                // [8]
     float* s_logit = s_x;
-    if (lane < TILE) {
-        const int c = lane, r0 = 2 * wave;
-        float l0 = B3[r0], l1 = B3[r0 + 1];
-        for (int k = 0; k < HID; k++) {
-            const float h = s_h[k * TILE + c];
-            l0 = fmaf(W3[r0 * HID + k], h, l0);
-            l1 = fmaf(W3[(r0 + 1) * HID + k], h, l1);
-        }
-        s_logit[r0 * TILE + c] = l0;
-        s_logit[(r0 + 1) * TILE + c] = l1;
+    static_assert(NWAVE == 8 && TILE == 64, "one logit row per wave, one env per lane");
+    {
+        const int c = lane, r = wave;
+        float l = B3[r];
+        for (int k = 0; k < HID; k++) l = fmaf(W3[r * HID + k], s_h[k * TILE + c], l);
+        s_logit[r * TILE + c] = l;
     }
     __syncthreads();
     if (tid < TILE && e0 + tid < n) {
@@ -208,31 +210,39 @@ __global__ void __launch_bounds__(256, WGS_PER_CU) k_policy(const float* __restr
         const int na = c_nact[role], mo = c_mask_off[role];
         float p[8], m[8];
         float mx = -INFINITY;
-        for (int j = 0; j < na; j++) mx = fmaxf(mx, s_logit[j * TILE + c]);
+        // fixed 8-trip loops guarded by na: fully unrolled, the arrays stay in registers
+#pragma unroll
+        for (int j = 0; j < 8; j++) if (j < na) mx = fmaxf(mx, s_logit[j * TILE + c]);
         float s = 0.0f;
-        for (int j = 0; j < na; j++) { p[j] = expf(s_logit[j * TILE + c] - mx); s += p[j]; }
+#pragma unroll
+        for (int j = 0; j < 8; j++) { p[j] = j < na ? expf(s_logit[j * TILE + c] - mx) : 0.0f; s += p[j]; }
         float s2 = 0.0f, ms = 0.0f;
-        for (int j = 0; j < na; j++) {
-            m[j] = (float)masks[(size_t)(mo + j) * n + e];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            m[j] = j < na ? (float)masks[(size_t)(mo + j) * n + e] : 0.0f;
             p[j] = (p[j] / s) * m[j];
             s2 += p[j];
             ms += m[j];
         }
-        for (int j = 0; j < na; j++) p[j] = s2 > 0.0f ? p[j] / s2 : m[j] / ms;
+#pragma unroll
+        for (int j = 0; j < 8; j++) p[j] = s2 > 0.0f ? p[j] / s2 : m[j] / ms;
         int act = 0;
         if (deterministic) {
             float best = p[0];
-            for (int j = 1; j < na; j++) if (p[j] > best) { best = p[j]; act = j; }
+#pragma unroll
+            for (int j = 1; j < 8; j++) if (j < na && p[j] > best) { best = p[j]; act = j; }
         } else {
             const uint64_t seed = *seedp;
             // keyed by the env's GLOBAL id: shards of a multi-GPU job draw independent streams
             const uint64_t h = fmix64(seed ^ fmix64(((uint64_t)(gid0 + (uint32_t)e) << 32) | step) ^
                                       (uint64_t)(role + 1) * 0x9E3779B97F4A7C15ull);
             const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
-            float cdf[8], tot = 0.0f;
-            for (int j = 0; j < na; j++) { tot += p[j]; cdf[j] = tot; }
+            float tot = 0.0f, cdf[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) { tot += j < na ? p[j] : 0.0f; cdf[j] = tot; }
             const float x = (1.0f - u) * tot;
-            for (int j = 0; j < na; j++) act += cdf[j] < x;
+#pragma unroll
+            for (int j = 0; j < 8; j++) act += (j < na && cdf[j] < x) ? 1 : 0;
             if (act >= na) act = na - 1;
         }
         actions[(size_t)role * n + e] = (uint8_t)act;
@@ -592,7 +602,7 @@ extern "C" int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t 
     if (!feats || !masks || !actor_w || !critic_w || !seed || !actions || !values)
         return fjsp_internal_fail("fjsp_a2c_policy: null buffer");
     dim3 grid((n + TILE - 1) / TILE, NAG + 1);
-    hipLaunchKernelGGL(k_policy, grid, dim3(256), 0, (hipStream_t)stream, feats, masks, n, actor_w, critic_w, seed, env_gid0,
+    hipLaunchKernelGGL(k_policy, grid, dim3(NTHR), 0, (hipStream_t)stream, feats, masks, n, actor_w, critic_w, seed, env_gid0,
                        step, deterministic, actions, values, probs);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
