@@ -510,9 +510,9 @@ __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t
     uint8_t order[NA];
 #pragma unroll
     for (int i = 0; i < NA; i++) order[i] = (uint8_t)(order_packed >> (8 * i));
-                     // slots: 0 entry -> LUT -> state + action loads landed, 1 action phase, 2 run,
-                     FJSP_DIAG(
-                     // 3 rewards, 4 observe, 5 term / trunc / status, 6 auto-reset + next obs, 7 state store drained
+    // stamp slots: 0 entry -> LUT -> state + action loads landed, 1 action phase, 2 run,
+    // 3 rewards, 4 observe, 5 term / trunc / status, 6 auto-reset + next obs, 7 state store drained
+    FJSP_DIAG(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (int i = 0; i < 8; i++) E.st_acc[i] = 0;
     E.st_t0 = __builtin_amdgcn_s_memtime();
