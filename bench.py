@@ -42,7 +42,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="bench steps: default 20 rollout batches (step) / 4 A2C batches (a2c)")
-    ap.add_argument("--warmup", type=int, default=None, help="default 5 rollout batches (step) / 1 A2C batch (a2c)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 5 rollout batches (step) / 3 A2C batches (a2c)")
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--batch-steps", type=int, default=256,
                     help="env-steps of every env per bench step (one rollout batch, train.py:59)")
@@ -67,7 +67,7 @@ def parse():
     if a.steps is None:
         a.steps = 20 if a.workload == "step" else 4
     if a.warmup is None:
-        a.warmup = 5 if a.workload == "step" else 1
+        a.warmup = 5 if a.workload == "step" else 3
     return a
 
 
@@ -356,9 +356,11 @@ def main():
     if world == 1 and not args.no_a2c:
         try:
             aenv = vec_env.FJSPVecEnv(N, device=dev)
-            # two warm-up batches: the first collect / update carry one-time costs (graph
-            # capture, allocator growth, library kernel selection: ~0.3 s / ~0.9 s)
-            a2c = a2c_throughput(aenv, N, 1, 3, 2, args.batch_size, 25, dedup=not args.no_dedup)
+            # four warm-up batches: the first collect / update carry one-time costs (graph
+            # capture, allocator growth, library kernel selection: ~0.3 s / ~0.9 s), and the
+            # grouped update's tensor sizes change with every batch's distinct-input counts, so
+            # the caching allocator needs a few batches to hold blocks for all of them
+            a2c = a2c_throughput(aenv, N, 1, 6, 4, args.batch_size, 25, dedup=not args.no_dedup)
             del aenv
             aenv = vec_env.FJSPVecEnv(N, device=dev)
             a2c["dense_update"] = a2c_throughput(aenv, N, 1, 3, 2, args.batch_size, 25, dedup=False)

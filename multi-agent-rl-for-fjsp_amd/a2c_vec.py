@@ -224,24 +224,25 @@ class ActorStack(nn.Module):
         computed and never gathered).  cols(agents, idx [k, u]) -> [k, 13, u] may stand in for x
         (the inputs of just the representatives)."""
         U = g.U
+        umax = g.first.shape[1]
         big = max(range(NA), key=lambda a: U[a])
         rest = [a for a in range(NA) if a != big]
         u2 = max(U[a] for a in rest)
+        ub = U[big]
         ridx = torch.tensor(rest, device=g.first.device)
         fr = g.first[ridx, :u2]
         if cols is None:
             xr = torch.gather(x[ridx], 2, fr[:, None, :].expand(NA - 1, x.shape[1], u2))
-            xb = x[big][:, g.first[big, :U[big]]]
+            xb = x[big][:, g.first[big, :ub]]
         else:
             xr = cols(ridx, fr)
-            xb = cols(torch.tensor([big], device=ridx.device), g.first[big:big + 1, :U[big]])[0]
+            xb = cols(torch.tensor([big], device=ridx.device), g.first[big:big + 1, :ub])[0]
         h = torch.relu(torch.baddbmm(self.b1[ridx], self.W1[ridx], xr))
         h = torch.relu(torch.baddbmm(self.b2[ridx], self.W2[ridx], h))
         pr = torch.softmax(torch.baddbmm(self.b3[ridx], self.W3[ridx], h) + self.logit_pad[ridx], dim=1)
         pb = self.agent_probs(big, xb)
-        umax = g.first.shape[1]
         out = [None] * NA
-        out[big] = torch.nn.functional.pad(pb, (0, umax - U[big]))
+        out[big] = torch.nn.functional.pad(pb, (0, umax - ub))
         for i, a in enumerate(rest):
             out[a] = torch.nn.functional.pad(pr[i], (0, umax - u2))
         return torch.stack(out)
@@ -490,12 +491,16 @@ class _GatherRuns(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, g):
         ctx.g = g
-        R, C, _ = y.shape
+        R, C, U = y.shape
+        ctx.U = U
         return torch.gather(y, 2, g.inv[:, None, :].expand(R, C, g.inv.shape[1]))
 
     @staticmethod
     def backward(ctx, gy):
-        return _run_sums(ctx.g, gy), None
+        gs = _run_sums(ctx.g, gy)                     # [R, C, Umax]: padding groups sum to 0
+        if gs.shape[2] >= ctx.U:
+            return gs[..., :ctx.U], None
+        return torch.nn.functional.pad(gs, (0, ctx.U - gs.shape[2])), None
 
 
 def _run_sums(g, gy):
@@ -616,6 +621,13 @@ class A2CLosses:
             c = gt[:, idx.reshape(-1)].view(GLOBAL_DIM, k, u)
             c = torch.cat([c, c.new_zeros(1, k, u)])
             return c[gidx[agents], torch.arange(k, device=idx.device)[:, None], :]
+        # the critic first: its GEMMs keep the GPU busy while the host issues the actors' many
+        # small launches (after the grouping's host synchronisations the queue is empty)
+        if gc is not None:
+            vu = mlp_forward(critic.net, gt[:, gc.first[0]].t()).reshape(1, 1, -1)
+            v = gc.gather(vu).reshape(-1)                            # [S]
+        else:
+            v = mlp_forward(critic.net, gt.t()).reshape(-1)
         adv_n = (adv - adv_mean[:, None]) / (adv_std[:, None] + 1e-8) if count > 1 else adv
         if ga is not None and feats.is_cuda:
             # the loss head and its gradient in one kernel (fjsp_a2c_actor_head)
@@ -631,11 +643,6 @@ class A2CLosses:
             pm = masked_probs(probs, agent_masks(masks, midx))
             logp = categorical_log_prob(pm, actions)                 # [8, S]
             actor_losses = -(adv_n * logp).sum(dim=1) / count - entropy_coef * ent.sum(dim=1) / count
-        if gc is not None:
-            vu = mlp_forward(critic.net, gt[:, gc.first[0]].t()).reshape(1, 1, -1)
-            v = gc.gather(vu).reshape(-1)                            # [S]
-        else:
-            v = mlp_forward(critic.net, gt.t()).reshape(-1)
         critic_loss = ((v[None, :] - returns) ** 2).sum() / (NA * count)
         return actor_losses, critic_loss
 

@@ -95,3 +95,15 @@ for _ in range(3):
 med = {k: round(float(np.median(v)), 3) for k, v in st.items()}
 med["total"] = round(sum(med.values()), 3)
 print(json.dumps({"N": N, "samples": T * N, "groups_actors": U[0], "groups_critic": U[1], "stage_ms": med}))
+
+# the same update unsynchronised (VecMultiAgentA2C.update), with and without the GAE pass
+tt = {"update_given_adv": [], "update_with_gae": [], "gae_only": []}
+for _ in range(3):
+    for key, fn in (("update_given_adv", lambda: L.update(ret, adv)), ("update_with_gae", lambda: L.update()),
+                    ("gae_only", lambda: L.advantages())):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        tt[key].append((time.perf_counter() - t0) * 1e3)
+print(json.dumps({k: round(float(np.median(v)), 3) for k, v in tt.items()}))
