@@ -162,6 +162,31 @@ __global__ void __launch_bounds__(NTHR, 4) k_policy(const float* __restrict__ fe
     const int role = blockIdx.y == 0 ? NAG : (int)blockIdx.y - 1;
     const int e0 = blockIdx.x * TILE;
     const bool critic = role == NAG;
+    if (!critic) {
+        // a tile in which the agent has exactly one valid action in every env: the draw (and
+        // argmax) returns that action whatever the network says, and the masked probabilities
+        // are exactly one-hot (p / p, or the uniform fallback over one action) -- skip the MLP.
+        // The station agents are forced in 96-100 % of an A2C collect's samples and whole
+        // tiles in 38-100 % (scripts/diag_forced_actions.py)
+        const int na = c_nact[role], mo = c_mask_off[role];
+        int forced = 1, only = 0;
+        if (tid < TILE && e0 + tid < n) {
+            int cnt = 0;
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                if (j < na && masks[(size_t)(mo + j) * n + e0 + tid] != 0) { cnt++; only = j; }
+            forced = cnt == 1;
+        }
+        if (__syncthreads_and(forced)) {
+            if (tid < TILE && e0 + tid < n) {
+                const int e = e0 + tid;
+                actions[(size_t)role * n + e] = (uint8_t)only;
+                if (probs_out)
+                    for (int j = 0; j < 8; j++) probs_out[((size_t)role * 8 + j) * n + e] = j == only ? 1.0f : 0.0f;
+            }
+            return;
+        }
+    }
     const int din = critic ? 38 : c_obs_dim[role];
     const int off = critic ? 0 : c_obs_off[role];
     const int dpad = critic ? FJSP_POLICY_CRITIC_DPAD : FJSP_POLICY_ACTOR_DPAD;

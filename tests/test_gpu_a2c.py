@@ -301,3 +301,48 @@ def test_critic_splitk_relu_backward(M, rows):
     assert float((y1 - y2).detach().abs().max()) <= 1e-5 * float(y2.detach().abs().max())
     for a, p in zip(g1, critic.parameters()):
         assert float((a - p.grad).abs().max()) <= 1e-4 * float(p.grad.abs().max())
+
+
+def test_fused_policy_forced_tiles(M):
+    """A 64-env tile in which an agent has exactly one valid action in every env skips the
+    actor's MLP in fjsp_a2c_policy: its actions are that action (greedy and sampled) and its
+    probabilities exactly one-hot, as the full path gives (masked renormalisation p / p); a tile
+    with one unforced env, and the critic's values, match the PyTorch policy path."""
+    A, V = M["A"], M["V"]
+    n = 1000
+    env = V.FJSPVecEnv(n)
+    learner = A.VecMultiAgentA2C(env, batch_size=8, seed=5, use_graph=False)
+    learner.reset(seeds=torch.arange(n), num_orders=25)
+    g = torch.Generator(device=env.device).manual_seed(11)
+    feats = torch.randint(0, 6, (A.GLOBAL_DIM, n), device=env.device, generator=g).float()
+    masks = (torch.rand(29, n, device=env.device, generator=g) < 0.6).to(torch.int8)
+    for a in range(8):
+        o = A.MASK_OFFS[a]
+        masks[o, :] = 1                                             # at least one valid action
+    forced_envs = torch.arange(0, 128, device=env.device)
+    for a in range(2, 8):                                            # the station agents
+        o = A.MASK_OFFS[a]
+        j = (forced_envs + a) % 3
+        masks[o:o + 3, :128] = 0
+        masks[o + j, forced_envs] = 1
+        masks[o:o + 3, 100] = 1                                      # tile 1 has one unforced env
+    act_t, pm_t, v_t = learner.policy(feats, masks, deterministic=True)
+    act = torch.zeros(8, n, dtype=torch.uint8, device=env.device)
+    val = torch.zeros(n, dtype=torch.float32, device=env.device)
+    probs = torch.zeros(8, 8, n, dtype=torch.float32, device=env.device)
+    learner.policy_fused(feats, masks, 0, True, act, val, probs)
+    torch.cuda.synchronize()
+    assert torch.allclose(probs, pm_t, atol=1e-5) and torch.allclose(val, v_t, atol=1e-5, rtol=1e-5)
+    for a in range(2, 8):
+        j = ((forced_envs + a) % 3)[:64]
+        onehot = torch.nn.functional.one_hot(j, 8).float().t()
+        assert torch.equal(probs[a][:, :64], onehot), a                # skipped tile: exact one-hot
+        assert torch.equal(act[a, :64].long(), j), a
+        assert torch.equal(probs[a][:, 64:128][:, torch.arange(64) != 36],
+                           torch.nn.functional.one_hot(((forced_envs + a) % 3)[64:], 8).float().t()
+                           [:, torch.arange(64) != 36]), a             # full path, forced envs
+    for r in range(5):
+        learner._rng.fill_(77 + r)
+        learner.policy_fused(feats, masks, r, False, act, val)
+        for a in range(2, 8):
+            assert torch.equal(act[a, :64].long(), ((forced_envs + a) % 3)[:64]), a
