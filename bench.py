@@ -63,6 +63,12 @@ def parse():
     ap.add_argument("--no-scale", action="store_true", help="skip the 16x-envs leg of the step workload")
     ap.add_argument("--no-dedup", action="store_true",
                     help="A2C update over every sample (no grouping of repeated inputs)")
+    ap.add_argument("--exchange", choices=["allreduce", "gather"], default="gather",
+                    help="a2c workload with several ranks: the once-per-batch exchange (gather = the north "
+                         "star's experience gather of the transition slabs into rank 0, a2c.py:324-336; "
+                         "allreduce = one flat gradient all_reduce)")
+    ap.add_argument("--init", choices=["random", "trained"], default="random",
+                    help="a2c workload: random-init networks or the reference's trained checkpoint")
     a = ap.parse_args()
     if a.steps is None:
         a.steps = 20 if a.workload == "step" else 4
@@ -142,12 +148,21 @@ def load_pmc(workload):
         return None
 
 
-def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=None, group=None, dedup=True):
+TRAINED_NPZ = os.path.join(REPO, "tests", "golden", "trained_policy.npz")
+
+
+def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=None, group=None, dedup=True,
+                   exchange="allreduce", init="random", stats=True):
     """Batched A2C training loop (a2c_vec.VecMultiAgentA2C): env-steps/s over whole batches
     (collect batch_size vector steps with the policy + GAE + one update).  dedup: the update
-    runs each network once per distinct input (A2CLosses; the same gradient)."""
+    runs each network once per distinct input (A2CLosses; the same gradient).  exchange: the
+    multi-rank exchange ("allreduce" of gradients or "gather" of the transition slabs into rank
+    0, a2c.py:324-336).  init "trained": start from the reference's trained checkpoint
+    (checkpoints/model.pt, carried as tests/golden/trained_policy.npz)."""
     A = importlib.import_module("multi-agent-rl-for-fjsp_amd.a2c_vec")
-    learner = A.VecMultiAgentA2C(env, batch_size=batch_size, seed=0, group=group, dedup=dedup)
+    learner = A.VecMultiAgentA2C(env, batch_size=batch_size, seed=0, group=group, dedup=dedup, exchange=exchange)
+    if init == "trained":
+        learner.load_state_dicts(A.load_npz_weights(TRAINED_NPZ))
     base = env.env_id_base
     learner.reset(seeds=torch.arange(base, base + N), num_orders=num_orders)
 
@@ -178,14 +193,34 @@ def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, tc = float(t[0]), float(t[1])
     steps = batches * batch_size * N * world
-    return {"value": steps / elapsed, "unit": "env-steps/s", "n_gpus": world, "batches": batches,
-            "batch_size": batch_size, "envs_per_gpu": N, "ms_per_batch": elapsed * 1e3 / batches,
-            "collect_ms_per_batch": tc * 1e3 / batches,
-            "update_ms_per_batch": (elapsed - tc) * 1e3 / batches,
-            "critic_loss_last": learner.critic_loss_history[-1], "update_dedup": bool(dedup),
-            "note": "predict (stacked-actor batched GEMMs + masked sampling) -> fjsp_step writing a2c "
-                    "features in HBM -> fp64 GAE kernel -> full-batch update (8 actors + critic, Adam); "
-                    "reference a2c.py loop: ~130 env-steps/s on one CPU core (SURVEY.md)"}
+    out = {"value": steps / elapsed, "unit": "env-steps/s", "n_gpus": world, "batches": batches,
+           "batch_size": batch_size, "envs_per_gpu": N, "ms_per_batch": elapsed * 1e3 / batches,
+           "collect_ms_per_batch": tc * 1e3 / batches,
+           "update_ms_per_batch": (elapsed - tc) * 1e3 / batches,
+           "critic_loss_last": learner.critic_loss_history[-1], "update_dedup": bool(dedup),
+           "exchange": exchange if world > 1 else None, "init": init,
+           "note": "fused MFMA predict (k_policy) -> fjsp_step writing a2c features in HBM (hipGraph-captured "
+                   "collect) -> fp64 GAE kernel -> grouped full-batch update (8 actors + critic, Adam); "
+                   "reference a2c.py loop: ~130 env-steps/s on one CPU core (SURVEY.md)"}
+    if world > 1:
+        out["exchange_bytes_per_rank_per_batch"] = (learner.exchange_bytes_per_batch() if exchange == "gather"
+                                                   else 4 * sum(p.numel() for p in list(learner.actors.parameters())
+                                                                + list(learner.critic.parameters())))
+    if stats:
+        # after the timed region: one more batch with synchronised stage timers (the update's
+        # stages on this rank: gather / learn (GAE + update; the learner rank's serial work under
+        # "gather") / broadcast), then what that batch looked like to the update
+        learner.exchange_timing = {}
+        learner.collect()
+        learner.update()
+        learner.roll_over()
+        torch.cuda.synchronize()
+        out["update_stage_ms"] = dict(learner.exchange_timing)
+        learner.exchange_timing = None
+        learner.collect()
+        torch.cuda.synchronize()
+        out["batch_stats"] = learner.batch_stats()
+    return out
 
 
 def main():
@@ -216,16 +251,22 @@ def main():
     env = vec_env.FJSPVecEnv(N, device=dev, env_id_base=base)
     if args.workload == "a2c":
         res = a2c_throughput(env, N, world, args.steps, args.warmup, args.batch_size, 25, dist,
-                             dist.group.WORLD if dist else None, dedup=not args.no_dedup)
+                             dist.group.WORLD if dist else None, dedup=not args.no_dedup, exchange=args.exchange,
+                             init=args.init)
         if rank == 0:
             out = {"metric": "env-steps/sec of the A2C training loop (BASELINE configs 4/5)",
                    "value": res["value"], "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
                    "warmup": args.warmup, "ms_per_step": res["ms_per_batch"], "higher_is_better": True,
                    "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (networks) + int32/f64 (env)",
-                   "data": "synthetic: envs seeded by global id, random-init networks (torch.manual_seed(0))",
+                   "data": "synthetic: envs seeded by global id, " + (
+                       "random-init networks (torch.manual_seed(0))" if args.init == "random" else
+                       "networks from the reference's trained checkpoints/model.pt"),
                    "config": {"workload": f"a2c_{N}envs", "envs_per_gpu": N, "global_envs": N * world,
-                              "batch_size": args.batch_size, "num_orders": 25,
-                              "parallelism": f"env-shard x{world}, one flat gradient all_reduce per batch"},
+                              "batch_size": args.batch_size, "num_orders": 25, "init": args.init,
+                              "exchange": args.exchange if world > 1 else None,
+                              "parallelism": f"env-shard x{world}" + (
+                                  "" if world == 1 else ", experience gather into rank 0 + parameter broadcast"
+                                  if args.exchange == "gather" else ", one flat gradient all_reduce per batch")},
                    "a2c": res}
             print(json.dumps(out), flush=True)
         if dist:
@@ -363,7 +404,13 @@ def main():
             a2c = a2c_throughput(aenv, N, 1, 6, 4, args.batch_size, 25, dedup=not args.no_dedup)
             del aenv
             aenv = vec_env.FJSPVecEnv(N, device=dev)
-            a2c["dense_update"] = a2c_throughput(aenv, N, 1, 3, 2, args.batch_size, 25, dedup=False)
+            # the same loop from the reference's trained checkpoint: the states a trained policy
+            # visits set the grouped update's distinct-input counts and the forced-tile share
+            a2c["trained_init"] = a2c_throughput(aenv, N, 1, 4, 4, args.batch_size, 25, dedup=not args.no_dedup,
+                                                 init="trained")
+            del aenv
+            aenv = vec_env.FJSPVecEnv(N, device=dev)
+            a2c["dense_update"] = a2c_throughput(aenv, N, 1, 3, 2, args.batch_size, 25, dedup=False, stats=False)
             del aenv
         except Exception as e:   # the headline metric does not depend on this leg
             a2c = {"error": f"{type(e).__name__}: {e}"}

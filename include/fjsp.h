@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define FJSP_ABI_VERSION 3
+#define FJSP_ABI_VERSION 4
 
 #define FJSP_NUM_AGENTS 8      /* pickup, agv, small, big, pkg_blue_1, pkg_blue_2, pkg_red, pkg_green */
 #define FJSP_OBS_I32 20        /* pickup 7 + agv 13 (position = 2) int32 observation fields */
@@ -53,6 +53,8 @@ extern "C" {
 #define FJSP_STATUS_PROD_LOST    0x10u  /* no packaging station with capacity: products lost (reference behaviour) */
 #define FJSP_STATUS_OVERWRITE    0x20u  /* machine START overwrote an unsignalled tray (reference behaviour) */
 #define FJSP_STATUS_SLOT_OVERFLOW 0x40u /* more trays in one episode than the slot arena holds (not emulated) */
+#define FJSP_STATUS_SPIN_TIMEOUT 0x80u  /* a wave of a multi-wave step kernel gave up waiting for another wave's
+                                           hand-off (bounded wait; results of that workgroup are invalid) */
 
 /* action_mode for fjsp_step_many */
 #define FJSP_ACTIONS_UNMASKED 0  /* uniform over the full action space (action_space.sample()) */
@@ -168,7 +170,11 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
  * workgroup, lanes >= ag_envs idle; auto = 64 for launches of fewer than 64 steps, else the
  * fewest that give every workgroup a CU of its own; identical results); "env_id_base" (0..2^32-1, default 0: the handle is the shard [value, value + N) of a
  * larger job — every env's MT19937 stream is re-seeded to np.random.seed(value + e), exactly
- * the stream env value + e of one big handle starts from; stream-ordered). */
+ * the stream env value + e of one big handle starts from; stream-ordered); "spin_cap"
+ * (1..2^31, default 2^22: sleep iterations a wave of a multi-wave step kernel waits for another
+ * wave's hand-off before it gives up and flags FJSP_STATUS_SPIN_TIMEOUT / fjsp_faults);
+ * "xcd_map" (0/1, default 1: k_step_ag hands 8 consecutive env blocks to workgroups on one XCD
+ * so that its L2 merges their partial output lines; identical results). */
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value);
 int fjsp_num_envs(const fjsp_handle* h);
 /* Bytes of device state per env (HBM footprint of the SoA state). */
@@ -299,6 +305,13 @@ int fjsp_last_kernel_ms(fjsp_handle* h, float* ms);
 /* Name of the kernel variant the last fjsp_step / fjsp_step_many launched ("" before any):
  * e.g. "k_step_pipe<lds>" (rocprof shows it as k_step_pipe). */
 const char* fjsp_last_kernel(const fjsp_handle* h);
+/* Fault word of the handle's multi-wave step kernels (k_step_ag, k_step_pipe with hand-offs):
+ * bit 0 = some workgroup's wave gave up a bounded wait for another wave's hand-off (its envs
+ * also carry FJSP_STATUS_SPIN_TIMEOUT).  Never set by a correct kernel: the bound (option
+ * "spin_cap", sleep iterations, default 2^22 ~ 0.1 s) exists so that a hand-off bug ends the
+ * launch with a flag instead of hanging the device.  Synchronises; clear != 0 zeroes the word.
+ * (No reference counterpart: the reference's agents run sequentially in one Python thread.) */
+int fjsp_faults(fjsp_handle* h, uint32_t* out, int32_t clear);
 
 #ifdef __cplusplus
 }

@@ -65,10 +65,10 @@ EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_c
            "fjsp_read_env", "fjsp_sync", "fjsp_last_kernel_ms", "fjsp_pack_a2c", "fjsp_a2c_layout",
            "fjsp_snapshot_bytes", "fjsp_snapshot", "fjsp_restore", "fjsp_last_kernel", "fjsp_a2c_policy",
            "fjsp_a2c_group_keys", "fjsp_a2c_group_verify", "fjsp_a2c_actor_head",
-           "fjsp_a2c_relu_bias_grad", "fjsp_a2c_value_head_grad"]
+           "fjsp_a2c_relu_bias_grad", "fjsp_a2c_value_head_grad", "fjsp_faults"]
 POLICY_ACTOR_FLOATS = 256 * 16 + 256 + 256 * 256 + 256 + 8 * 256 + 16
 POLICY_CRITIC_FLOATS = 256 * 40 + 256 + 256 * 256 + 256 + 128 * 256 + 128 + 128 + 16
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lib = None
 
@@ -133,6 +133,7 @@ def lib():
         "fjsp_snapshot": (I, [P, P]),
         "fjsp_restore": (I, [P, P]),
         "fjsp_last_kernel": (ctypes.c_char_p, [P]),
+        "fjsp_faults": (I, [P, ctypes.POINTER(U32), I]),
         "fjsp_a2c_policy": (I, [P, P, I, P, P, P, U32, U32, I, P, P, P, P]),
         "fjsp_a2c_group_keys": (I, [P, I, I, P, P]),
         "fjsp_a2c_group_verify": (I, [P, I, I, P, P, P, P]),

@@ -350,17 +350,33 @@ def _fmix64(z):
     return z ^ shr(z, 31)
 
 
+def _s64(c):
+    c &= _M64
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+_ROLE_KEYS = {}
+
+
+def role_keys(device):
+    """The per-agent keys (a + 1) * golden-ratio of the policy draw, int64 [8] on `device`
+    (built once per device: a host-to-device copy must not happen inside a graph capture)."""
+    device = torch.device(device)
+    if device not in _ROLE_KEYS:
+        _ROLE_KEYS[device] = torch.tensor([_s64((a + 1) * 0x9E3779B97F4A7C15) for a in range(NA)],
+                                          dtype=torch.int64, device=device)
+    return _ROLE_KEYS[device]
+
+
 def counter_uniform(seed, gid, step, device):
     """U [8, 1, B] in [0, 1) keyed by (seed, global env id, step, agent) exactly as the fused
     policy kernel's draw (fjsp_policy.hip): shards of a multi-GPU job draw independent streams
-    and the eager and fused paths see the same uniforms."""
-    def s64(c):
-        c &= _M64
-        return c - (1 << 64) if c >= (1 << 63) else c
+    and the eager and fused paths see the same uniforms.  seed: a Python int or an int64
+    tensor of one element on `device` (read at run time: a captured graph re-keys with it)."""
     g = torch.as_tensor(gid, device=device).to(torch.int64) & 0xFFFFFFFF
     inner = _fmix64((g << 32) | (int(step) & 0xFFFFFFFF))
-    role = torch.tensor([s64((a + 1) * 0x9E3779B97F4A7C15) for a in range(NA)], dtype=torch.int64, device=device)
-    h = _fmix64((s64(seed) ^ inner)[None, :] ^ role[:, None])            # [8, B]
+    s = seed.reshape(1) if torch.is_tensor(seed) else _s64(seed)
+    h = _fmix64((s ^ inner)[None, :] ^ role_keys(device)[:, None])         # [8, B]
     return ((h >> 40) & 0xFFFFFF).to(torch.float32).mul_(1.0 / 16777216.0).unsqueeze(1)
 
 
@@ -706,11 +722,19 @@ def init_networks(seed=None, hidden=256, device="cpu"):
     return actors.to(device), critic.to(device)
 
 
+def flat_grads(actors, critic):
+    """Every parameter's gradient (8 stacked actors, then the critic) as one flat f32 tensor."""
+    return torch.cat([p.grad.reshape(-1) if p.grad is not None else torch.zeros_like(p).reshape(-1)
+                      for p in list(actors.parameters()) + list(critic.parameters())])
+
+
 def update_step(actors, critic, optim_actor, optim_critic, feats, masks, actions, ret, adv, gidx, midx,
-                entropy_coef, max_grad_norm, group=None, dedup=False):
+                entropy_coef, max_grad_norm, group=None, dedup=False, grad_probe=None):
     """One _update (a2c.py:647-703) on a [T, ., N] batch (this rank's shard of it).
 
     feats f32 [T, 38, N], masks int8 [T, 29, N], actions u8 [T, 8, N], ret / adv f64 [T, 8, N].
+    grad_probe(flat f32 grads): called with the reduced gradients before clipping and Adam
+    (tests compare them across exchanges).
     Returns (actor losses per agent, critic loss) as Python floats (the loss histories)."""
     from . import distributed as D
     T, _, N = feats.shape
@@ -725,6 +749,8 @@ def update_step(actors, critic, optim_actor, optim_critic, feats, masks, actions
                                                   entropy_coef, mean, std, count, dedup)
     (actor_losses.sum() + critic_loss).backward()
     D.allreduce_grads(list(actors.parameters()) + list(critic.parameters()), group)
+    if grad_probe is not None:
+        grad_probe(flat_grads(actors, critic).detach().clone())
     clip_per_agent_(actors, max_grad_norm)
     torch.nn.utils.clip_grad_norm_(critic.parameters(), max_grad_norm)
     optim_actor.step()
@@ -794,13 +820,19 @@ class VecMultiAgentA2C:
         # sampling key: (seed, batch) -> counter hash per (global env id, step, agent); the same
         # on every rank, the env's global id separates the shards
         self._rng_host = int.from_bytes(__import__("os").urandom(7), "little") if seed is None else int(seed)
+        # the draw key lives on the device for both policy paths: a captured collect reads it
+        # at replay time, so every replay draws new actions
+        self._rng = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._rng.fill_(self._rng_host)
+        role_keys(self.device)
         if self.fused_policy:
             self._pw_actor, self._pw_critic = pack_policy_weights(self.actors, self.critic)
-            self._rng = torch.zeros(1, dtype=torch.int64, device=self.device)
-            self._rng.fill_(self._rng_host)
         self._graph = None
         self._graph_det = None
         self._eager_batches = 0
+        self.gae_fn = batch_advantages     # finish_trajectory over a batch (tests may inject a CPU stand-in)
+        self.grad_probe = None             # grad_probe(flat reduced grads) before clip / Adam (tests)
+        self.exchange_timing = None        # dict of synchronised stage times (ms) when not None (bench)
 
     # ------------------------------------------------------------ rollout storage
     def _alloc(self):
@@ -877,7 +909,7 @@ class VecMultiAgentA2C:
         else:
             g0 = self.env.env_id_base if gid0 is None else gid0
             gid = torch.arange(g0, g0 + pm.shape[2], device=pm.device)
-            act = sample_categorical(pm, counter_uniform(self._rng_host, gid, t, pm.device))
+            act = sample_categorical(pm, counter_uniform(self._rng, gid, t, pm.device))
         v = self.critic(feats.t()).view(-1)
         return act, pm, v
 
@@ -896,8 +928,7 @@ class VecMultiAgentA2C:
         bootstrap value, ~40 launches per step) is captured once into a hipGraph and replayed:
         the buffers and parameters are static, Adam updates the weights in place."""
         self._rng_host += 1
-        if self.fused_policy:
-            self._rng.fill_(self._rng_host)   # re-keys the sampling of the (captured) batch
+        self._rng.fill_(self._rng_host)       # re-keys the sampling of the (captured) batch
         if action_fn is None and self.use_graph:
             if self._graph is not None and self._graph_det == deterministic:
                 self._graph.replay()
@@ -945,25 +976,42 @@ class VecMultiAgentA2C:
         """finish_trajectory over the batch (transition_memory.py:45-105) with the fp64 GAE
         kernel: an episode end bootstraps 0 (a2c.py:357), the batch end V(s_T) (a2c.py:321-332)."""
         b = self._bufs
-        return batch_advantages(b["rewards"], b["values"], b["term"] | b["trunc"], self.gamma, self.lamb,
-                                self.use_gae)
+        return self.gae_fn(b["rewards"], b["values"], b["term"] | b["trunc"], self.gamma, self.lamb, self.use_gae)
+
+    def _mark(self, name, t0):
+        """Stage timing for the bench (synchronising): adds ms since t0 to exchange_timing."""
+        import time
+        if self.exchange_timing is None:
+            return t0
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        t = time.perf_counter()
+        self.exchange_timing[name] = self.exchange_timing.get(name, 0.0) + (t - t0) * 1e3
+        return t
 
     def update(self, ret=None, adv=None):
         """_update (a2c.py:647-703) over the batch's T x N transitions (x world with a group).
 
         exchange "allreduce": GAE on this rank, one flat gradient all_reduce (distributed.py);
         exchange "gather": the transitions go to the learner rank (ret / adv are recomputed
-        there over the gathered batch), the new parameters come back in one broadcast."""
-        if self.exchange == "gather" and self.group is not None:
+        there over the gathered batch), the new parameters come back in one broadcast.  Only
+        the learner rank steps Adam under "gather": its moments live there (the other ranks'
+        optimisers stay at their initial state), so a run that later switches to "allreduce"
+        or resumes an optimiser must take it from the learner rank."""
+        from . import distributed as D
+        if self.exchange == "gather" and D.active(self.group):
             al, cl = self._update_gathered()
         else:
+            import time
+            t0 = time.perf_counter()
             if ret is None:
                 ret, adv = self.advantages()
             b = self._bufs
             T = self.batch_size
             al, cl = update_step(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
                                  b["masks"][:T], b["actions"], ret, adv, self.gidx, self.midx, self.entropy_coef,
-                                 self.max_grad_norm, self.group, self.dedup)
+                                 self.max_grad_norm, self.group, self.dedup, self.grad_probe)
+            self._mark("learn", t0)
         for a, x in zip(AGENTS, al):
             self.actor_loss_history[a].append(x)
         self.critic_loss_history.append(cl)
@@ -974,26 +1022,53 @@ class VecMultiAgentA2C:
         """Experience gather into the learner (rank 0 of the group): the reference's
         transition_memory filled with every rank's transitions, finish_trajectory + _update
         over the whole batch (a2c.py:324-336), then the parameters broadcast back."""
+        import time
         from . import distributed as D
         import torch.distributed as dist
+        t0 = time.perf_counter()
         b = self._bufs
         T = self.batch_size
         slab = {"feats": b["feats"][:T], "masks": b["masks"][:T], "actions": b["actions"], "rewards": b["rewards"],
                 "values": b["values"], "done": b["term"] | b["trunc"]}
         full = D.gather_slabs(slab, dst=0, group=self.group)
+        t0 = self._mark("gather", t0)
         params = list(self.actors.parameters()) + list(self.critic.parameters())
         stats = torch.zeros(NA + 1, dtype=torch.float32, device=self.device)
         if dist.get_rank(self.group) == 0:
             cat = lambda x: x.movedim(0, -2).reshape(*x.shape[1:-1], -1)   # [W, ..., n] -> [..., W*n]  # noqa: E731
             g = {k: cat(v) for k, v in full.items()}
-            ret, adv = batch_advantages(g["rewards"], g["values"], g["done"], self.gamma, self.lamb, self.use_gae)
+            del full
+            ret, adv = self.gae_fn(g["rewards"], g["values"], g["done"], self.gamma, self.lamb, self.use_gae)
             al, cl = update_step(self.actors, self.critic, self.optim_actor, self.optim_critic, g["feats"], g["masks"],
                                  g["actions"], ret, adv, self.gidx, self.midx, self.entropy_coef,
-                                 self.max_grad_norm, D.LOCAL, self.dedup)
+                                 self.max_grad_norm, D.LOCAL, self.dedup, self.grad_probe)
             stats.copy_(torch.tensor(al + [cl], dtype=torch.float32))
+        t0 = self._mark("learn", t0)
         D.broadcast_flat(params + [stats], src=0, group=self.group)
+        self._mark("broadcast", t0)
         v = stats.cpu().tolist()
         return v[:NA], v[NA]
+
+    @torch.no_grad()
+    def batch_stats(self):
+        """What the last collected batch looked like to the update (diagnostics, synchronising):
+        per agent the share of samples whose action was forced (one valid action) and of 64-env
+        tiles where every env was forced (k_policy skips those tiles' MLPs), and the number of
+        distinct inputs each network saw (the grouped update runs each network once per
+        distinct input)."""
+        b = self._bufs
+        T = self.batch_size
+        m = b["masks"][:T].int()
+        forced, tiles = {}, {}
+        for i, a in enumerate(AGENTS):
+            o, k = MASK_OFFS[i], N_ACTIONS[i]
+            f = m[:, o:o + k, :].sum(1) == 1                     # [T, N]
+            forced[a] = float(f.float().mean())
+            n64 = (self.N // 64) * 64
+            tiles[a] = float(f[:, :n64].reshape(T, -1, 64).all(-1).float().mean()) if n64 else 0.0
+        g = RowGroups(group_keys(b["feats"][:T].contiguous()))
+        return {"samples": T * self.N, "forced_share": forced, "forced_tile_share": tiles,
+                "distinct_inputs": dict(zip(AGENTS, g.U[:NA])), "distinct_global_states": g.U[NA]}
 
     def exchange_bytes_per_batch(self):
         """Bytes one rank sends per batch with exchange="gather" (the transition slab)."""
@@ -1098,9 +1173,8 @@ class VecMultiAgentA2C:
 
     def load_model(self, path):
         """Loads a reference checkpoint (or one written by save_model) without executing
-        anything from the file (weights_only=True)."""
-        ck = torch.load(path, map_location="cpu", weights_only=True)
-        self.load_state_dicts(ck)
+        anything from the file (load_checkpoint: weights_only=True)."""
+        self.load_state_dicts(load_checkpoint(path))
 
     def load_state_dicts(self, ck):
         """load_model (a2c.py:756-775): only the agents the checkpoint holds are overwritten
@@ -1118,6 +1192,49 @@ class VecMultiAgentA2C:
             self.critic.load_state_dict(ck["critic_net"])
         if getattr(self, "fused_policy", False):
             self.repack()
+
+
+def _checkpoint_globals():
+    """The only non-tensor globals a reference checkpoint pickles: a2c.py:80 stores
+    act_space.n — a numpy int64 scalar under gymnasium — into act_dims, which save_model
+    (a2c.py:745-753) pickles as numpy.core.multiarray.scalar(dtype('int64'), bytes).  Under
+    numpy 2 the function lives in numpy._core, so it is allowlisted under its pickled name."""
+    import numpy as np
+    try:
+        from numpy._core import multiarray as ma
+    except ImportError:                                   # numpy 1.x
+        from numpy.core import multiarray as ma
+    return [(ma.scalar, "numpy.core.multiarray.scalar"), np.dtype, type(np.dtype(np.int64))]
+
+
+def load_checkpoint(path):
+    """A reference (a2c.py:733-775) or save_model checkpoint as a dict, read with
+    torch.load(weights_only=True) and an allowlist of exactly the numpy scalar global and the
+    int64 dtype class (nothing from the file is executed; there is no weights_only=False
+    fallback).  obs_dims / act_dims / global_obs_dim come back as Python ints."""
+    with torch.serialization.safe_globals(_checkpoint_globals()):
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+    for k in ("obs_dims", "act_dims"):
+        if isinstance(ck.get(k), dict):
+            ck[k] = {a: int(v) for a, v in ck[k].items()}
+    if "global_obs_dim" in ck:
+        ck["global_obs_dim"] = int(ck["global_obs_dim"])
+    return ck
+
+
+def load_npz_weights(path):
+    """A checkpoint's tensors stored as an .npz (w_actor.<agent>.<param>, w_critic.<param>;
+    tests/golden/gen_trained_golden.py) -> the load_state_dicts dict."""
+    import numpy as np
+    z = np.load(path)
+    ck = {"actor_nets": {}, "critic_net": {}}
+    for k in z.files:
+        if k.startswith("w_actor."):
+            _, a, p = k.split(".", 2)
+            ck["actor_nets"].setdefault(a, {})[p] = torch.from_numpy(z[k].copy())
+        elif k.startswith("w_critic."):
+            ck["critic_net"][k[len("w_critic."):]] = torch.from_numpy(z[k].copy())
+    return ck
 
 
 def num_params(model):

@@ -98,6 +98,8 @@ struct Cfg {
     int step_size, max_steps, tray_cap, mask_tray_cap, storage_cap, pool0, pkg_cap;
     int ptk_small, ptk_big, ptk_pack;   // processing times in steps
     const double* lut;                  // RLUT_SIZE doubles
+    uint32_t spin_cap;                  // bound on a hand-off wait (sleep iterations; the multi-wave kernels)
+    int xcd_map;                        // env blocks of consecutive workgroups on one XCD (xcd_block)
 };
 
 // Host side: fill the reward table from RewardModel weights (w in fjsp_reward_weights order).
@@ -134,7 +136,8 @@ inline void build_reward_lut(const double* w, int step_size, double* lut) {
 
 // status bits (include/fjsp.h)
 constexpr uint32_t ST_DIVERGED = 0x1u, ST_OBS_OVERFLOW = 0x2u, ST_PKG_WAIT = 0x4u, ST_TRAY_LOST = 0x8u,
-                   ST_PROD_LOST = 0x10u, ST_OVERWRITE = 0x20u, ST_SLOT_OVERFLOW = 0x40u;
+                   ST_PROD_LOST = 0x10u, ST_OVERWRITE = 0x20u, ST_SLOT_OVERFLOW = 0x40u,
+                   ST_SPIN_TIMEOUT = 0x80u;   // a wave's wait for another wave's hand-off hit its bound
 
 // Number of packed u32 words of Env in the SoA state buffer.
 constexpr int NWORDS = 40;   // rows of the HBM state buffer (30 used)

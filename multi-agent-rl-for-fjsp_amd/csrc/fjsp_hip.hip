@@ -45,8 +45,41 @@ struct DevState {
     uint16_t* scstep;
     uint32_t* mt;       // [2][n][624] MT rows (live one selected by W3 bit 31)
     uint32_t* nxt;      // [MAX_ORDERS][n] pre-drawn next order tables (W[PGW])
+    uint32_t* fault;    // the handle's fault word (fjsp_faults): bit 0 = a bounded hand-off wait gave up
     int n;
 };
+
+// Bounded wait of one wave for a hand-off flag another wave of its workgroup releases.  The
+// waves of a workgroup are co-resident, so a correct kernel always gets there; the bound turns a
+// hand-off bug into a flagged launch (ST_SPIN_TIMEOUT on the workgroup's envs, the handle's fault
+// word) instead of a device hang.  Once one wait of the workgroup gave up (*abort) the others
+// stop waiting too, after at most 256 more sleeps each.
+__device__ __forceinline__ void spin_until(uint32_t* flag, uint32_t v, uint32_t* abort, uint32_t cap) {
+    for (uint32_t it = 0; __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v; it++) {
+        if ((it & 255u) == 255u || it >= cap) {
+            if (it >= cap || __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                break;
+            }
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// Env block of workgroup b of nb.  Workgroups are dealt to the 8 XCDs round-robin (b -> XCD
+// b % 8, MI355X_MICROARCH.md), and each XCD has its own L2.  With few envs per workgroup the
+// byte fields of 8 consecutive env blocks share one 128-B line of an output row: mapping them to
+// one XCD lets its L2 merge the partial lines into whole ones before they go to HBM (dealt
+// round-robin, 8 L2s each wrote back a 16-B piece of every line).  Only the speed depends on the
+// dispatch order; any b -> block bijection gives the same results.
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+    return (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);
+}
+
+// The workgroup's give-up flag into the handle's fault word (one lane; a vector atomic).
+__device__ __forceinline__ void report_abort(const DevState& S, uint32_t abort) {
+    if (abort) __hip_atomic_fetch_or(S.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // ---------------------------------------------------------------- load / store of Env
 // The register state is the HBM row layout itself (fjsp_env.h, struct Env): 30 coalesced words.
@@ -943,7 +976,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
     __shared__ uint32_t s_post[PG ? NPOST : 1][BLOCK];
     __shared__ uint32_t s_pick[PG ? 6 : 1][BLOCK];   // next_order, W4, W5, W7, result, flags
     __shared__ uint32_t s_agv[PG ? 12 : 1][BLOCK];   // W5, W6, W7..W12, result, flags, move, pend
-    __shared__ uint32_t s_postflag, s_pickflag;
+    __shared__ uint32_t s_postflag, s_pickflag, s_abort;
     __shared__ uint16_t s_code[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint8_t s_next[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint16_t s_cstep[LDS ? MAX_SLOTS * BLOCK : 1];
@@ -964,6 +997,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
         s_act[0][0][lane] = pack_actions(act, 0);
         s_act[0][1][lane] = pack_actions(act, 4);
     }
+    if (threadIdx.x == 0) s_abort = 0;
     if constexpr (PG) {   // step-0 mailboxes
         if (threadIdx.x == 0) { s_postflag = 0; s_pickflag = 0; }
         if (wave == 0 && valid) {
@@ -1096,8 +1130,11 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
                     S.scstep[(size_t)q * S.n + e] = T.scstep[q * BLOCK];
                 }
             }
+            // every wait happened before the last barrier: a give-up is visible here
+            if (s_abort) E.w[2] |= ST_SPIN_TIMEOUT | ST_DIVERGED;
             env_store(E, S.words, S.n, e);
         }
+        if (lane == 0) report_abort(S, s_abort);
         FJSP_DIAG(
         if (lane == 0)
             for (int i = 0; i < 8; i++) atomicAdd((unsigned long long*)&g_stamps[i], (unsigned long long)E.st_acc[i]);
@@ -1149,8 +1186,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
             }
             if constexpr (PG) {   // step k + 1's pickup, once the sim wave has posted its state
                 if (part == 0 && pre && k + 1 < K) {
-                    while (__hip_atomic_load(&s_postflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (uint32_t)(k + 1))
-                        __builtin_amdgcn_s_sleep(1);
+                    spin_until(&s_postflag, (uint32_t)(k + 1), &s_abort, C.spin_cap);
                     if (valid) {
                         Env Ep;
 #pragma unroll
@@ -1186,13 +1222,13 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
                     const int truncated = E.step() >= C.max_steps;
                     if (out.term) st32(out.term, t * n + ue, (uint8_t)all_done);
                     if (out.trunc) st32(out.trunc, t * n + ue, (uint8_t)truncated);
-                    if (out.status) st32(out.status, t * n + ue, E.status());
+                    if (out.status)
+                        st32(out.status, t * n + ue, E.status() | (s_abort ? ST_SPIN_TIMEOUT | ST_DIVERGED : 0u));
                 }
             }
             if constexpr (PG) {   // step k + 1's AGV, on the posted state and that step's pickup
                 if (part == 1 && pre && k + 1 < K) {
-                    while (__hip_atomic_load(&s_pickflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (uint32_t)(k + 1))
-                        __builtin_amdgcn_s_sleep(1);
+                    spin_until(&s_pickflag, (uint32_t)(k + 1), &s_abort, C.spin_cap);
                     if (valid) {
                         Env Ea;
 #pragma unroll
@@ -1370,9 +1406,6 @@ __device__ __forceinline__ void ag_emit(int part, const uint32_t* v, uint32_t t,
     }
 }
 
-__device__ __forceinline__ void ag_spin(uint32_t* flag, uint32_t v) {
-    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
-}
 
 // EPW: envs per workgroup (64, 32 or 16; lanes >= EPW idle): fewer envs per CU spread N envs
 // over more CUs (every workgroup keeps its 150 KB of LDS, so one workgroup per CU).
@@ -1402,6 +1435,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     __shared__ uint32_t s_kpost[3][BLOCK];      // K after step k: W1 (completed orders) by step parity, final status
     __shared__ uint32_t s_flag1;   // AM posted step k's pickup / AGV words and machine lists (k + 1)
     __shared__ uint32_t s_uflag;   // E3 posted step k+1's pickup (k + 1)
+    __shared__ uint32_t s_abort;   // a bounded hand-off wait of this workgroup gave up (spin_until)
     __shared__ uint4 s_pk[BLOCK];   // E3: W0, W4, W5, W7 after step k+1's pickup
     __shared__ uint2 s_pkr[BLOCK];  // E3: its result word, status bits
     __shared__ double s_lut[RLUT_SIZE];
@@ -1409,7 +1443,8 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     C.lut = s_lut;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / BLOCK);
     const int lane = threadIdx.x % BLOCK;
-    const int e = blockIdx.x * EPW + lane;
+    const int blk = C.xcd_map ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const int e = blk * EPW + lane;
     const bool valid = lane < EPW && e < S.n;
     const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
     const Tables TL{s_orders + lane, s_code + lane, s_next + lane, s_cstep + lane, BLOCK};
@@ -1424,7 +1459,10 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             s_act[j][1][lane] = pack_actions(act, 4);
         }
     }
-    if (threadIdx.x == 0) { s_flag1 = 0; s_uflag = 0; }
+    if (threadIdx.x == 0) { s_flag1 = 0; s_uflag = 0; s_abort = 0; }
+    auto ag_spin = [&](uint32_t* flag, uint32_t v) __attribute__((always_inline)) {
+        spin_until(flag, v, &s_abort, C.spin_cap);
+    };
     if (valid) {
         // the env's order table, used slot prefix and pre-drawn table live in LDS for the launch
         // (copied in before the first barrier: K's first completions read them), copied by all
@@ -1608,6 +1646,8 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             s_act[0][0][lane] = (uint32_t)E.norders();   // for the copy-out by all waves below
             s_act[0][1][lane] = (uint32_t)E.slot_next();
             E.w[2] |= s_kpost[2][lane];
+            // every wait happened before the last barrier: a give-up is visible here
+            if (s_abort) E.w[2] |= ST_SPIN_TIMEOUT | ST_DIVERGED;
 #pragma unroll
             for (int i = 0; i < NSTATE; i++)
                 if (!((K_WORDS >> i) & 1u)) S.words[i * n + e] = E.w[i];
@@ -1761,7 +1801,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             AG_BARRIER();
         }
     } else if (wave == AG_PD) {
-        predraw_wave<CR, PB, true, true>(S, K, lane, e, valid, (size_t)blockIdx.x * EPW, s_mb, s_cp, s_nxt);
+        predraw_wave<CR, PB, true, true>(S, K, lane, e, valid, (size_t)blk * EPW, s_mb, s_cp, s_nxt);
     } else {
         // E0: step k+2's actions, rewards, the pickup's masks; E1: int32 and float32 fields; E2:
         // int8 fields, term, trunc, status, the AGV's pickup / drop masks; E3: step k+1's pickup
@@ -1808,6 +1848,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 const uint32_t t = (uint32_t)(k - 1);
                 uint32_t v[SNAP_N];
                 snap_get(snap[(k - 1) & 1], lane, v);
+                if (part == 2 && s_abort) v[SA_ST] |= ST_SPIN_TIMEOUT | ST_DIVERGED;
                 FJSP_DIAG(
                 __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the snapshot arrived
                 )
@@ -1820,6 +1861,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         }
     }
     __syncthreads();
+    if (threadIdx.x == 0) report_abort(S, s_abort);
     FJSP_DIAG(
     const uint64_t t_out = __builtin_amdgcn_s_memtime();
     )
@@ -1920,6 +1962,7 @@ struct fjsp_handle {
     int ag_epw;      // k_step_ag envs per workgroup: 64 / 32 / 16, 0 = auto (FJSP_AG_EPW / "ag_envs")
     const char* last_kernel;   // name of the last step kernel launched (fjsp_last_kernel)
     uint32_t env_id_base;      // global id of env 0 (fjsp_set_option "env_id_base")
+    uint32_t* fault_dev;       // fjsp_faults word
 };
 
 static thread_local std::string g_err;
@@ -2053,6 +2096,8 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     h->dcfg.ptk_small = c.pt_small / c.step_size;
     h->dcfg.ptk_big = c.pt_big / c.step_size;
     h->dcfg.ptk_pack = c.pt_packaging / c.step_size;
+    h->dcfg.spin_cap = 1u << 22;   // ~0.1 s of sleeps: far beyond any legitimate hand-off wait
+    h->dcfg.xcd_map = 1;
 
     const size_t n = (size_t)num_envs;
     const size_t b_words = (size_t)NWORDS * n * 4, b_orders = (size_t)MAX_ORDERS * n * 4;
@@ -2081,6 +2126,11 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     if (e != hipSuccess) { h->ev1 = nullptr; return bail("hipEventCreate", e); }
     e = hipMalloc(&h->lut_dev, sizeof(double) * RLUT_SIZE);
     if (e != hipSuccess) { h->lut_dev = nullptr; return bail("hipMalloc(reward table)", e); }
+    e = hipMalloc(&h->fault_dev, sizeof(uint32_t));
+    if (e != hipSuccess) { h->fault_dev = nullptr; return bail("hipMalloc(fault word)", e); }
+    e = hipMemsetAsync(h->fault_dev, 0, sizeof(uint32_t), h->stream);
+    if (e != hipSuccess) return bail("fault word", e);
+    h->S.fault = h->fault_dev;
     h->dcfg.lut = h->lut_dev;
     {
         fjsp_reward_weights w;
@@ -2106,6 +2156,7 @@ int fjsp_destroy(fjsp_handle* h) {
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->lut_dev) (void)hipFree(h->lut_dev);
+    if (h->fault_dev) (void)hipFree(h->fault_dev);
     if (h->base) (void)hipFree(h->base);
     delete h;
     return 0;
@@ -2124,6 +2175,12 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
         return 0;
     }
     if (!strcmp(name, "timing")) { h->timing = value != 0; if (!h->timing) h->timed = 0; return 0; }
+    if (!strcmp(name, "xcd_map")) { h->dcfg.xcd_map = value != 0; return 0; }
+    if (!strcmp(name, "spin_cap")) {
+        if (value < 1 || value > 0x7FFFFFFFll) return fail("spin_cap must be in 1..2^31-1");
+        h->dcfg.spin_cap = (uint32_t)value;
+        return 0;
+    }
     if (!strcmp(name, "env_id_base")) {
         // the handle is shard [value, value + n) of a larger job: env e's default stream becomes
         // np.random.seed(value + e), as for env value + e of one big handle (stream-ordered)
@@ -2366,6 +2423,15 @@ int fjsp_restore(fjsp_handle* h, const void* src) {
 
 const char* fjsp_last_kernel(const fjsp_handle* h) {
     return (h && h->last_kernel) ? h->last_kernel : "";
+}
+
+int fjsp_faults(fjsp_handle* h, uint32_t* out, int32_t clear) {
+    if (!h || !out) return fail("null argument");
+    DeviceGuard g(h->device);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipMemcpy(out, h->fault_dev, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (clear) HIPCHK(hipMemset(h->fault_dev, 0, sizeof(uint32_t)));
+    return 0;
 }
 
 int fjsp_sync(fjsp_handle* h) {

@@ -257,6 +257,13 @@ class FJSPVecEnv:
     def sync(self):
         nat.check(nat.lib().fjsp_sync(self._h))
 
+    def faults(self, clear=False):
+        """The handle's fault word (fjsp_faults; synchronises): bit 0 = a bounded hand-off wait
+        of a multi-wave step kernel gave up (its envs carry FJSP_STATUS_SPIN_TIMEOUT)."""
+        w = ctypes.c_uint32()
+        nat.check(nat.lib().fjsp_faults(self._h, ctypes.byref(w), int(bool(clear))))
+        return w.value
+
 
 def gae(rewards, values, done, boot, gamma, lamb, out_ret=None, out_adv=None):
     """Returns + GAE (transition_memory.py:83-105) on device tensors.

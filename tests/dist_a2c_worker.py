@@ -1,14 +1,18 @@
-"""One rank of the 2-rank A2C rehearsal of BASELINE config 5 (run by tests/test_gpu_shards.py
-under torch.distributed.run; gloo between the ranks, every rank on cuda:0).
+"""One rank of the multi-rank A2C rehearsals of BASELINE config 5 (run by tests/test_gpu_shards.py
+and tests/test_gpu_config5.py under torch.distributed.run; gloo between the ranks, every rank on
+cuda:0).
 
 Rank r steps the env shard [r*n, (r+1)*n) (FJSPVecEnv(env_id_base=r*n)) and trains with the
-exchange given on the command line; it saves its first batch's rollout buffers, the loss
-histories and the final parameters for the parent test to compare with one learner over 2n
-envs."""
+exchange given on the command line.  It saves, for the parent test to compare with one learner
+over world*n envs: its first batch's rollout buffers (or, with --shard-digest, a sha256 of each
+buffer's bytes), the reduced gradients of the first update before clipping / Adam (the learner
+rank only under exchange="gather"), the loss histories and the parameters."""
 import argparse
+import hashlib
 import importlib
 import os
 import sys
+import time
 
 import torch
 import torch.distributed as dist
@@ -16,9 +20,15 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
+BUFS = ("feats", "masks", "actions", "values", "rewards", "term", "trunc")
+
 
 def flat(L):
     return torch.cat([p.detach().reshape(-1).cpu() for p in list(L.actors.parameters()) + list(L.critic.parameters())])
+
+
+def digest(t):
+    return hashlib.sha256(t.contiguous().cpu().numpy().tobytes()).hexdigest()
 
 
 def main():
@@ -28,6 +38,7 @@ def main():
     ap.add_argument("--shard-batches", type=int, default=2)
     ap.add_argument("--shard-exchange", default="allreduce")
     ap.add_argument("--shard-out", required=True)
+    ap.add_argument("--shard-digest", action="store_true", help="save sha256 digests of the first batch, not tensors")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
@@ -37,21 +48,31 @@ def main():
     env = V.FJSPVecEnv(a.shard_envs, device="cuda:0", env_id_base=rank * a.shard_envs)
     L = A.VecMultiAgentA2C(env, batch_size=a.shard_batch, seed=5, group=dist.group.WORLD, exchange=a.shard_exchange)
     L.reset(num_orders=25)
+    grads = []
     first = None
+    t_update = []
     for i in range(a.shard_batches):
         L.collect()
         if i == 0:
             b = L._bufs
-            first = {k: b[k].cpu().clone() for k in ("feats", "masks", "actions", "values", "rewards", "term",
-                                                       "trunc")}
+            if a.shard_digest:
+                first = {k: digest(b[k]) for k in BUFS}
+            else:
+                first = {k: b[k].cpu().clone() for k in BUFS}
+            L.grad_probe = lambda g: grads.append(g.cpu())
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         L.update()
+        torch.cuda.synchronize()
+        t_update.append(time.perf_counter() - t0)
+        L.grad_probe = None
         L.roll_over()
         if i == 0:
             params1 = flat(L)
     torch.cuda.synchronize()
     torch.save({"first": first, "params1": params1, "params": flat(L), "critic": L.critic_loss_history,
-                "actor": [L.actor_loss_history[k] for k in A.AGENTS],
-                "exchange_bytes": L.exchange_bytes_per_batch()},
+                "actor": [L.actor_loss_history[k] for k in A.AGENTS], "grads1": grads[0] if grads else None,
+                "exchange_bytes": L.exchange_bytes_per_batch(), "t_update": t_update},
                os.path.join(a.shard_out, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()

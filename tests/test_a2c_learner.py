@@ -165,24 +165,84 @@ def test_checkpoint_format_roundtrip(tmp_path):
         assert torch.equal(v, _params(a2, c2)[k]), k
 
 
+def _bare_learner(seed=0):
+    actors, critic = A.init_networks(seed=seed)
+    learner = A.VecMultiAgentA2C.__new__(A.VecMultiAgentA2C)
+    learner.actors, learner.critic, learner.device = actors, critic, torch.device("cpu")
+    learner.gidx, learner.midx = A.gather_index("cpu"), A.mask_index("cpu")
+    return learner
+
+
 def test_reference_checkpoint_loads_if_present():
-    """The reference's own checkpoints/model.pt (weights_only loader; skipped when the
-    reference tree is absent, e.g. on the GPU box)."""
+    """The reference's own checkpoints/model.pt through load_model (torch.load(weights_only=
+    True) with the numpy scalar / int64 dtype allowlist; a2c.py:733-775): the reference tree is
+    absent on the GPU box, where the weights travel as tests/golden/trained_policy.npz."""
     import os
     path = "/root/reference/checkpoints/model.pt"
     if not os.path.exists(path):
-        pytest.skip("reference checkpoint not available")
-    try:
-        ck = torch.load(path, map_location="cpu", weights_only=True)
-    except Exception as e:   # the safe loader refused the file: do not fall back to pickle
-        pytest.skip(f"weights_only loader refused the reference checkpoint: {type(e).__name__}")
-    actors, critic = A.init_networks(seed=0)
-    learner = A.VecMultiAgentA2C.__new__(A.VecMultiAgentA2C)
-    learner.actors, learner.critic, learner.device = actors, critic, torch.device("cpu")
-    learner.load_state_dicts(ck)
+        pytest.skip("reference tree not present (GPU box): covered by the trained_policy.npz tests")
+    learner = _bare_learner()
+    learner.load_model(path)
+    ck = A.load_checkpoint(path)
+    assert ck["act_dims"] == dict(zip(spec.AGENTS, A.N_ACTIONS)) and ck["global_obs_dim"] == 38
+    assert all(type(v) is int for v in ck["act_dims"].values())
+    z = np.load(f"{P.GOLDEN}/trained_policy.npz")
     for i, a in enumerate(spec.AGENTS):
         for k, v in ck["actor_nets"][a].items():
-            assert torch.equal(actors.actor_state_dict(i)[k], v), (a, k)
+            assert torch.equal(learner.actors.actor_state_dict(i)[k], v), (a, k)
+            assert np.array_equal(z[f"w_actor.{a}.{k}"], v.numpy()), (a, k)
+    for k, v in ck["critic_net"].items():
+        assert torch.equal(learner.critic.state_dict()[k], v), k
+        assert np.array_equal(z[f"w_critic.{k}"], v.numpy()), k
+
+
+def test_checkpoint_loader_refuses_other_globals(tmp_path):
+    """The allowlist is exactly the numpy scalar + int64 dtype: any other pickled global (here
+    a numpy array reconstruction) is refused, never unpickled."""
+    path = tmp_path / "bad.pt"
+    torch.save({"actor_nets": {}, "x": np.arange(3)}, str(path))
+    with pytest.raises(Exception):
+        A.load_checkpoint(str(path))
+
+
+TRAINED = [0, 1, 2, 3, 4, 5, 6, 7]
+
+
+@pytest.fixture(scope="module")
+def trained():
+    return np.load(f"{P.GOLDEN}/trained_policy.npz")
+
+
+@pytest.mark.parametrize("seed", TRAINED)
+def test_trained_policy_greedy_matches_reference(trained, seed):
+    """The reference's trained weights (npz of checkpoints/model.pt) in the batched policy:
+    greedy actions equal the reference's predict(deterministic=True) at every state of its
+    test() rollout, values within 1e-5 relative (fp32, per-sample GEMV vs batched GEMM)."""
+    learner = _bare_learner()
+    learner.load_state_dicts(A.load_npz_weights(f"{P.GOLDEN}/trained_policy.npz"))
+    f = torch.from_numpy(trained[f"s{seed}_gstate"].T.copy())          # [38, T]
+    m = torch.from_numpy(trained[f"s{seed}_masks"].T.copy())
+    with torch.no_grad():
+        pm = A.masked_probs(learner.actors(A.actor_inputs(f, learner.gidx)), A.agent_masks(m, learner.midx))
+        v = learner.critic(f.t()).view(-1)
+    assert np.array_equal(torch.argmax(pm, dim=1).numpy().T, trained[f"s{seed}_actions"])
+    assert np.allclose(v.numpy(), trained[f"s{seed}_values"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("seed", [0, 4, 6])
+def test_trained_policy_rollout_replays_on_oracle(trained, seed):
+    """The reference's test() trajectory under the trained policy: its recorded greedy actions
+    replayed through the oracle give the recorded pre-step features, masks and rewards."""
+    idx = spec.a2c_feature_index()
+    num_orders, steps = int(trained[f"s{seed}_meta"][0]), int(trained[f"s{seed}_meta"][1])
+    env = O.OracleEnv()
+    r = env.reset(seed=seed, num_orders=num_orders)
+    for t in range(steps):
+        flat = np.concatenate([r["obs_i32"], r["obs_i8"], r["obs_f32"]]).astype(np.float32)
+        assert np.array_equal(flat[idx], trained[f"s{seed}_gstate"][t]), t
+        assert np.array_equal(r["masks"], trained[f"s{seed}_masks"][t]), t
+        r = env.step(trained[f"s{seed}_actions"][t])
+        assert r["rewards"].tobytes() == trained[f"s{seed}_rewards"][t].tobytes(), t
 
 
 def test_sampler_never_returns_invalid_actions():

@@ -134,6 +134,37 @@ def test_graph_replay_equals_eager(M):
         assert torch.equal(runs[0][i], runs[1][i])
 
 
+def test_eager_policy_graph_rekeys_each_batch(M):
+    """The PyTorch policy path (fused_policy=False) captured into the collect graph reads the
+    draw key from the device: every replay draws new actions, and each batch equals the eager
+    loop's (same weights: no update between the batches)."""
+    A, V = M["A"], M["V"]
+    n, T = 256, 16
+    runs = []
+    for use_graph in (False, True):
+        env = V.FJSPVecEnv(n)
+        L = A.VecMultiAgentA2C(env, batch_size=T, seed=8, use_graph=use_graph, fused_policy=False)
+        L.reset(seeds=torch.arange(n), num_orders=25)
+        acts = []
+        for _ in range(4):
+            L.collect()
+            acts.append(L._bufs["actions"].clone())
+            L.roll_over()
+        assert (L._graph is not None) == use_graph
+        runs.append(acts)
+    eager, graph = runs
+    for b in range(4):
+        assert torch.equal(eager[b], graph[b]), b
+    # replays of one captured graph draw new actions (a frozen key would repeat the AGV's
+    # choices wherever the observation repeats; here whole batches would coincide only then)
+    assert not torch.equal(graph[2], graph[3])
+    L._rng.fill_(12345)
+    a0 = L.policy(L._bufs["feats"][0], L._bufs["masks"][0], t=0)[0]
+    L._rng.fill_(12346)
+    a1 = L.policy(L._bufs["feats"][0], L._bufs["masks"][0], t=0)[0]
+    assert not torch.equal(a0, a1)                      # the device key reaches the eager draw
+
+
 def test_fused_policy_kernel_matches_torch_policy(M):
     """fjsp_a2c_policy (one MFMA kernel per step) == the PyTorch policy path: masked
     probabilities and values within 1e-5, greedy actions equal (up to near-ties), sampled

@@ -210,3 +210,38 @@ def test_agents_envs_per_workgroup(G, epw):
     for k in LEAN:
         assert P.bits_equal(runs[0][0][k], runs[1][0][k]), k
     _same_views(runs[0][1], runs[1][1])
+
+
+@pytest.mark.parametrize("agents", [1, 0])
+def test_bounded_handoff_waits(G, agents):
+    """The hand-off waits of the multi-wave kernels (k_step_ag's flag spins, k_step_pipe's
+    mailboxes) are bounded.  At the default bound a 4 096-env x 1 024-step bench launch never
+    gives up (fault word 0, no env carries FJSP_STATUS_SPIN_TIMEOUT).  At a bound of one sleep a
+    wait that finds the flag unset gives up: the launch still ends, and a workgroup that gave up
+    flags every env it holds (status bit 0x80 | DIVERGED, fault word bit 0) while workgroups that
+    did not are byte-identical to the unbounded run."""
+    env = _env(G, 4096, agents)
+    env.reset(num_orders=30)
+    st = G.to_np(env.rollout(1024, action_seed=3, policy="random"))["status"]
+    torch.cuda.synchronize()
+    assert env.last_kernel() == (AG if agents else "k_step_pipe<lds,2emit,predraw>")
+    assert env.faults() == 0 and not (st & 0x80).any()
+    n = 256
+    ref = _env(G, n, agents)
+    ref.reset(num_orders=30)
+    r0 = G.to_np(ref.rollout(64, action_seed=5, policy="random"))
+    tight = _env(G, n, agents)
+    G.native.check(G.native.lib().fjsp_set_option(tight.handle, b"spin_cap", 1))
+    tight.reset(num_orders=30)
+    r1 = G.to_np(tight.rollout(64, action_seed=5, policy="random"))
+    fault = tight.faults(clear=True)
+    flagged = (r1["status"][-1] & 0x80) != 0                      # [n]: the env's workgroup gave up
+    assert bool(fault & 1) == bool(flagged.any())
+    assert tight.faults() == 0                                    # cleared
+    ok = ~flagged
+    for k in LEAN:
+        if k == "status":
+            continue
+        assert np.array_equal(r1[k][:, ok], r0[k][:, ok]), k
+    if flagged.any():
+        assert ((r1["status"][-1][flagged] & 0x81) == 0x81).all()

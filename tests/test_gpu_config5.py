@@ -1,0 +1,106 @@
+"""BASELINE config 5 at its full size, rehearsed on one GPU: 32 768 envs = 8 shards x 4 096
+(global env ids rank * 4096 + e), A2C batch 256, both exchanges of a2c.py:324-336.
+
+* Stepping: 8 handles with env_id_base r * 4096 produce, over 256 steps with auto-resets, the
+  bytes of one 32 768-env handle (every lean output field), and sampled envs of shards 3 and 7
+  the bytes of the oracle at their global ids.
+* Training: 8 ranks (gloo between them, all on cuda:0, launched as fresh processes by
+  torch.distributed.run) each run VecMultiAgentA2C on its 4 096-env shard for one 256-step
+  batch with exchange "allreduce" (gradients summed over ranks) or "gather" (every rank's
+  transition slab into the learner rank).  Their first batch is byte-identical to the
+  corresponding slice of one 32 768-env learner's (sha256 per buffer), and the reduced
+  gradients before clipping / Adam equal that learner's to 1e-5 relative per parameter
+  tensor."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from oracle import oracle as O  # noqa: E402
+from tests import parity_util as P  # noqa: E402
+from tests.test_gpu_shards import _single_learner, run_ranks  # noqa: E402
+
+WORLD, NS, T = 8, 4096, 256
+LEAN = ("obs_i32", "obs_i8", "obs_f32", "masks", "rewards", "term", "trunc", "status")
+
+
+@pytest.fixture(scope="module")
+def G():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    from tests import gpu_util
+    return gpu_util
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("policy", ["random", "masked"])
+def test_eight_shards_equal_one_32768_handle_and_oracle(G, policy):
+    V = G.vec_env
+    big = V.FJSPVecEnv(WORLD * NS)
+    big.reset(num_orders=30)
+    rb = big.rollout(T, action_seed=77, policy=policy)
+    for r in range(WORLD):
+        sh = V.FJSPVecEnv(NS, env_id_base=r * NS)
+        sh.reset(num_orders=30)
+        rs = sh.rollout(T, action_seed=77, policy=policy)
+        for k in LEAN:
+            a, b = getattr(rb, k), getattr(rs, k)
+            assert torch.equal(a[..., r * NS:(r + 1) * NS], b), (policy, r, k)
+        if r in (3, 7):
+            # sampled envs of the shard == the oracle at their global ids (seeded np.random.seed(gid))
+            got = G.to_np(rs)                  # [T, N, F] / [T, N]
+            for e0 in (0, 2045, NS - 8):
+                rec, _, _ = O.rollout(8, T, gid0=r * NS + e0, num_orders=30, action_seed=77,
+                                      policy={"random": 0, "masked": 1}[policy])
+                for k in LEAN:
+                    if k == "status":
+                        continue
+                    sl = got[k][:, e0:e0 + 8]
+                    assert np.array_equal(sl, rec[k].reshape(sl.shape)), (policy, r, e0, k)
+            del got
+        del sh, rs
+        torch.cuda.empty_cache()
+    ends = int((rb.term | rb.trunc).sum())
+    assert ends >= WORLD * NS                  # every env crossed at least one auto-reset
+
+
+def _digest(t):
+    return hashlib.sha256(t.contiguous().cpu().numpy().tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def single(G):
+    """One learner over all 32 768 envs: first-batch buffers and first-update gradients."""
+    first, grads, L = _single_learner(WORLD * NS, T, 1)
+    digests = {k: [_digest(v[..., r * NS:(r + 1) * NS]) for r in range(WORLD)] for k, v in first.items()}
+    out = {"digests": digests, "grads": grads, "critic": L.critic_loss_history[0],
+           "actor": [h[0] for h in L.actor_loss_history.values()]}
+    del L, first
+    torch.cuda.empty_cache()
+    return out
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("exchange", ["allreduce", "gather"])
+def test_eight_rank_a2c_equals_one_32768_env_learner(G, single, tmp_path, exchange):
+    ranks = run_ranks(WORLD, NS, T, 1, exchange, tmp_path, digest=True, timeout=900)
+    for r, rk in enumerate(ranks):
+        for k, d in rk["first"].items():
+            assert d == single["digests"][k][r], (exchange, r, k)
+    errs = P.assert_grads_close(ranks[0]["grads1"], single["grads"])
+    print(exchange, "max relative gradient error per tensor:", max(e for _, e in errs))
+    if exchange == "allreduce":
+        for rk in ranks[1:]:
+            assert torch.equal(rk["grads1"], ranks[0]["grads1"])
+    else:
+        assert all(rk["grads1"] is None for rk in ranks[1:])
+        assert ranks[0]["exchange_bytes"] == T * NS * 258 + NS * 4
+    for rk in ranks[1:]:
+        assert torch.equal(rk["params"], ranks[0]["params"])
+    assert ranks[0]["critic"][0] == pytest.approx(single["critic"], rel=1e-5)
+    assert np.allclose([a[0] for a in ranks[0]["actor"]], single["actor"], rtol=1e-4, atol=1e-6)
