@@ -459,6 +459,11 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kernel_name, "avg_launch_ms": avg_launch_ms,
                          "algo_bytes_per_env_step": ALGO_BYTES_FUSED,
+                         # SURVEY.md 8(d) prices an env-step at 219 B, 8 of them the u8 actions
+                         # read from HBM; this kernel draws its actions on the device, so its
+                         # algorithmic bytes are the 211 B of outputs (the 219 B figures beside)
+                         "achieved_219B": achieved * ALGO_BYTES_STEP / ALGO_BYTES_FUSED,
+                         "frac_219B": achieved * ALGO_BYTES_STEP / ALGO_BYTES_FUSED / HBM_PEAK_GBS,
                          "env_steps_per_launch": N * steps_per_launch},
             "cpu_baseline": cpu,
             "chunk_200": chunk_200,
