@@ -171,10 +171,8 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
  * fewest that give every workgroup a CU of its own; identical results); "env_id_base" (0..2^32-1, default 0: the handle is the shard [value, value + N) of a
  * larger job — every env's MT19937 stream is re-seeded to np.random.seed(value + e), exactly
  * the stream env value + e of one big handle starts from; stream-ordered); "spin_cap"
- * (1..2^31, default 2^22: sleep iterations a wave of a multi-wave step kernel waits for another
- * wave's hand-off before it gives up and flags FJSP_STATUS_SPIN_TIMEOUT / fjsp_faults);
- * "xcd_map" (0/1, default 1: k_step_ag hands 8 consecutive env blocks to workgroups on one XCD
- * so that its L2 merges their partial output lines; identical results). */
+ * (256..2^31-1, default 2^22: sleep iterations, checked every 256 a wave of a multi-wave step kernel waits for another
+ * wave's hand-off before it gives up and flags FJSP_STATUS_SPIN_TIMEOUT / fjsp_faults). */
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value);
 int fjsp_num_envs(const fjsp_handle* h);
 /* Bytes of device state per env (HBM footprint of the SoA state). */
@@ -308,7 +306,8 @@ int fjsp_last_kernel_ms(fjsp_handle* h, float* ms);
 /* Name of the kernel variant the last fjsp_step / fjsp_step_many launched ("" before any):
  * e.g. "k_step_pipe<lds>" (rocprof shows it as k_step_pipe). */
 const char* fjsp_last_kernel(const fjsp_handle* h);
-/* Fault word of the handle's multi-wave step kernels (k_step_ag, k_step_pipe with hand-offs):
+/* Fault word of the handle's multi-wave step kernels (part of the handle's state: a snapshot /
+ * restore carries it) (k_step_ag, k_step_pipe with hand-offs):
  * bit 0 = some workgroup's wave gave up a bounded wait for another wave's hand-off (its envs
  * also carry FJSP_STATUS_SPIN_TIMEOUT).  Never set by a correct kernel: the bound (option
  * "spin_cap", sleep iterations, default 2^22 ~ 0.1 s) exists so that a hand-off bug ends the

@@ -98,8 +98,6 @@ struct Cfg {
     int step_size, max_steps, tray_cap, mask_tray_cap, storage_cap, pool0, pkg_cap;
     int ptk_small, ptk_big, ptk_pack;   // processing times in steps
     const double* lut;                  // RLUT_SIZE doubles
-    uint32_t spin_cap;                  // bound on a hand-off wait (sleep iterations; the multi-wave kernels)
-    int xcd_map;                        // env blocks of consecutive workgroups on one XCD (xcd_block)
 };
 
 // Host side: fill the reward table from RewardModel weights (w in fjsp_reward_weights order).

@@ -45,19 +45,32 @@ struct DevState {
     uint16_t* scstep;
     uint32_t* mt;       // [2][n][624] MT rows (live one selected by W3 bit 31)
     uint32_t* nxt;      // [MAX_ORDERS][n] pre-drawn next order tables (W[PGW])
-    uint32_t* fault;    // the handle's fault word (fjsp_faults): bit 0 = a bounded hand-off wait gave up
     int n;
 };
+// Handle words after the state rows ([NWORDS][n] u32 + AUX_WORDS): the fault word (fjsp_faults:
+// bit 0 = a bounded hand-off wait gave up) and the bound of those waits (option "spin_cap").
+// Not kernel arguments: a pointer or a field more in DevState / Cfg, live through the step loops,
+// pushed k_step_ag into SGPR spills (+6 % per step, measured).
+constexpr int AUX_WORDS = 4, AUX_FAULT = 0, AUX_SPIN_CAP = 1;
+__device__ __forceinline__ uint32_t* aux_words(const DevState& S) { return S.words + (size_t)NWORDS * S.n; }
 
 // Bounded wait of one wave for a hand-off flag another wave of its workgroup releases.  The
 // waves of a workgroup are co-resident, so a correct kernel always gets there; the bound turns a
 // hand-off bug into a flagged launch (ST_SPIN_TIMEOUT on the workgroup's envs, the handle's fault
 // word) instead of a device hang.  Once one wait of the workgroup gave up (*abort) the others
-// stop waiting too, after at most 256 more sleeps each.
-__device__ __forceinline__ void spin_until(uint32_t* flag, uint32_t v, uint32_t* abort, uint32_t cap) {
-    for (uint32_t it = 0; __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v; it++) {
-        if ((it & 255u) == 255u || it >= cap) {
-            if (it >= cap || __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+// stop waiting too, after at most 256 more sleeps each (so the bound is a multiple of 256
+// sleeps, at least 256).  abort and cap live in LDS and are read
+// only every 256 sleeps: nothing of the bound stays live in registers across the step loop (a
+// cap held in an SGPR through the loop pushed the multi-wave kernels into SGPR spills, +6 %).
+__device__ __forceinline__ void spin_until(uint32_t* flag, uint32_t v, uint32_t* abort, const uint32_t* cap) {
+#ifdef FJSP_X_UNBOUNDED   // diagnostic build only: the r02 unbounded wait
+    (void)abort; (void)cap;
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
+    return;
+#endif
+    for (uint32_t it = 1; __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v; it++) {
+        if ((it & 255u) == 0u) {
+            if (it >= *cap || __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
                 __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 break;
             }
@@ -78,7 +91,7 @@ __device__ __forceinline__ int xcd_block(int b, int nb) {
 
 // The workgroup's give-up flag into the handle's fault word (one lane; a vector atomic).
 __device__ __forceinline__ void report_abort(const DevState& S, uint32_t abort) {
-    if (abort) __hip_atomic_fetch_or(S.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (abort) __hip_atomic_fetch_or(aux_words(S) + AUX_FAULT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------- load / store of Env
@@ -976,7 +989,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
     __shared__ uint32_t s_post[PG ? NPOST : 1][BLOCK];
     __shared__ uint32_t s_pick[PG ? 6 : 1][BLOCK];   // next_order, W4, W5, W7, result, flags
     __shared__ uint32_t s_agv[PG ? 12 : 1][BLOCK];   // W5, W6, W7..W12, result, flags, move, pend
-    __shared__ uint32_t s_postflag, s_pickflag, s_abort;
+    __shared__ uint32_t s_postflag, s_pickflag, s_abort, s_cap;
     __shared__ uint16_t s_code[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint8_t s_next[LDS ? MAX_SLOTS * BLOCK : 1];
     __shared__ uint16_t s_cstep[LDS ? MAX_SLOTS * BLOCK : 1];
@@ -997,7 +1010,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
         s_act[0][0][lane] = pack_actions(act, 0);
         s_act[0][1][lane] = pack_actions(act, 4);
     }
-    if (threadIdx.x == 0) s_abort = 0;
+    if (threadIdx.x == 0) { s_abort = 0; s_cap = aux_words(S)[AUX_SPIN_CAP]; }
     if constexpr (PG) {   // step-0 mailboxes
         if (threadIdx.x == 0) { s_postflag = 0; s_pickflag = 0; }
         if (wave == 0 && valid) {
@@ -1186,7 +1199,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
             }
             if constexpr (PG) {   // step k + 1's pickup, once the sim wave has posted its state
                 if (part == 0 && pre && k + 1 < K) {
-                    spin_until(&s_postflag, (uint32_t)(k + 1), &s_abort, C.spin_cap);
+                    spin_until(&s_postflag, (uint32_t)(k + 1), &s_abort, &s_cap);
                     if (valid) {
                         Env Ep;
 #pragma unroll
@@ -1228,7 +1241,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
             }
             if constexpr (PG) {   // step k + 1's AGV, on the posted state and that step's pickup
                 if (part == 1 && pre && k + 1 < K) {
-                    spin_until(&s_pickflag, (uint32_t)(k + 1), &s_abort, C.spin_cap);
+                    spin_until(&s_pickflag, (uint32_t)(k + 1), &s_abort, &s_cap);
                     if (valid) {
                         Env Ea;
 #pragma unroll
@@ -1436,6 +1449,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     __shared__ uint32_t s_flag1;   // AM posted step k's pickup / AGV words and machine lists (k + 1)
     __shared__ uint32_t s_uflag;   // E3 posted step k+1's pickup (k + 1)
     __shared__ uint32_t s_abort;   // a bounded hand-off wait of this workgroup gave up (spin_until)
+    __shared__ uint32_t s_cap;     // its bound (aux word AUX_SPIN_CAP)
     __shared__ uint4 s_pk[BLOCK];   // E3: W0, W4, W5, W7 after step k+1's pickup
     __shared__ uint2 s_pkr[BLOCK];  // E3: its result word, status bits
     __shared__ double s_lut[RLUT_SIZE];
@@ -1443,7 +1457,11 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     C.lut = s_lut;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / BLOCK);
     const int lane = threadIdx.x % BLOCK;
-    const int blk = C.xcd_map ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+#ifdef FJSP_X_NOXCD   // diagnostic build only: workgroup b holds env block b
+    const int blk = (int)blockIdx.x;
+#else
+    const int blk = xcd_block((int)blockIdx.x, (int)gridDim.x);
+#endif
     const int e = blk * EPW + lane;
     const bool valid = lane < EPW && e < S.n;
     const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
@@ -1459,9 +1477,9 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             s_act[j][1][lane] = pack_actions(act, 4);
         }
     }
-    if (threadIdx.x == 0) { s_flag1 = 0; s_uflag = 0; s_abort = 0; }
+    if (threadIdx.x == 0) { s_flag1 = 0; s_uflag = 0; s_abort = 0; s_cap = aux_words(S)[AUX_SPIN_CAP]; }
     auto ag_spin = [&](uint32_t* flag, uint32_t v) __attribute__((always_inline)) {
-        spin_until(flag, v, &s_abort, C.spin_cap);
+        spin_until(flag, v, &s_abort, &s_cap);
     };
     if (valid) {
         // the env's order table, used slot prefix and pre-drawn table live in LDS for the launch
@@ -1848,7 +1866,9 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 const uint32_t t = (uint32_t)(k - 1);
                 uint32_t v[SNAP_N];
                 snap_get(snap[(k - 1) & 1], lane, v);
+#ifndef FJSP_X_NOABORTST
                 if (part == 2 && s_abort) v[SA_ST] |= ST_SPIN_TIMEOUT | ST_DIVERGED;
+#endif
                 FJSP_DIAG(
                 __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the snapshot arrived
                 )
@@ -1962,7 +1982,6 @@ struct fjsp_handle {
     int ag_epw;      // k_step_ag envs per workgroup: 64 / 32 / 16, 0 = auto (FJSP_AG_EPW / "ag_envs")
     const char* last_kernel;   // name of the last step kernel launched (fjsp_last_kernel)
     uint32_t env_id_base;      // global id of env 0 (fjsp_set_option "env_id_base")
-    uint32_t* fault_dev;       // fjsp_faults word
 };
 
 static thread_local std::string g_err;
@@ -2096,11 +2115,9 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     h->dcfg.ptk_small = c.pt_small / c.step_size;
     h->dcfg.ptk_big = c.pt_big / c.step_size;
     h->dcfg.ptk_pack = c.pt_packaging / c.step_size;
-    h->dcfg.spin_cap = 1u << 22;   // ~0.1 s of sleeps: far beyond any legitimate hand-off wait
-    h->dcfg.xcd_map = 1;
 
     const size_t n = (size_t)num_envs;
-    const size_t b_words = (size_t)NWORDS * n * 4, b_orders = (size_t)MAX_ORDERS * n * 4;
+    const size_t b_words = ((size_t)NWORDS * n + AUX_WORDS) * 4, b_orders = (size_t)MAX_ORDERS * n * 4;
     const size_t b_scode = (size_t)MAX_SLOTS * n * 2, b_snext = (size_t)MAX_SLOTS * n, b_scstep = (size_t)MAX_SLOTS * n * 2;
     const size_t b_mt = (size_t)2 * MT_N * n * 4, b_nxt = (size_t)MAX_ORDERS * n * 4;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -2126,11 +2143,14 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     if (e != hipSuccess) { h->ev1 = nullptr; return bail("hipEventCreate", e); }
     e = hipMalloc(&h->lut_dev, sizeof(double) * RLUT_SIZE);
     if (e != hipSuccess) { h->lut_dev = nullptr; return bail("hipMalloc(reward table)", e); }
-    e = hipMalloc(&h->fault_dev, sizeof(uint32_t));
-    if (e != hipSuccess) { h->fault_dev = nullptr; return bail("hipMalloc(fault word)", e); }
-    e = hipMemsetAsync(h->fault_dev, 0, sizeof(uint32_t), h->stream);
-    if (e != hipSuccess) return bail("fault word", e);
-    h->S.fault = h->fault_dev;
+    {
+        // the aux words: fault 0, hand-off bound ~0.1 s of sleeps (far beyond any legitimate wait)
+        const uint32_t aux[AUX_WORDS] = {0u, 1u << 22, 0u, 0u};
+        e = hipMemcpyAsync(h->S.words + (size_t)NWORDS * n, aux, sizeof(aux), hipMemcpyHostToDevice, h->stream);
+        if (e != hipSuccess) return bail("aux words", e);
+        e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return bail("aux words", e);
+    }
     h->dcfg.lut = h->lut_dev;
     {
         fjsp_reward_weights w;
@@ -2156,7 +2176,6 @@ int fjsp_destroy(fjsp_handle* h) {
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->lut_dev) (void)hipFree(h->lut_dev);
-    if (h->fault_dev) (void)hipFree(h->fault_dev);
     if (h->base) (void)hipFree(h->base);
     delete h;
     return 0;
@@ -2175,10 +2194,12 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
         return 0;
     }
     if (!strcmp(name, "timing")) { h->timing = value != 0; if (!h->timing) h->timed = 0; return 0; }
-    if (!strcmp(name, "xcd_map")) { h->dcfg.xcd_map = value != 0; return 0; }
     if (!strcmp(name, "spin_cap")) {
-        if (value < 1 || value > 0x7FFFFFFFll) return fail("spin_cap must be in 1..2^31-1");
-        h->dcfg.spin_cap = (uint32_t)value;
+        if (value < 256 || value > 0x7FFFFFFFll) return fail("spin_cap must be in 256..2^31-1");
+        DeviceGuard g(h->device);
+        const uint32_t v = (uint32_t)value;
+        HIPCHK(hipStreamSynchronize(h->stream));
+        HIPCHK(hipMemcpy(h->S.words + (size_t)NWORDS * h->n + AUX_SPIN_CAP, &v, 4, hipMemcpyHostToDevice));
         return 0;
     }
     if (!strcmp(name, "env_id_base")) {
@@ -2429,8 +2450,9 @@ int fjsp_faults(fjsp_handle* h, uint32_t* out, int32_t clear) {
     if (!h || !out) return fail("null argument");
     DeviceGuard g(h->device);
     HIPCHK(hipStreamSynchronize(h->stream));
-    HIPCHK(hipMemcpy(out, h->fault_dev, sizeof(uint32_t), hipMemcpyDeviceToHost));
-    if (clear) HIPCHK(hipMemset(h->fault_dev, 0, sizeof(uint32_t)));
+    uint32_t* w = h->S.words + (size_t)NWORDS * h->n + AUX_FAULT;
+    HIPCHK(hipMemcpy(out, w, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (clear) HIPCHK(hipMemset(w, 0, sizeof(uint32_t)));
     return 0;
 }
 

@@ -22,6 +22,7 @@
 // PyTorch's GEMMs only by rounding (tests: 1e-5).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/fjsp.h"
 
@@ -148,20 +149,45 @@ __device__ __forceinline__ void hidden256(const float* __restrict__ W, const flo
     __syncthreads();
 }
 
+// The critic's three hidden layers on the first 32 * NC columns of the tile -> h3 [128][TILE].
+template <int NC>
+__device__ __forceinline__ void critic_cols(const float* __restrict__ critic_w, const float* s_x, float* s_h, int wave,
+                                            int lane) {
+    hidden256<FJSP_POLICY_CRITIC_DPAD, NC>(critic_w, s_x, s_h, wave, lane);
+    const float* W3 = critic_w + 256 * FJSP_POLICY_CRITIC_DPAD + 256 + 256 * 256 + 256;   // packed [4][32][64][4]
+    const float* B3 = W3 + 128 * HID;                  // [128]
+    f32x16 acc[1][NC];
+    if (wave < 4) {                                    // 128 rows = 4 row tiles
+        zero_acc<1, NC>(acc);
+        mfma_rows<1, 128, NC>(W3, wave, s_h, lane, acc);
+    }
+    __syncthreads();
+    if (wave < 4) store_rows<1, NC>(acc, 32 * wave, B3, s_h, lane);
+    __syncthreads();
+}
+
 // Work item b of a k_policy launch over nt 64-env tiles, longest first (the hardware dispatcher
 // hands workgroups out in order as slots free up: list scheduling, longest processing time
 // first): [0, 2 nt) the critic on 32-env halves (3 392 MFMAs per 64 envs: on one CU its two
 // waves per SIMD would take 22.6 us alone, the longest item by far), [2 nt, 4 nt) the AGV's
 // and the pickup station's actors, [4 nt, 10 nt) the six stations' actors (mostly forced tiles
 // that skip their MLP).  role NAG = critic.
+constexpr int POLICY_ORDER = 0;   // default order (policy_item)
 struct PolicyItem {
     int role, e0, half;
 };
-__device__ __forceinline__ PolicyItem policy_item(int b, int nt) {
-    if (b < 2 * nt) return {NAG, (b >> 1) * TILE + (b & 1) * 32, 1};
-    if (b < 3 * nt) return {1, (b - 2 * nt) * TILE, 0};
-    if (b < 4 * nt) return {0, (b - 3 * nt) * TILE, 0};
-    const int j = b - 4 * nt;
+// order (FJSP_POLICY_ORDER, measured): bit 0 = the critic on 32-env halves (else 64-env tiles),
+// bit 1 = the actors longest first with the stations interleaved (else role-major in agent order,
+// r02's layout).  The critic's items always come first.
+__device__ __forceinline__ PolicyItem policy_item(int b, int nt, int order) {
+    const bool halves = order & 1;
+    const int nc = halves ? 2 * nt : nt;
+    if (b < nc) return halves ? PolicyItem{NAG, (b >> 1) * TILE + (b & 1) * 32, 1} : PolicyItem{NAG, b * TILE, 0};
+    b -= nc;
+    if (!(order & 2)) return {b / nt, (b % nt) * TILE, 0};
+    if (b < nt) return {1, b * TILE, 0};
+    if (b < 2 * nt) return {0, (b - nt) * TILE, 0};
+    const int j = b - 2 * nt;
     return {2 + j % 6, (j / 6) * TILE, 0};
 }
 
@@ -169,12 +195,13 @@ __global__ void __launch_bounds__(NTHR, 4) k_policy(const float* __restrict__ fe
                                                    int n, const float* __restrict__ actor_w,
                                                    const float* __restrict__ critic_w, const uint64_t* __restrict__ seedp,
                                                    uint32_t gid0, uint32_t step, int deterministic, uint8_t* __restrict__ actions,
-                                                   float* __restrict__ values, float* __restrict__ probs_out, int item0) {
+                                                   float* __restrict__ values, float* __restrict__ probs_out, int item0,
+                                                   int order) {
     __shared__ float s_x[FJSP_POLICY_CRITIC_DPAD * TILE];   // inputs; later the logits [8][TILE]
     __shared__ float s_h[HID * TILE];                        // h1, then h2 (then critic h3)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const PolicyItem it = policy_item((int)blockIdx.x + item0, (n + TILE - 1) / TILE);
+    const PolicyItem it = policy_item((int)blockIdx.x + item0, (n + TILE - 1) / TILE, order);
     const int role = it.role, e0 = it.e0;
     const bool critic = role == NAG;
     if (!critic) {
@@ -205,27 +232,18 @@ __global__ void __launch_bounds__(NTHR, 4) k_policy(const float* __restrict__ fe
     const int din = critic ? 38 : c_obs_dim[role];
     const int off = critic ? 0 : c_obs_off[role];
     const int dpad = critic ? FJSP_POLICY_CRITIC_DPAD : FJSP_POLICY_ACTOR_DPAD;
-    const int cols = critic ? 32 : TILE;               // the critic's items are 32-env halves
+    const int cols = critic && it.half ? 32 : TILE;   // a critic item is a 32-env half or a 64-env tile
     for (int i = tid; i < dpad * cols; i += NTHR) {
         const int k = i / cols, c = i % cols;
         s_x[k * TILE + c] = (k < din && e0 + c < n) ? feats[(size_t)(off + k) * n + e0 + c] : 0.0f;
     }
     __syncthreads();
     if (critic) {
-        hidden256<FJSP_POLICY_CRITIC_DPAD, 1>(critic_w, s_x, s_h, wave, lane);
-        const float* W3 = critic_w + 256 * FJSP_POLICY_CRITIC_DPAD + 256 + 256 * 256 + 256;   // packed [4][32][64][4]
-        const float* B3 = W3 + 128 * HID;                  // [128]
-        const float* W4 = B3 + 128;                        // [128]
-        const float* B4 = W4 + 128;                        // [1]
-        f32x16 acc[1][1];
-        if (wave < 4) {                                    // 128 rows = 4 row tiles
-            zero_acc<1, 1>(acc);
-            mfma_rows<1, 128, 1>(W3, wave, s_h, lane, acc);
-        }
-        __syncthreads();
-        if (wave < 4) store_rows<1, 1>(acc, 32 * wave, B3, s_h, lane);   // h3 [128][32 of TILE]
-        __syncthreads();
-        if (tid < 32 && e0 + tid < n) {
+        if (it.half) critic_cols<1>(critic_w, s_x, s_h, wave, lane);
+        else critic_cols<NCOL>(critic_w, s_x, s_h, wave, lane);
+        const float* B4 = critic_w + 256 * FJSP_POLICY_CRITIC_DPAD + 256 + 256 * 256 + 256 + 128 * HID + 128 + 128;
+        const float* W4 = B4 - 128;
+        if (tid < cols && e0 + tid < n) {
             float v = B4[0];
             for (int k = 0; k < 128; k++) v = fmaf(W4[k], s_h[k * TILE + tid], v);
             values[e0 + tid] = v;
@@ -645,9 +663,12 @@ extern "C" int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t 
     const int nt = (n + TILE - 1) / TILE;
     // policy_item: 2 nt critic halves, then 8 nt actor tiles; without actions only the first
     // range (values), without values only the second (actions)
-    const int item0 = values ? 0 : 2 * nt, item1 = actions ? 10 * nt : 2 * nt;
+    const char* ov = getenv("FJSP_POLICY_ORDER");
+    const int order = ov ? atoi(ov) & 3 : POLICY_ORDER;
+    const int nc = (order & 1) ? 2 * nt : nt;
+    const int item0 = values ? 0 : nc, item1 = actions ? nc + 8 * nt : nc;
     hipLaunchKernelGGL(k_policy, dim3(item1 - item0), dim3(NTHR), 0, (hipStream_t)stream, feats, masks, n, actor_w, critic_w,
-                       seed, env_gid0, step, deterministic, actions, values, probs, item0);
+                       seed, env_gid0, step, deterministic, actions, values, probs, item0, order);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

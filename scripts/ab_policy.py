@@ -5,7 +5,7 @@ turn, HIP events per launch; outputs (greedy actions, values, probabilities) com
 byte with the first library's.  Libraries through raw ctypes (the signature is unchanged since
 ABI 3).
 
-usage: python scripts/ab_policy.py [N] [init] lib ...
+usage: python scripts/ab_policy.py [N] [init] lib[:order[:all|actors|values]] ...   (order -> FJSP_POLICY_ORDER)
 """
 import ctypes
 import importlib
@@ -42,7 +42,14 @@ T = L.batch_size
 
 res = {"N": N, "init": INIT, "steps": T, "libs": []}
 ref = None
-for path in libs:
+for spec in libs:
+    path, _, rest = spec.partition(":")
+    order, _, part = rest.partition(":")
+    part = part or "all"
+    if order:
+        os.environ["FJSP_POLICY_ORDER"] = order
+    else:
+        os.environ.pop("FJSP_POLICY_ORDER", None)
     lib = ctypes.CDLL(os.path.abspath(path))
     f = lib.fjsp_a2c_policy
     f.argtypes = [P, P, ctypes.c_int32, P, P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32, P, P, P, P]
@@ -52,8 +59,9 @@ for path in libs:
 
     def run(t, det, pr=None):
         rc = f(P(feats[t].data_ptr()), P(masks[t].data_ptr()), N, P(L._pw_actor.data_ptr()), P(L._pw_critic.data_ptr()),
-               P(L._rng.data_ptr()), 0, t, det, P(act.data_ptr()), P(val.data_ptr()),
-               None if pr is None else P(pr.data_ptr()), P(stream.cuda_stream))
+               P(L._rng.data_ptr()), 0, t, det, None if part == "values" else P(act.data_ptr()),
+               None if part == "actors" else P(val.data_ptr()),
+               None if pr is None or part == "values" else P(pr.data_ptr()), P(stream.cuda_stream))
         assert rc == 0
     outs = []
     for t in (0, 100, 255):
@@ -74,9 +82,9 @@ for path in libs:
     same = None
     if ref is None:
         ref = outs
-    else:
+    elif part == "all":
         same = all(torch.equal(a[i], b[i]) for a, b in zip(outs, ref) for i in range(3))
-    res["libs"].append({"lib": path, "median_us": float(np.median(ms)), "mean_us": float(np.mean(ms)),
+    res["libs"].append({"lib": spec, "median_us": float(np.median(ms)), "mean_us": float(np.mean(ms)),
                         "p10_us": float(np.percentile(ms, 10)), "p90_us": float(np.percentile(ms, 90)),
                         "outputs_equal_to_first": same})
 print(json.dumps(res))

@@ -6,10 +6,10 @@ mkdir -p gpurun_out
 ( while true; do date +%T >> gpurun_out/heartbeat.log; sleep 45; done ) &
 HB=$!; trap 'kill $HB 2>/dev/null' EXIT
 PK=multi-agent-rl-for-fjsp_amd
-timeout -k 10 200 python scripts/ab_step.py 4096 10 $PK/libfjsp_r02.so $PK/libfjsp.so:xcd_map=0 $PK/libfjsp.so:xcd_map=1 > gpurun_out/ab_step.json 2> gpurun_out/ab_step.err
+timeout -k 10 200 python scripts/ab_step.py 4096 10 $PK/libfjsp_r02.so $PK/libfjsp.so $PK/libfjsp_noxcd.so > gpurun_out/ab_step.json 2> gpurun_out/ab_step.err
 rc=$?; echo "ab_step rc=$rc"; tail -c 1500 gpurun_out/ab_step.json; [ $rc -le 1 ] || exit $rc
 for init in random trained; do
-  timeout -k 10 200 python scripts/ab_policy.py 4096 $init $PK/libfjsp_r02.so $PK/libfjsp.so > gpurun_out/ab_policy_$init.json 2>> gpurun_out/ab_policy.err
+  timeout -k 10 200 python scripts/ab_policy.py 4096 $init $PK/libfjsp_r02.so $PK/libfjsp.so:0 $PK/libfjsp.so:1 $PK/libfjsp.so:2 $PK/libfjsp.so:3 $PK/libfjsp.so:0:actors $PK/libfjsp.so:0:values $PK/libfjsp.so:3:actors $PK/libfjsp.so:3:values > gpurun_out/ab_policy_$init.json 2>> gpurun_out/ab_policy.err
   rc=$?; echo "ab_policy $init rc=$rc"; tail -c 1500 gpurun_out/ab_policy_$init.json; [ $rc -le 1 ] || exit $rc
 done
 for init in random trained; do

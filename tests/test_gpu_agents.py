@@ -216,8 +216,9 @@ def test_agents_envs_per_workgroup(G, epw):
 def test_bounded_handoff_waits(G, agents):
     """The hand-off waits of the multi-wave kernels (k_step_ag's flag spins, k_step_pipe's
     mailboxes) are bounded.  At the default bound a 4 096-env x 1 024-step bench launch never
-    gives up (fault word 0, no env carries FJSP_STATUS_SPIN_TIMEOUT).  At a bound of one sleep a
-    wait that finds the flag unset gives up: the launch still ends, and a workgroup that gave up
+    gives up (fault word 0, no env carries FJSP_STATUS_SPIN_TIMEOUT).  At the smallest bound (256
+    sleeps, ~7 us: the first step waits that long for the tables' copy-in) a wait may give up:
+    the launch still ends, and a workgroup that gave up
     flags every env it holds (status bit 0x80 | DIVERGED, fault word bit 0) while workgroups that
     did not are byte-identical to the unbounded run."""
     env = _env(G, 4096, agents)
@@ -231,7 +232,7 @@ def test_bounded_handoff_waits(G, agents):
     ref.reset(num_orders=30)
     r0 = G.to_np(ref.rollout(64, action_seed=5, policy="random"))
     tight = _env(G, n, agents)
-    G.native.check(G.native.lib().fjsp_set_option(tight.handle, b"spin_cap", 1))
+    G.native.check(G.native.lib().fjsp_set_option(tight.handle, b"spin_cap", 256))
     tight.reset(num_orders=30)
     r1 = G.to_np(tight.rollout(64, action_seed=5, policy="random"))
     fault = tight.faults(clear=True)
