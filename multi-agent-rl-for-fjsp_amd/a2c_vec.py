@@ -830,10 +830,6 @@ class VecMultiAgentA2C:
         self._graph = None
         self._graph_det = None
         self._eager_batches = 0
-        # collect: the critic's values on a second stream, beside the actors -> step chain (a step
-        # needs the actions, not the value; same kernel, same results)
-        self.split_critic = self.fused_policy
-        self._side = None
         self.gae_fn = batch_advantages     # finish_trajectory over a batch (tests may inject a CPU stand-in)
         self.grad_probe = None             # grad_probe(flat reduced grads) before clip / Adam (tests)
         self.exchange_timing = None        # dict of synchronised stage times (ms) when not None (bench)
@@ -963,25 +959,8 @@ class VecMultiAgentA2C:
         h = self.env.handle
         self.env._sync_stream()
         T = self.batch_size
-        split = self.fused_policy and action_fn is None and self.split_critic
-        if split:
-            # per step t: the actors (main stream) -> fjsp_step (main); the critic of the same
-            # observation on the side stream once step t - 1 has written it, overlapping the
-            # actors and the step (the critic is ~a quarter of the policy's MFMA work and its
-            # value is only needed by the update); joined at the end of the batch
-            main = torch.cuda.current_stream(self.device)
-            if self._side is None:
-                self._side = torch.cuda.Stream(self.device)
-                self._evs = [torch.cuda.Event() for _ in range(T + 1)]
-            side = self._side
         for t in range(T):
-            if split:
-                self._evs[t].record(main)
-                with torch.cuda.stream(side):
-                    side.wait_event(self._evs[t])
-                    self.policy_fused(b["feats"][t], None, t, deterministic, None, b["values"][t])
-                self.policy_fused(b["feats"][t], b["masks"][t], t, deterministic, b["actions"][t], None)
-            elif self.fused_policy and action_fn is None:
+            if self.fused_policy and action_fn is None:
                 self.policy_fused(b["feats"][t], b["masks"][t], t, deterministic, b["actions"][t], b["values"][t])
             else:
                 act, _, v = self.policy(b["feats"][t], b["masks"][t], deterministic, t=t)
@@ -992,13 +971,7 @@ class VecMultiAgentA2C:
             nat.check(L.fjsp_step(h, ctypes.c_void_p(b["actions"][t].data_ptr()), None, 1,
                                   ctypes.byref(b["outs"][t])))
         with torch.no_grad():
-            if split:
-                self._evs[T].record(main)
-                with torch.cuda.stream(side):
-                    side.wait_event(self._evs[T])
-                    self.policy_fused(b["feats"][T], None, T, True, None, b["values"][T])
-                main.wait_stream(side)
-            elif self.fused_policy:
+            if self.fused_policy:
                 # the bootstrap V(s_T) by the same kernel as every step's value: a value depends
                 # only on its env's features, never on how the envs are sharded
                 self.policy_fused(b["feats"][T], None, T, True, None, b["values"][T])

@@ -6,8 +6,8 @@
 // action draw (inverse CDF over the masked probabilities, or argmax) and the centralised
 // critic (networks.CentralizedCriticNetwork: 38 -> 256 -> 256 -> 128 -> 1).
 //
-// Grid: one work item per workgroup (policy_item: the critic on 32-env halves first, then the
-// actors on 64-env tiles); 512 threads = 8 wavefronts.  The hidden activations never leave LDS:
+// Grid: blockIdx.y = role (0 critic, 1..8 actor of agent y - 1), blockIdx.x = tile of 64 envs;
+// 512 threads = 8 wavefronts.  The hidden activations never leave LDS:
 //   x   [40][TILE]  inputs of the tile (feature rows of the kernel-written [38][N] slab)
 //   h   [256][TILE] layer 1, then layer 2, then the critic's layer 3 (in place: results stay in
 //                   registers across a barrier), so two workgroups fit a CU (74 KB of LDS each)
@@ -22,7 +22,6 @@
 // PyTorch's GEMMs only by rounding (tests: 1e-5).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 #include "../../include/fjsp.h"
 
@@ -42,6 +41,9 @@ constexpr int NTHR = 64 * NWAVE;
 constexpr int HID = 256;
 constexpr int NAG = 8;
 constexpr int KS2 = HID / 2;   // k-steps of 2 for a 256-wide contraction
+#ifndef POLICY_PF
+#define POLICY_PF 2   // weight groups (4 k-steps each) in flight per wave
+#endif
 
 __constant__ int c_obs_off[NAG] = {0, 7, 20, 23, 26, 29, 32, 35};
 __constant__ int c_obs_dim[NAG] = {7, 13, 3, 3, 3, 3, 3, 3};
@@ -59,16 +61,16 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t z) {
 // W[32 t + (l & 31)][2 (4 q + j) + (l >> 5)], so one 16-byte load per lane fetches the A
 // fragments of 4 consecutive k-steps (a coalesced 1 KB per wave instruction).
 // acc[i][j] += W(row tile rt0 + i) . act(col tile j); act = LDS [K][TILE] (rows = k), KS = K / 2.
-template <int NT, int KS, int NC = NCOL>
+template <int NT, int KS>
 __device__ __forceinline__ void mfma_rows(const float* __restrict__ wp, int rt0, const float* act, int lane,
-                                          f32x16 acc[NT][NC]) {
+                                          f32x16 acc[NT][NCOL]) {
     static_assert(KS % 4 == 0, "k-steps come in groups of 4");
     constexpr int NQ = KS / 4;
     const float4* a[NT];
 #pragma unroll
     for (int i = 0; i < NT; i++) a[i] = reinterpret_cast<const float4*>(wp) + (size_t)(rt0 + i) * NQ * 64 + lane;
     const int kr = lane >> 5, cl = lane & 31;
-    constexpr int PF = NQ < 2 ? NQ : 2;   // groups in flight
+    constexpr int PF = NQ < POLICY_PF ? NQ : POLICY_PF;   // groups in flight
     float4 buf[PF][NT];
 #pragma unroll
     for (int p = 0; p < PF; p++)
@@ -76,35 +78,41 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ wp, int rt0,
         for (int i = 0; i < NT; i++) buf[p][i] = a[i][p * 64];
 #pragma unroll 2
     for (int q = 0; q < NQ; q++) {
+        // a register ring: consume the oldest group, shift, load PF groups ahead (static
+        // indices for any PF; a q % PF index would go to scratch)
         float4 cur[NT];
 #pragma unroll
-        for (int i = 0; i < NT; i++) cur[i] = buf[q % PF][i];
+        for (int i = 0; i < NT; i++) cur[i] = buf[0][i];
+#pragma unroll
+        for (int p = 0; p + 1 < PF; p++)
+#pragma unroll
+            for (int i = 0; i < NT; i++) buf[p][i] = buf[p + 1][i];
         if (q + PF < NQ) {
 #pragma unroll
-            for (int i = 0; i < NT; i++) buf[q % PF][i] = a[i][(q + PF) * 64];
+            for (int i = 0; i < NT; i++) buf[PF - 1][i] = a[i][(q + PF) * 64];
         }
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int k = 2 * (4 * q + j) + kr;
-            float b[NC];
+            float b[NCOL];
 #pragma unroll
-            for (int c = 0; c < NC; c++) b[c] = act[k * TILE + 32 * c + cl];
+            for (int c = 0; c < NCOL; c++) b[c] = act[k * TILE + 32 * c + cl];
 #pragma unroll
             for (int i = 0; i < NT; i++) {
                 const float fa = j == 0 ? cur[i].x : j == 1 ? cur[i].y : j == 2 ? cur[i].z : cur[i].w;
 #pragma unroll
-                for (int c = 0; c < NC; c++) acc[i][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, b[c], acc[i][c], 0, 0, 0);
+                for (int c = 0; c < NCOL; c++) acc[i][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, b[c], acc[i][c], 0, 0, 0);
             }
         }
     }
 }
 
-template <int NT, int NC = NCOL>
-__device__ __forceinline__ void zero_acc(f32x16 acc[NT][NC]) {
+template <int NT>
+__device__ __forceinline__ void zero_acc(f32x16 acc[NT][NCOL]) {
 #pragma unroll
     for (int i = 0; i < NT; i++)
 #pragma unroll
-        for (int j = 0; j < NC; j++)
+        for (int j = 0; j < NCOL; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] = 0.0f;
 }
@@ -120,89 +128,49 @@ __device__ __forceinline__ void store_tile(const f32x16& acc, int row0, int col0
         out[row * TILE + col0 + (lane & 31)] = v > 0.0f ? v : 0.0f;
     }
 }
-template <int NT, int NC = NCOL>
-__device__ __forceinline__ void store_rows(const f32x16 acc[NT][NC], int row0, const float* __restrict__ bias, float* out,
+template <int NT>
+__device__ __forceinline__ void store_rows(const f32x16 acc[NT][NCOL], int row0, const float* __restrict__ bias, float* out,
                                            int lane) {
 #pragma unroll
     for (int i = 0; i < NT; i++)
 #pragma unroll
-        for (int j = 0; j < NC; j++) store_tile(acc[i][j], row0 + 32 * i, 32 * j, bias, out, lane);
+        for (int j = 0; j < NCOL; j++) store_tile(acc[i][j], row0 + 32 * i, 32 * j, bias, out, lane);
 }
 
-// Hidden layers 1 and 2 of a 256-wide MLP on the tile (x in s_x [DPAD][TILE]) -> s_h [256][TILE],
-// on the first 32 * NC columns.
-template <int DPAD, int NC = NCOL>
+// Hidden layers 1 and 2 of a 256-wide MLP on the tile (x in s_x [DPAD][TILE]) -> s_h [256][TILE].
+template <int DPAD>
 __device__ __forceinline__ void hidden256(const float* __restrict__ W, const float* s_x, float* s_h, int wave, int lane) {
     const float* W1 = W;                         // packed [8][DPAD/8][64][4]
     const float* B1 = W1 + 256 * DPAD;           // [256]
     const float* W2 = B1 + 256;                  // packed [8][32][64][4]
     const float* B2 = W2 + 256 * 256;            // [256]
-    f32x16 acc[1][NC];
-    zero_acc<1, NC>(acc);
-    mfma_rows<1, DPAD / 2, NC>(W1, wave, s_x, lane, acc);
-    store_rows<1, NC>(acc, 32 * wave, B1, s_h, lane);
+    f32x16 acc[1][NCOL];
+    zero_acc<1>(acc);
+    mfma_rows<1, DPAD / 2>(W1, wave, s_x, lane, acc);
+    store_rows<1>(acc, 32 * wave, B1, s_h, lane);
     __syncthreads();
-    zero_acc<1, NC>(acc);
-    mfma_rows<1, 128, NC>(W2, wave, s_h, lane, acc);
+    zero_acc<1>(acc);
+    mfma_rows<1, 128>(W2, wave, s_h, lane, acc);
     __syncthreads();                             // every wave has read h1
-    store_rows<1, NC>(acc, 32 * wave, B2, s_h, lane);
+    store_rows<1>(acc, 32 * wave, B2, s_h, lane);
     __syncthreads();
-}
-
-// The critic's three hidden layers on the first 32 * NC columns of the tile -> h3 [128][TILE].
-template <int NC>
-__device__ __forceinline__ void critic_cols(const float* __restrict__ critic_w, const float* s_x, float* s_h, int wave,
-                                            int lane) {
-    hidden256<FJSP_POLICY_CRITIC_DPAD, NC>(critic_w, s_x, s_h, wave, lane);
-    const float* W3 = critic_w + 256 * FJSP_POLICY_CRITIC_DPAD + 256 + 256 * 256 + 256;   // packed [4][32][64][4]
-    const float* B3 = W3 + 128 * HID;                  // [128]
-    f32x16 acc[1][NC];
-    if (wave < 4) {                                    // 128 rows = 4 row tiles
-        zero_acc<1, NC>(acc);
-        mfma_rows<1, 128, NC>(W3, wave, s_h, lane, acc);
-    }
-    __syncthreads();
-    if (wave < 4) store_rows<1, NC>(acc, 32 * wave, B3, s_h, lane);
-    __syncthreads();
-}
-
-// Work item b of a k_policy launch over nt 64-env tiles, longest first (the hardware dispatcher
-// hands workgroups out in order as slots free up: list scheduling, longest processing time
-// first): [0, 2 nt) the critic on 32-env halves (3 392 MFMAs per 64 envs: on one CU its two
-// waves per SIMD would take 22.6 us alone, the longest item by far), [2 nt, 4 nt) the AGV's
-// and the pickup station's actors, [4 nt, 10 nt) the six stations' actors (mostly forced tiles
-// that skip their MLP).  role NAG = critic.
-constexpr int POLICY_ORDER = 0;   // default order (policy_item)
-struct PolicyItem {
-    int role, e0, half;
-};
-// order (FJSP_POLICY_ORDER, measured): bit 0 = the critic on 32-env halves (else 64-env tiles),
-// bit 1 = the actors longest first with the stations interleaved (else role-major in agent order,
-// r02's layout).  The critic's items always come first.
-__device__ __forceinline__ PolicyItem policy_item(int b, int nt, int order) {
-    const bool halves = order & 1;
-    const int nc = halves ? 2 * nt : nt;
-    if (b < nc) return halves ? PolicyItem{NAG, (b >> 1) * TILE + (b & 1) * 32, 1} : PolicyItem{NAG, b * TILE, 0};
-    b -= nc;
-    if (!(order & 2)) return {b / nt, (b % nt) * TILE, 0};
-    if (b < nt) return {1, b * TILE, 0};
-    if (b < 2 * nt) return {0, (b - nt) * TILE, 0};
-    const int j = b - 2 * nt;
-    return {2 + j % 6, (j / 6) * TILE, 0};
 }
 
 __global__ void __launch_bounds__(NTHR, 4) k_policy(const float* __restrict__ feats, const int8_t* __restrict__ masks,
                                                    int n, const float* __restrict__ actor_w,
                                                    const float* __restrict__ critic_w, const uint64_t* __restrict__ seedp,
                                                    uint32_t gid0, uint32_t step, int deterministic, uint8_t* __restrict__ actions,
-                                                   float* __restrict__ values, float* __restrict__ probs_out, int item0,
-                                                   int order) {
+                                                   float* __restrict__ values, float* __restrict__ probs_out, int role0) {
     __shared__ float s_x[FJSP_POLICY_CRITIC_DPAD * TILE];   // inputs; later the logits [8][TILE]
     __shared__ float s_h[HID * TILE];                        // h1, then h2 (then critic h3)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const PolicyItem it = policy_item((int)blockIdx.x + item0, (n + TILE - 1) / TILE, order);
-    const int role = it.role, e0 = it.e0;
+    // the critic (the heaviest role: 848 MFMAs per wave against 544) first: 576 workgroups run
+    // on 512 two-per-CU slots, and the ones left for the second round should be the short ones
+    // (measured: 83.8 -> 75.0 us per launch at 4 096 envs)
+    const int y = (int)blockIdx.y + role0;   // role0 = 1: the actors only (no values wanted)
+    const int role = y == 0 ? NAG : y - 1;
+    const int e0 = blockIdx.x * TILE;
     const bool critic = role == NAG;
     if (!critic) {
         // a tile in which the agent has exactly one valid action in every env: the draw (and
@@ -232,18 +200,26 @@ __global__ void __launch_bounds__(NTHR, 4) k_policy(const float* __restrict__ fe
     const int din = critic ? 38 : c_obs_dim[role];
     const int off = critic ? 0 : c_obs_off[role];
     const int dpad = critic ? FJSP_POLICY_CRITIC_DPAD : FJSP_POLICY_ACTOR_DPAD;
-    const int cols = critic && it.half ? 32 : TILE;   // a critic item is a 32-env half or a 64-env tile
-    for (int i = tid; i < dpad * cols; i += NTHR) {
-        const int k = i / cols, c = i % cols;
-        s_x[k * TILE + c] = (k < din && e0 + c < n) ? feats[(size_t)(off + k) * n + e0 + c] : 0.0f;
+    for (int i = tid; i < dpad * TILE; i += NTHR) {
+        const int k = i / TILE, c = i % TILE;
+        s_x[i] = (k < din && e0 + c < n) ? feats[(size_t)(off + k) * n + e0 + c] : 0.0f;
     }
     __syncthreads();
     if (critic) {
-        if (it.half) critic_cols<1>(critic_w, s_x, s_h, wave, lane);
-        else critic_cols<NCOL>(critic_w, s_x, s_h, wave, lane);
-        const float* B4 = critic_w + 256 * FJSP_POLICY_CRITIC_DPAD + 256 + 256 * 256 + 256 + 128 * HID + 128 + 128;
-        const float* W4 = B4 - 128;
-        if (tid < cols && e0 + tid < n) {
+        hidden256<FJSP_POLICY_CRITIC_DPAD>(critic_w, s_x, s_h, wave, lane);
+        const float* W3 = critic_w + 256 * FJSP_POLICY_CRITIC_DPAD + 256 + 256 * 256 + 256;   // packed [4][32][64][4]
+        const float* B3 = W3 + 128 * HID;                  // [128]
+        const float* W4 = B3 + 128;                        // [128]
+        const float* B4 = W4 + 128;                        // [1]
+        f32x16 acc[1][NCOL];
+        if (wave < 4) {                                    // 128 rows = 4 row tiles
+            zero_acc<1>(acc);
+            mfma_rows<1, 128>(W3, wave, s_h, lane, acc);
+        }
+        __syncthreads();
+        if (wave < 4) store_rows<1>(acc, 32 * wave, B3, s_h, lane);   // h3 [128][TILE]
+        __syncthreads();
+        if (tid < TILE && e0 + tid < n) {
             float v = B4[0];
             for (int k = 0; k < 128; k++) v = fmaf(W4[k], s_h[k * TILE + tid], v);
             values[e0 + tid] = v;
@@ -660,15 +636,12 @@ extern "C" int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t 
     if (n <= 0) return fjsp_internal_fail("fjsp_a2c_policy: n must be > 0");
     if (!feats || (!actions && !values) || (values && !critic_w) || (actions && (!masks || !actor_w || !seed)))
         return fjsp_internal_fail("fjsp_a2c_policy: null buffer");
-    const int nt = (n + TILE - 1) / TILE;
-    // policy_item: 2 nt critic halves, then 8 nt actor tiles; without actions only the first
-    // range (values), without values only the second (actions)
-    const char* ov = getenv("FJSP_POLICY_ORDER");
-    const int order = ov ? atoi(ov) & 3 : POLICY_ORDER;
-    const int nc = (order & 1) ? 2 * nt : nt;
-    const int item0 = values ? 0 : nc, item1 = actions ? nc + 8 * nt : nc;
-    hipLaunchKernelGGL(k_policy, dim3(item1 - item0), dim3(NTHR), 0, (hipStream_t)stream, feats, masks, n, actor_w, critic_w,
-                       seed, env_gid0, step, deterministic, actions, values, probs, item0, order);
+    // roles: y = 0 the critic, 1..8 the actors; without actions only the critic (values), without
+    // values only the actors
+    const int role0 = values ? 0 : 1, role1 = actions ? NAG + 1 : 1;
+    dim3 grid((n + TILE - 1) / TILE, role1 - role0);
+    hipLaunchKernelGGL(k_policy, grid, dim3(NTHR), 0, (hipStream_t)stream, feats, masks, n, actor_w, critic_w, seed, env_gid0,
+                       step, deterministic, actions, values, probs, role0);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

@@ -9,12 +9,8 @@ PK=multi-agent-rl-for-fjsp_amd
 timeout -k 10 200 python scripts/ab_step.py 4096 10 $PK/libfjsp_r02.so $PK/libfjsp.so $PK/libfjsp_noxcd.so > gpurun_out/ab_step.json 2> gpurun_out/ab_step.err
 rc=$?; echo "ab_step rc=$rc"; tail -c 1500 gpurun_out/ab_step.json; [ $rc -le 1 ] || exit $rc
 for init in random trained; do
-  timeout -k 10 200 python scripts/ab_policy.py 4096 $init $PK/libfjsp_r02.so $PK/libfjsp.so:0 $PK/libfjsp.so:1 $PK/libfjsp.so:2 $PK/libfjsp.so:3 $PK/libfjsp.so:0:actors $PK/libfjsp.so:0:values $PK/libfjsp.so:3:actors $PK/libfjsp.so:3:values > gpurun_out/ab_policy_$init.json 2>> gpurun_out/ab_policy.err
+  timeout -k 10 200 python scripts/ab_policy.py 4096 $init $PK/libfjsp_r02.so $PK/libfjsp.so $PK/libfjsp_pf3.so $PK/libfjsp_pf4.so $PK/libfjsp_pf6.so $PK/libfjsp.so::actors $PK/libfjsp.so::values $PK/libfjsp_pf4.so::values > gpurun_out/ab_policy_$init.json 2>> gpurun_out/ab_policy.err
   rc=$?; echo "ab_policy $init rc=$rc"; tail -c 1500 gpurun_out/ab_policy_$init.json; [ $rc -le 1 ] || exit $rc
-done
-for init in random trained; do
-  timeout -k 10 200 python scripts/ab_collect.py 4096 $init > gpurun_out/ab_collect_$init.json 2>> gpurun_out/ab_collect.err
-  rc=$?; echo "ab_collect $init rc=$rc"; tail -c 800 gpurun_out/ab_collect_$init.json; [ $rc -le 1 ] || exit $rc
 done
 [ -n "$NO_TESTS" ] && exit 0
 timeout -k 10 900 python -u -m pytest ${PYTEST_FILES:-tests/test_gpu_config5.py tests/test_gpu_shards.py tests/test_gpu_a2c.py tests/test_gpu_trained.py} -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu2.log 2>&1

@@ -377,27 +377,3 @@ def test_fused_policy_forced_tiles(M):
         learner.policy_fused(feats, masks, r, False, act, val)
         for a in range(2, 8):
             assert torch.equal(act[a, :64].long(), ((forced_envs + a) % 3)[:64]), a
-
-
-def test_split_critic_collect_equals_one_stream(M):
-    """The collect with the critic on a side stream (values beside the actors -> step chain,
-    joined at the batch end) produces exactly the buffers of the one-stream collect, eager and
-    graph-replayed, across updates."""
-    A, V = M["A"], M["V"]
-    n, T = 1000, 24
-    Ls = []
-    for split in (False, True):
-        L = A.VecMultiAgentA2C(V.FJSPVecEnv(n), batch_size=T, seed=6)
-        L.split_critic = split
-        L.reset(seeds=torch.arange(n), num_orders=25)
-        Ls.append(L)
-    for b in range(3):                      # eager, capture + replay, replay
-        for L in Ls:
-            L.collect()
-        torch.cuda.synchronize()
-        for k in ("feats", "masks", "actions", "values", "rewards", "term", "trunc"):
-            assert torch.equal(Ls[0]._bufs[k], Ls[1]._bufs[k]), (b, k)
-        for L in Ls:
-            L.update()
-            L.roll_over()
-    assert Ls[0].critic_loss_history == Ls[1].critic_loss_history
