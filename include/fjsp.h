@@ -250,8 +250,7 @@ int64_t fjsp_snapshot_bytes(const fjsp_handle* h);
  * hipGraph can be re-keyed between replays), values f32 [N], optional masked
  * probabilities f32 [8][8][N] (NULL to skip).  actions == NULL: the critic's values only (masks,
  * actor_w and seed may then be NULL; e.g. the batch-end bootstrap V(s_T), a2c.py:321-332);
- * values == NULL: the actors only (critic_w may be NULL).  The two halves can run on two
- * streams: a step needs the actions, not the value.  Stream-ordered on `stream`. */
+ * values == NULL: the actors only (critic_w may be NULL).  Stream-ordered on `stream`. */
 #define FJSP_POLICY_ACTOR_DPAD 16
 #define FJSP_POLICY_CRITIC_DPAD 40
 #define FJSP_POLICY_ACTOR_FLOATS (256 * 16 + 256 + 256 * 256 + 256 + 8 * 256 + 16)

@@ -41,9 +41,6 @@ constexpr int NTHR = 64 * NWAVE;
 constexpr int HID = 256;
 constexpr int NAG = 8;
 constexpr int KS2 = HID / 2;   // k-steps of 2 for a 256-wide contraction
-#ifndef POLICY_PF
-#define POLICY_PF 2   // weight groups (4 k-steps each) in flight per wave
-#endif
 
 __constant__ int c_obs_off[NAG] = {0, 7, 20, 23, 26, 29, 32, 35};
 __constant__ int c_obs_dim[NAG] = {7, 13, 3, 3, 3, 3, 3, 3};
@@ -70,7 +67,7 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ wp, int rt0,
 #pragma unroll
     for (int i = 0; i < NT; i++) a[i] = reinterpret_cast<const float4*>(wp) + (size_t)(rt0 + i) * NQ * 64 + lane;
     const int kr = lane >> 5, cl = lane & 31;
-    constexpr int PF = NQ < POLICY_PF ? NQ : POLICY_PF;   // groups in flight
+    constexpr int PF = NQ < 2 ? NQ : 2;   // groups in flight (3, 4, 6 in a register ring: no faster, r03)
     float4 buf[PF][NT];
 #pragma unroll
     for (int p = 0; p < PF; p++)
@@ -78,18 +75,12 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ wp, int rt0,
         for (int i = 0; i < NT; i++) buf[p][i] = a[i][p * 64];
 #pragma unroll 2
     for (int q = 0; q < NQ; q++) {
-        // a register ring: consume the oldest group, shift, load PF groups ahead (static
-        // indices for any PF; a q % PF index would go to scratch)
         float4 cur[NT];
 #pragma unroll
-        for (int i = 0; i < NT; i++) cur[i] = buf[0][i];
-#pragma unroll
-        for (int p = 0; p + 1 < PF; p++)
-#pragma unroll
-            for (int i = 0; i < NT; i++) buf[p][i] = buf[p + 1][i];
+        for (int i = 0; i < NT; i++) cur[i] = buf[q % PF][i];
         if (q + PF < NQ) {
 #pragma unroll
-            for (int i = 0; i < NT; i++) buf[PF - 1][i] = a[i][(q + PF) * 64];
+            for (int i = 0; i < NT; i++) buf[q % PF][i] = a[i][(q + PF) * 64];
         }
 #pragma unroll
         for (int j = 0; j < 4; j++) {
