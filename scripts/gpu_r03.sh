@@ -14,7 +14,7 @@ if [ -z "$NO_SMOKE" ]; then
   rc=$?; echo "smoke rc=$rc"; ok $rc || exit $rc
 fi
 if [ -z "$NO_TESTS" ]; then
-  timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -x -v --timeout 200 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+  FJSP_REPORT_DIR=gpurun_out/reports timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -x -v --timeout 200 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log; ok $rc || exit $rc
 fi
 [ -n "$NO_BENCH" ] && exit 0

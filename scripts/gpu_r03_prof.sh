@@ -21,4 +21,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c -T -d "$OUT/$c" -o $c --output-format csv -- python3 bench.py $A2C > "$OUT/$c.log" 2>&1
   rc=$?; echo "a2c $c rc=$rc"; bad $rc && exit $rc
 done
+# the gather exchange's learner: one GPU running GAE + the update over 8 x 4 096 envs x 256 steps
+timeout -k 10 300 python3 bench.py --workload a2c --envs 32768 --steps 3 --warmup 2 > "$OUT/a2c_32768envs.log" 2>&1
+rc=$?; echo "a2c 32768 rc=$rc"; tail -c 600 "$OUT/a2c_32768envs.log"
 exit 0
