@@ -377,3 +377,45 @@ def test_fused_policy_forced_tiles(M):
         learner.policy_fused(feats, masks, r, False, act, val)
         for a in range(2, 8):
             assert torch.equal(act[a, :64].long(), ((forced_envs + a) % 3)[:64]), a
+
+
+def test_a2c_config4_full_batch(M):
+    """BASELINE config 4 at its size: 4 096 envs x one 256-step batch (train.py --batch_size 256,
+    num_orders 25).  Sampled actions respect the masks, three envs replay on the oracle over the
+    whole batch (features, masks, rewards bit-exact), and the grouped update's gradients equal the
+    dense update's to 1e-4 relative per parameter tensor (the same sum of ~10^6 f32 terms per
+    weight in another order: f64 run sums over groups against f32 GEMM accumulation)."""
+    A, V, spec = M["A"], M["V"], M["spec"]
+    n, T = 4096, 256
+    env = V.FJSPVecEnv(n)
+    learner = A.VecMultiAgentA2C(env, batch_size=T, seed=12)
+    learner.reset(seeds=torch.arange(n) + 500, num_orders=25)
+    learner.collect()
+    b = learner._bufs
+    acts = b["actions"].long()
+    for a in range(8):
+        chosen = b["masks"][:T, A.MASK_OFFS[a]:A.MASK_OFFS[a] + A.N_ACTIONS[a], :].gather(1, acts[:, a:a + 1, :])
+        assert bool((chosen == 1).all()), a
+    idx = spec.a2c_feature_index()
+    feats, masks, rew = b["feats"].cpu().numpy(), b["masks"].cpu().numpy(), b["rewards"].cpu().numpy()
+    an = acts.cpu().numpy()
+    for e in (1, 1777, 4094):
+        o = O.OracleEnv()
+        r = o.reset(seed=500 + e, num_orders=25)
+        for t in range(T):
+            flat = np.concatenate([r["obs_i32"], r["obs_i8"], r["obs_f32"]]).astype(np.float32)
+            assert P.bits_equal(feats[t, :, e], flat[idx]), (e, t)
+            assert P.bits_equal(masks[t, :, e], r["masks"]), (e, t)
+            r = o.step(an[t, :, e])
+            assert P.bits_equal(rew[t, :, e], r["rewards"]), (e, t)
+            if r["term"] or r["trunc"]:
+                r = o.reset(num_orders=25)
+    ret, adv = learner.advantages()
+    grads = []
+    for dedup in (False, True):
+        actors, critic = A.init_networks(seed=13, device="cuda")
+        oa = torch.optim.Adam(actors.parameters(), lr=3e-4)
+        oc = torch.optim.Adam(critic.parameters(), lr=1e-3)
+        A.update_step(actors, critic, oa, oc, b["feats"][:T], b["masks"][:T], b["actions"], ret, adv, learner.gidx,
+                      learner.midx, 0.01, 0.5, dedup=dedup, grad_probe=lambda g: grads.append(g.cpu()))
+    P.assert_grads_close(grads[1], grads[0], rel=1e-4)
