@@ -227,16 +227,16 @@ class ActorStack(nn.Module):
         umax = g.first.shape[1]
         big = max(range(NA), key=lambda a: U[a])
         rest = [a for a in range(NA) if a != big]
-        u2 = max(U[a] for a in rest)
-        ub = U[big]
-        ridx = torch.tensor(rest, device=g.first.device)
+        u2 = bucket(max(U[a] for a in rest))
+        ub = bucket(U[big])
+        ridx = _index_tensor(tuple(rest), g.first.device)
         fr = g.first[ridx, :u2]
         if cols is None:
             xr = torch.gather(x[ridx], 2, fr[:, None, :].expand(NA - 1, x.shape[1], u2))
             xb = x[big][:, g.first[big, :ub]]
         else:
             xr = cols(ridx, fr)
-            xb = cols(torch.tensor([big], device=ridx.device), g.first[big:big + 1, :ub])[0]
+            xb = cols(_index_tensor((big,), ridx.device), g.first[big:big + 1, :ub])[0]
         h = torch.relu(torch.baddbmm(self.b1[ridx], self.W1[ridx], xr))
         h = torch.relu(torch.baddbmm(self.b2[ridx], self.W2[ridx], h))
         pr = torch.softmax(torch.baddbmm(self.b3[ridx], self.W3[ridx], h) + self.logit_pad[ridx], dim=1)
@@ -427,6 +427,21 @@ def group_keys(feats):
                       row_keys(feats.permute(1, 0, 2).reshape(GLOBAL_DIM, T * N))[None]])
 
 
+def bucket(u):
+    """A group count rounded up to a coarse bucket (1/16 to 1/8 of the count: ≤ 12.5 % more
+    columns, ~6 % on average), so that the update's shapes repeat from batch to batch and its
+    captured graph (VecMultiAgentA2C._update_graphed, one per shape signature) is replayed
+    instead of recaptured.  Padding groups own no samples: computed, never gathered, zero
+    gradient.  Eager and captured updates use the same buckets, so they agree bit for bit.
+    FJSP_GROUP_BUCKETS=0: exact counts."""
+    import os
+    u = int(u)
+    if os.environ.get("FJSP_GROUP_BUCKETS", "1") == "0" or u <= 64:
+        return u
+    step = 1 << max(5, u.bit_length() - 4)
+    return -(-u // step) * step
+
+
 class RowGroups:
     """Distinct values of each row of keys int64 [R, S] (one flat sort for all rows):
     U[r] groups in row r; inv [R, S] = each sample's group, first [R, Umax] = a representative
@@ -448,7 +463,7 @@ class RowGroups:
         new[:, 1:] = sk[:, 1:] != sk[:, :-1]
         seg = _prefix_sum(new.to(torch.int64)) - 1
         self.U = (seg[:, -1] + 1).tolist()                        # the one host sync
-        umax = max(self.U)
+        umax = bucket(max(self.U))
         idx = torch.where(new, seg, torch.full_like(seg, umax))
         pos = torch.arange(S, device=dev).expand(R, S)
         starts = torch.full((R, umax + 1), S, dtype=torch.int64, device=dev).scatter_(1, idx, pos)[:, :umax]
@@ -462,9 +477,10 @@ class RowGroups:
         """The groupings of rows lo..hi-1 alone (views; Umax = their own largest count)."""
         g = RowGroups.__new__(RowGroups)
         g.U = self.U[lo:hi]
-        um = max(g.U)
+        um = bucket(max(g.U))
         g.first, g.ends = self.first[lo:hi, :um], self.ends[lo:hi, :um]
-        g.inv, g.rep, g.perm = self.inv[lo:hi], self.rep[lo:hi], self.perm[lo:hi]
+        g.inv, g.perm = self.inv[lo:hi], self.perm[lo:hi]
+        g.rep = None if self.rep is None else self.rep[lo:hi]   # (the captured update keeps none)
         return g
 
     def gather(self, y):
@@ -563,8 +579,7 @@ class _ActorHead(torch.autograd.Function):
         for a in range(NA):
             o, k = MASK_OFFS[a], N_ACTIONS[a]
             torch.gather(grad[o:o + k], 1, g.perm[a].expand(k, S), out=srt[o:o + k])
-        row_agent = torch.repeat_interleave(torch.arange(NA, device=grad.device),
-                                            torch.tensor(N_ACTIONS, device=grad.device))
+        row_agent = _index_tensor(tuple(a for a in range(NA) for _ in range(N_ACTIONS[a])), grad.device)
         srt.mul_(gl.to(grad.dtype)[row_agent, None])
         cs = _prefix_sum(srt.double())
         ce = torch.gather(cs, 1, (g.ends - 1)[row_agent])
@@ -575,6 +590,25 @@ class _ActorHead(torch.autograd.Function):
 
 
 _VALID_ROWS = {}
+_INDEX = {}
+
+
+def _index_tensor(values, device):
+    """A small int64 index tensor on `device`, built once per (values, device): a host-to-device
+    copy must not happen inside a graph capture (the captured update, VecMultiAgentA2C)."""
+    key = (values, torch.device(device))
+    if key not in _INDEX:
+        _INDEX[key] = torch.tensor(values, dtype=torch.int64, device=device)
+    return _INDEX[key]
+
+
+def warm_index_tensors(device):
+    """Every index tensor the grouped update may ask for (each choice of the largest actor)."""
+    for big in range(NA):
+        _index_tensor(tuple(a for a in range(NA) if a != big), device)
+        _index_tensor((big,), device)
+    _index_tensor(tuple(a for a in range(NA) for _ in range(N_ACTIONS[a])), device)
+    _valid_rows(device)
 
 
 def _valid_rows(device):
@@ -616,14 +650,18 @@ class A2CLosses:
 
     @staticmethod
     def compute(actors, critic, feats, masks, actions, returns, adv, gidx, midx, entropy_coef,
-                adv_mean, adv_std, count, dedup=False):
+                adv_mean, adv_std, count, dedup=False, groups=None):
+        """groups = (ga, gc): a verified grouping computed by the caller (the captured update);
+        else dedup groups here (keys, sort, check: two host synchronisations)."""
         f3 = feats if feats.dim() == 3 else feats[None]
         T, _, n = f3.shape
         S = T * n
         gt = f3.permute(1, 0, 2).reshape(GLOBAL_DIM, S)                # [38, S]
-        x = None if dedup and feats.is_cuda else actor_inputs(feats, gidx)   # [8, 13, S]
+        x = None if (dedup or groups is not None) and feats.is_cuda else actor_inputs(feats, gidx)   # [8, 13, S]
         ga = gc = None
-        if dedup:
+        if groups is not None:
+            ga, gc = groups
+        elif dedup:
             f3 = f3.contiguous()
             gr = RowGroups(group_keys(f3))                          # 8 actor rows + the critic's
             ga, gc = gr.rows(0, NA), gr.rows(NA, NA + 1)
@@ -728,14 +766,11 @@ def flat_grads(actors, critic):
                       for p in list(actors.parameters()) + list(critic.parameters())])
 
 
-def update_step(actors, critic, optim_actor, optim_critic, feats, masks, actions, ret, adv, gidx, midx,
-                entropy_coef, max_grad_norm, group=None, dedup=False, grad_probe=None):
-    """One _update (a2c.py:647-703) on a [T, ., N] batch (this rank's shard of it).
-
-    feats f32 [T, 38, N], masks int8 [T, 29, N], actions u8 [T, 8, N], ret / adv f64 [T, 8, N].
-    grad_probe(flat f32 grads): called with the reduced gradients before clipping and Adam
-    (tests compare them across exchanges).
-    Returns (actor losses per agent, critic loss) as Python floats (the loss histories)."""
+def update_core(actors, critic, optim_actor, optim_critic, feats, masks, actions, ret, adv, gidx, midx,
+                entropy_coef, max_grad_norm, group=None, dedup=False, grad_probe=None, groups=None):
+    """update_step without the final host copies: returns the (all-reduced) actor losses [8] and
+    critic loss [1] as device tensors.  With groups (a verified grouping) and no group / probe it
+    issues no host synchronisation, so a graph can capture it."""
     from . import distributed as D
     T, _, N = feats.shape
     S = T * N
@@ -746,7 +781,7 @@ def update_step(actors, critic, optim_actor, optim_critic, feats, masks, actions
     optim_actor.zero_grad(set_to_none=True)
     optim_critic.zero_grad(set_to_none=True)
     actor_losses, critic_loss = A2CLosses.compute(actors, critic, feats, masks, acts, ret32, adv32, gidx, midx,
-                                                  entropy_coef, mean, std, count, dedup)
+                                                  entropy_coef, mean, std, count, dedup, groups)
     (actor_losses.sum() + critic_loss).backward()
     D.allreduce_grads(list(actors.parameters()) + list(critic.parameters()), group)
     if grad_probe is not None:
@@ -757,6 +792,19 @@ def update_step(actors, critic, optim_actor, optim_critic, feats, masks, actions
     optim_critic.step()
     al = D.allreduce_sum(actor_losses.detach(), group)
     cl = D.allreduce_sum(critic_loss.detach().view(1), group)
+    return al, cl
+
+
+def update_step(actors, critic, optim_actor, optim_critic, feats, masks, actions, ret, adv, gidx, midx,
+                entropy_coef, max_grad_norm, group=None, dedup=False, grad_probe=None):
+    """One _update (a2c.py:647-703) on a [T, ., N] batch (this rank's shard of it).
+
+    feats f32 [T, 38, N], masks int8 [T, 29, N], actions u8 [T, 8, N], ret / adv f64 [T, 8, N].
+    grad_probe(flat f32 grads): called with the reduced gradients before clipping and Adam
+    (tests compare them across exchanges).
+    Returns (actor losses per agent, critic loss) as Python floats (the loss histories)."""
+    al, cl = update_core(actors, critic, optim_actor, optim_critic, feats, masks, actions, ret, adv, gidx, midx,
+                         entropy_coef, max_grad_norm, group, dedup, grad_probe)
     return al.cpu().tolist(), float(cl.cpu()[0])
 
 
@@ -806,8 +854,9 @@ class VecMultiAgentA2C:
         self.global_obs_dim = GLOBAL_DIM
         self.actors, self.critic = init_networks(seed, hidden, self.device)
         fused = self.device.type == "cuda"      # one multi-tensor kernel per step (same Adam math)
-        self.optim_actor = torch.optim.Adam(self.actors.parameters(), lr=lr_actor, fused=fused)
-        self.optim_critic = torch.optim.Adam(self.critic.parameters(), lr=lr_critic, fused=fused)
+        # capturable: the step counters live on the device, so the update can be graph-captured
+        self.optim_actor = torch.optim.Adam(self.actors.parameters(), lr=lr_actor, fused=fused, capturable=fused)
+        self.optim_critic = torch.optim.Adam(self.critic.parameters(), lr=lr_critic, fused=fused, capturable=fused)
         self.gidx = gather_index(self.device)
         self.midx = mask_index(self.device)
         self.actor_loss_history = {a: [] for a in AGENTS}
@@ -831,6 +880,14 @@ class VecMultiAgentA2C:
         self._graph_det = None
         self._eager_batches = 0
         self.gae_fn = batch_advantages     # finish_trajectory over a batch (tests may inject a CPU stand-in)
+        # the update after the grouping as hipGraphs, one per shape signature (_update_graphed):
+        # bit-identical to the eager update, but measured no faster at 4 096 envs (the update is
+        # GPU-bound: 9.7 ms replayed against 9.0-9.6 eager; every new signature costs a capture,
+        # scripts/ab_update.py), so opt-in
+        self.graph_update = False
+        self._ugraphs = {}
+        self._upool = None
+        self._eager_updates = 0
         self.grad_probe = None             # grad_probe(flat reduced grads) before clip / Adam (tests)
         self.exchange_timing = None        # dict of synchronised stage times (ms) when not None (bench)
 
@@ -1013,8 +1070,12 @@ class VecMultiAgentA2C:
         optimisers stay at their initial state), so a run that later switches to "allreduce"
         or resumes an optimiser must take it from the learner rank."""
         from . import distributed as D
+        res = None
         if self.exchange == "gather" and D.active(self.group):
             al, cl = self._update_gathered()
+        elif (ret is None and self.graph_update and self.grad_probe is None and not D.active(self.group)
+              and self._eager_updates >= 1 and (res := self._update_graphed()) is not None):
+            al, cl = res
         else:
             t0 = self._start()
             if ret is None:
@@ -1024,12 +1085,86 @@ class VecMultiAgentA2C:
             al, cl = update_step(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
                                  b["masks"][:T], b["actions"], ret, adv, self.gidx, self.midx, self.entropy_coef,
                                  self.max_grad_norm, self.group, self.dedup, self.grad_probe)
+            self._eager_updates += 1
             self._mark("learn", t0)
         for a, x in zip(AGENTS, al):
             self.actor_loss_history[a].append(x)
         self.critic_loss_history.append(cl)
-        self.repack()
+        if res is None:
+            self.repack()                  # the captured update repacks inside its graph
         return al, cl
+
+    def _update_graphed(self):
+        """The update with everything after the grouping replayed from a hipGraph.
+
+        Eager: GAE, the grouping keys, the sort and the collision check (two host
+        synchronisations: the group counts set the shapes, a collision falls back to the dense
+        update).  The rest — advantage statistics, the networks on their distinct inputs, the
+        loss head, backward, per-agent clipping, Adam, the policy kernel's weight repack — has
+        fixed shapes for a given signature of (bucketed) group counts, so it is captured once per
+        signature and replayed on static copies of the batch's grouping (~430 launches become
+        one; the host-side gaps between them were ~2 ms per update).  Returns (actor losses,
+        critic loss) or None when the caller must run the eager update."""
+        b = self._bufs
+        T = self.batch_size
+        t0 = self._start()
+        ret, adv = self.advantages()
+        f3 = b["feats"][:T]
+        gr = RowGroups(group_keys(f3))
+        ga, gc = gr.rows(0, NA), gr.rows(NA, NA + 1)
+        if not group_verify(f3, ga, gc):
+            return None                                             # a hash collision: dense, eager
+        U = gr.U
+        big = max(range(NA), key=lambda a: U[a])
+        sig = (gr.first.shape[1], ga.first.shape[1], gc.first.shape[1], big, bucket(U[big]),
+               bucket(max(U[a] for a in range(NA) if a != big)))
+        e = self._ugraphs.pop(sig, None)
+        if e is None:
+            e = self._capture_update(gr, ret, adv)
+            while len(self._ugraphs) >= 6:                          # least recently used out
+                self._ugraphs.pop(next(iter(self._ugraphs)))
+        self._ugraphs[sig] = e                                      # most recently used last
+        if e.get("fresh"):
+            e["fresh"] = False
+        else:
+            for k in ("first", "ends", "inv", "perm"):
+                getattr(e["gr"], k).copy_(getattr(gr, k))
+            self._st_ret.copy_(ret)
+            self._st_adv.copy_(adv)
+        e["graph"].replay()
+        self._mark("learn", t0)
+        return e["al"].cpu().tolist(), float(e["cl"].cpu()[0])
+
+    def _capture_update(self, gr, ret, adv):
+        """Capture the update after the grouping for the shapes of grouping gr (update_graph)."""
+        from . import distributed as D
+        T = self.batch_size
+        b = self._bufs
+        if self._upool is None:
+            self._upool = torch.cuda.graph_pool_handle()
+            self._st_ret = torch.empty_like(ret)
+            self._st_adv = torch.empty_like(adv)
+            warm_index_tensors(self.device)
+        self._st_ret.copy_(ret)
+        self._st_adv.copy_(adv)
+        sgr = RowGroups.__new__(RowGroups)
+        sgr.U = list(gr.U)
+        for k in ("first", "ends", "inv", "perm"):
+            setattr(sgr, k, getattr(gr, k).clone())
+        sgr.rep = None
+        groups = (sgr.rows(0, NA), sgr.rows(NA, NA + 1))
+        al_st = torch.zeros(NA, dtype=torch.float32, device=self.device)
+        cl_st = torch.zeros(1, dtype=torch.float32, device=self.device)
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(g, pool=self._upool):
+            al, cl = update_core(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
+                                 b["masks"][:T], b["actions"], self._st_ret, self._st_adv, self.gidx, self.midx,
+                                 self.entropy_coef, self.max_grad_norm, D.LOCAL, True, None, groups)
+            al_st.copy_(al)
+            cl_st.copy_(cl)
+            self.repack()
+        return {"graph": g, "gr": sgr, "al": al_st, "cl": cl_st, "fresh": True}
 
     def _update_gathered(self):
         """Experience gather into the learner (rank 0 of the group): the reference's

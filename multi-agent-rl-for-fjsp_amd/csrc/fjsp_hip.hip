@@ -75,7 +75,9 @@ __device__ __forceinline__ void spin_until(uint32_t* flag, uint32_t v, uint32_t*
                 break;
             }
         }
+#ifndef FJSP_X_SPIN_NOSLEEP   // diagnostic build: poll without sleeping
         __builtin_amdgcn_s_sleep(1);
+#endif
     }
 }
 

@@ -419,3 +419,29 @@ def test_a2c_config4_full_batch(M):
         A.update_step(actors, critic, oa, oc, b["feats"][:T], b["masks"][:T], b["actions"], ret, adv, learner.gidx,
                       learner.midx, 0.01, 0.5, dedup=dedup, grad_probe=lambda g: grads.append(g.cpu()))
     P.assert_grads_close(grads[1], grads[0], rel=1e-4)
+
+
+def test_graphed_update_equals_eager_update(M):
+    """The update after the grouping replayed from hipGraphs (one per shape signature, static
+    copies of each batch's grouping) computes exactly what the eager update computes: the same
+    loss histories and parameters, bit for bit, over batches that capture new signatures and
+    batches that replay captured ones."""
+    A, V = M["A"], M["V"]
+    n, T, nb = 512, 48, 7
+    runs = []
+    for graphed in (False, True):
+        L = A.VecMultiAgentA2C(V.FJSPVecEnv(n), batch_size=T, seed=14)
+        L.graph_update = graphed
+        L.reset(seeds=torch.arange(n), num_orders=25)
+        for _ in range(nb):
+            L.collect()
+            L.update()
+            L.roll_over()
+        torch.cuda.synchronize()
+        params = torch.cat([p.detach().reshape(-1) for p in list(L.actors.parameters()) + list(L.critic.parameters())])
+        runs.append((L.critic_loss_history, [L.actor_loss_history[a] for a in M["spec"].AGENTS], params.cpu(),
+                     len(L._ugraphs)))
+    assert runs[0][3] == 0 and 1 <= runs[1][3] <= nb - 1
+    assert runs[1][0] == runs[0][0]
+    assert runs[1][1] == runs[0][1]
+    assert torch.equal(runs[1][2], runs[0][2])
