@@ -257,7 +257,7 @@ def main():
             out = {"metric": "env-steps/sec of the A2C training loop (BASELINE configs 4/5)",
                    "value": res["value"], "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
                    "warmup": args.warmup, "ms_per_step": res["ms_per_batch"], "higher_is_better": True,
-                   "scaling": "weak", "vs_baseline": None, "dtype": "fp32 (networks) + int32/f64 (env)",
+                   "scaling": "weak", "vs_baseline": None, "dtype": "f32 (networks; k_policy: f32 operands as 3 bf16 planes on the MFMA, f32 accumulate) + int32/f64 (env)",
                    "data": "synthetic: envs seeded by global id, " + (
                        "random-init networks (torch.manual_seed(0))" if args.init == "random" else
                        "networks from the reference's trained checkpoints/model.pt"),

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define FJSP_ABI_VERSION 4
+#define FJSP_ABI_VERSION 5
 
 #define FJSP_NUM_AGENTS 8      /* pickup, agv, small, big, pkg_blue_1, pkg_blue_2, pkg_red, pkg_green */
 #define FJSP_OBS_I32 20        /* pickup 7 + agv 13 (position = 2) int32 observation fields */
@@ -237,13 +237,15 @@ int fjsp_a2c_layout(int32_t* out);
 int64_t fjsp_snapshot_bytes(const fjsp_handle* h);
 
 /* ---- fused A2C policy step (a2c.py:168-252 predict for all agents and envs; networks.py) ----
- * feats f32 [38][N] (fjsp_out.feats layout), masks int8 [29][N]; weights pre-packed, every
- * K >= 16 matrix W [R][K] in MFMA order P(W) = [R/32][K/8][64 lanes][4], element (t, q, l, j) =
- * W[32 t + (l & 31)][2 (4 q + j) + (l >> 5)]:
+ * feats f32 [38][N] (fjsp_out.feats layout), masks int8 [29][N]; weights pre-split and pre-packed
+ * (ABI 5): every K >= 16 matrix W [R][K] as three bf16 planes hi = bf16(W), mid = bf16(W - hi),
+ * lo = bf16(W - hi - mid) (round to nearest even) in MFMA order P(W) = [R/32][K/16][3][64 lanes][8]
+ * bf16, element (t, kb, p, l, j) = plane p of W[32 t + (l & 31)][16 kb + 8 (l >> 5) + j]
+ * (3 R K / 2 floats of the buffer); biases and the VALU layers as f32:
  *   actor_w: 8 agents x FJSP_POLICY_ACTOR_FLOATS: P(W1 [256][16], inputs zero-padded) | b1 [256] |
  *            P(W2 [256][256]) | b2 [256] | W3 [8][256] (rows >= n_a zero) | b3 [16]
- *   critic_w: P(W1 [256][40]) | b1 [256] | P(W2 [256][256]) | b2 [256] | P(W3 [128][256]) |
- *            b3 [128] | W4 [128] | b4 [16]
+ *   critic_w: P(W1 [256][48], inputs zero-padded) | b1 [256] | P(W2 [256][256]) | b2 [256] |
+ *            P(W3 [128][256]) | b3 [128] | W4 [128] | b4 [16]
  * Out: actions u8 [8][N] (argmax if deterministic, else an inverse-CDF draw from the masked
  * distribution keyed by (*seed, env_gid0 + env, step, agent) — the env's global id, so the
  * shards of a multi-GPU job draw independent streams; `seed` is a DEVICE pointer so a captured
@@ -252,9 +254,9 @@ int64_t fjsp_snapshot_bytes(const fjsp_handle* h);
  * actor_w and seed may then be NULL; e.g. the batch-end bootstrap V(s_T), a2c.py:321-332);
  * values == NULL: the actors only (critic_w may be NULL).  Stream-ordered on `stream`. */
 #define FJSP_POLICY_ACTOR_DPAD 16
-#define FJSP_POLICY_CRITIC_DPAD 40
-#define FJSP_POLICY_ACTOR_FLOATS (256 * 16 + 256 + 256 * 256 + 256 + 8 * 256 + 16)
-#define FJSP_POLICY_CRITIC_FLOATS (256 * 40 + 256 + 256 * 256 + 256 + 128 * 256 + 128 + 128 + 16)
+#define FJSP_POLICY_CRITIC_DPAD 48
+#define FJSP_POLICY_ACTOR_FLOATS (3 * 256 * 16 / 2 + 256 + 3 * 256 * 256 / 2 + 256 + 8 * 256 + 16)
+#define FJSP_POLICY_CRITIC_FLOATS (3 * 256 * 48 / 2 + 256 + 3 * 256 * 256 / 2 + 256 + 3 * 128 * 256 / 2 + 128 + 128 + 16)
 int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const float* actor_w, const float* critic_w,
                     const uint64_t* seed, uint32_t env_gid0, uint32_t step, int32_t deterministic, uint8_t* actions,
                     float* values,

@@ -66,9 +66,10 @@ EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_c
            "fjsp_snapshot_bytes", "fjsp_snapshot", "fjsp_restore", "fjsp_last_kernel", "fjsp_a2c_policy",
            "fjsp_a2c_group_keys", "fjsp_a2c_group_verify", "fjsp_a2c_actor_head",
            "fjsp_a2c_relu_bias_grad", "fjsp_a2c_value_head_grad", "fjsp_faults"]
-POLICY_ACTOR_FLOATS = 256 * 16 + 256 + 256 * 256 + 256 + 8 * 256 + 16
-POLICY_CRITIC_FLOATS = 256 * 40 + 256 + 256 * 256 + 256 + 128 * 256 + 128 + 128 + 16
-ABI_VERSION = 4
+POLICY_ACTOR_DPAD, POLICY_CRITIC_DPAD = 16, 48
+POLICY_ACTOR_FLOATS = 3 * 256 * 16 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 8 * 256 + 16
+POLICY_CRITIC_FLOATS = 3 * 256 * 48 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 3 * 128 * 256 // 2 + 128 + 128 + 16
+ABI_VERSION = 5
 
 _lib = None
 

@@ -715,28 +715,42 @@ def clip_per_agent_(actors, max_norm):
 
 
 # ---------------------------------------------------------------- fused policy kernel weights
+def split_bf16x3(W):
+    """f32 -> (hi, mid, lo) bf16 with W = hi + mid + lo up to 2^-24 |W| (each difference is exact
+    in f32; round to nearest even, as the kernel splits its activations)."""
+    W = W.float()
+    hi = W.to(torch.bfloat16)
+    r = W - hi.float()
+    mid = r.to(torch.bfloat16)
+    return hi, mid, (r - mid.float()).to(torch.bfloat16)
+
+
 def pack_mfma(W):
-    """[..., R, K] -> [..., R/32, K/8, 64, 4] with (t, q, l, j) = W[32 t + (l & 31)][2 (4 q + j) + (l >> 5)]:
-    the A-operand lane order of v_mfma_f32_32x32x2_f32 in groups of 4 k-steps, one float4
-    load per lane per group (csrc/fjsp_policy.hip)."""
+    """[..., R, K] f32 -> [..., R/32, K/16, 3, 64, 4] f32 words holding [..., 3, 64, 8] bf16 with
+    (t, kb, p, l, j) = plane p of W[32 t + (l & 31)][16 kb + 8 (l >> 5) + j]: the A-operand lane order
+    of v_mfma_f32_32x32x16_bf16, one 16-byte load per lane per plane and 16-deep block, the three
+    planes of split_bf16x3 (csrc/fjsp_policy.hip, include/fjsp.h)."""
     *lead, R, K = W.shape
     nl = len(lead)
-    W = W.reshape(*lead, R // 32, 32, K // 8, 4, 2)                  # t, i, q, j, kk
-    W = W.permute(*range(nl), nl, nl + 2, nl + 4, nl + 1, nl + 3)     # t, q, kk, i, j
-    return W.reshape(*lead, R // 32, K // 8, 64, 4)
+    Pl = torch.stack(split_bf16x3(W), dim=nl)                                # [..., 3, R, K]
+    Pl = Pl.reshape(*lead, 3, R // 32, 32, K // 16, 2, 8)                     # p, t, i, kb, hh, j
+    Pl = Pl.permute(*range(nl), nl + 1, nl + 3, nl, nl + 4, nl + 2, nl + 5)   # t, kb, p, hh, i, j
+    return Pl.contiguous().view(torch.float32).reshape(*lead, R // 32, K // 16, 3, 64, 4)
 
 
 @torch.no_grad()
 def pack_policy_weights(actors, critic, out_actor=None, out_critic=None):
-    """Actor stack + critic -> the flat f32 buffers fjsp_a2c_policy reads (include/fjsp.h)."""
+    """Actor stack + critic -> the flat buffers fjsp_a2c_policy reads (include/fjsp.h): the MFMA
+    layers' weights as bf16 planes in lane order, biases and the VALU layers as f32."""
     dev = actors.W1.device
     z = lambda *s: torch.zeros(*s, device=dev)  # noqa: E731
-    w1 = torch.cat([actors.W1, z(NA, actors.hidden, 16 - DPAD)], dim=2)            # [8, 256, 16]
-    b3 = torch.cat([actors.b3[:, :, 0], z(NA, 8)], dim=1)                             # [8, 16]
+    w1 = torch.cat([actors.W1, z(NA, actors.hidden, nat.POLICY_ACTOR_DPAD - DPAD)], dim=2)   # [8, 256, 16]
+    b3 = torch.cat([actors.b3[:, :, 0], z(NA, 8)], dim=1)                                     # [8, 16]
     a = torch.cat([pack_mfma(w1).reshape(NA, -1), actors.b1.reshape(NA, -1), pack_mfma(actors.W2).reshape(NA, -1),
                    actors.b2.reshape(NA, -1), actors.W3.reshape(NA, -1), b3], dim=1).reshape(-1)
     n = critic.net
-    c = torch.cat([pack_mfma(torch.cat([n[0].weight, z(256, 2)], dim=1)).reshape(-1), n[0].bias,
+    cw1 = torch.cat([n[0].weight, z(256, nat.POLICY_CRITIC_DPAD - n[0].weight.shape[1])], dim=1)   # [256, 48]
+    c = torch.cat([pack_mfma(cw1).reshape(-1), n[0].bias,
                    pack_mfma(n[2].weight).reshape(-1), n[2].bias, pack_mfma(n[4].weight).reshape(-1), n[4].bias,
                    n[6].weight.reshape(-1), torch.cat([n[6].bias, z(15)])])
     assert a.numel() == NA * nat.POLICY_ACTOR_FLOATS and c.numel() == nat.POLICY_CRITIC_FLOATS

@@ -6,41 +6,79 @@
 // action draw (inverse CDF over the masked probabilities, or argmax) and the centralised
 // critic (networks.CentralizedCriticNetwork: 38 -> 256 -> 256 -> 128 -> 1).
 //
-// Grid: blockIdx.y = role (0 critic, 1..8 actor of agent y - 1), blockIdx.x = tile of 64 envs;
-// 512 threads = 8 wavefronts.  The hidden activations never leave LDS:
-//   x   [40][TILE]  inputs of the tile (feature rows of the kernel-written [38][N] slab)
-//   h   [256][TILE] layer 1, then layer 2, then the critic's layer 3 (in place: results stay in
-//                   registers across a barrier), so two workgroups fit a CU (74 KB of LDS each)
-// Every layer with K >= 16 runs on v_mfma_f32_32x32x2_f32 (exact f32 fma chains): each wave
-// owns 32 output rows x the tile's 64 envs = two 32 x 32 tiles sharing one weight fragment (the
-// critic's 128-row layer 3: waves 0..3).
-// The actor's 256 -> n_a logits and the critic's 128 -> 1 value are VALU dot products.
-// MFMA A operands (weights) are pre-packed on the host per (row tile, k-step) in lane order
-// (fjsp_pack_policy_weights layout below), so each k-step's A fragment is one coalesced
-// 256-byte load; B fragments (activations) are conflict-free LDS reads.
-// f32 arithmetic throughout (the reference networks are f32); summation order differs from
-// PyTorch's GEMMs only by rounding (tests: 1e-5).
+// Grid (1-D, 512 threads = 8 wavefronts per workgroup, two workgroups per CU: 70 KB of LDS):
+//   blocks [0, nc)            the critic on tiles of 32 envs (values wanted)
+//   blocks [nc, nc + 8 na)    actor (b - nc) / na on tiles of 64 envs (actions wanted)
+// The hidden activations never leave LDS, as bf16 planes (below) [3][env][k]:
+//   actor:  x [3][64][16+8]; h1 in two K halves [3][64][128+8] (rows 0..127, then 128..255:
+//           layer 2 is summed over the two halves, so one half-size buffer serves)
+//   critic: x [3][32][48+8]; h1, then h2 [3][32][256+8] (in place across a barrier)
+// Every layer with K >= 16 runs on v_mfma_f32_32x32x16_bf16 with f32 operands split into three
+// bf16 planes (six plane products per 16-deep block, below).  Actor: each wave owns 32 rows of
+// layer 2 x the tile's 64 envs (two 32 x 32 tiles sharing each weight fragment); layer 1 one
+// 32 x 32 tile per wave and half.  Critic: one 32-row tile per wave (layer 3: waves 0..3).  The
+// actor's 256 -> n_a logits and the critic's 128 -> 1 value are f32 VALU dot products straight
+// from the accumulators.  Weights are pre-split and pre-packed per (row tile, 16-deep block,
+// plane) in lane order (a2c_vec.pack_policy_weights, include/fjsp.h), so each A fragment is one
+// coalesced 1 KB load per wave; B fragments (activations) are 16-byte conflict-free LDS reads.
+// Numerics: each product carries <= ~2^-22 relative error (f32's own rounding is 2^-24 per
+// operation), sums in f32; the outputs equal PyTorch's f32 policy within 1e-5 (tests) and the
+// reference's greedy actions on its trained policy.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/fjsp.h"
+#include "fjsp_stamps.h"
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+// diagnostic builds only (-DFJSP_STAMPS, scripts/diag_policy_stamps.py): per workgroup, wave 0's
+// phase clock stamps; slots 0 / 10 s_memrealtime at entry / exit, 1..9 s_memtime at entry,
+// forced check, inputs, layer 1, h1, layer 2, h2, critic layer 3 or actor logits, exit; 11 HW_ID,
+// 12 XCC_ID, 13 role | forced << 8
+FJSP_DIAG(__device__ unsigned long long g_pstamps[2048 * 16];)
+#ifdef FJSP_STAMPS
+#define PST(i, v)                                                                                \
+    do {                                                                                         \
+        if (tid == 0) g_pstamps[(size_t)blockIdx.x * 16 + (i)] = (unsigned long long)(v);        \
+    } while (0)
+#else
+#define PST(i, v) ((void)0)
+#endif
 
-// 64 envs per workgroup on 8 waves: each weight fragment loaded from L2 feeds two MFMAs (one
-// per 32-env column tile), half the weight traffic of 32-env tiles at the same waves per CU
-// (two 74 KB workgroups = 16 waves).  The weight loads, one 256-byte A fragment per MFMA with
-// 32-env tiles, are what bounds this kernel: 4 SIMDs x 256 B per 16-cycle MFMA = the CU's
-// 64 B/clk vector-memory path.
-constexpr int TILE = 64;              // envs per workgroup
-constexpr int NCOL = TILE / 32;       // 32-column MFMA tiles per row tile
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int TA = 64;                // envs per actor workgroup (two 32-env column tiles)
+constexpr int TC = 32;                // envs per critic workgroup
 constexpr int NWAVE = 8;
 constexpr int NTHR = 64 * NWAVE;
 constexpr int HID = 256;
 constexpr int NAG = 8;
-constexpr int KS2 = HID / 2;   // k-steps of 2 for a 256-wide contraction
+constexpr int A_DPAD = FJSP_POLICY_ACTOR_DPAD, C_DPAD = FJSP_POLICY_CRITIC_DPAD;
+static_assert(A_DPAD % 16 == 0 && C_DPAD % 16 == 0, "inputs come in 16-deep MFMA blocks");
+
+// f32 products on the bf16 matrix cores.  Every f32 operand x is carried as three bf16 planes,
+// hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid) (both differences exact in f32), so
+// x = hi + mid + lo up to 2^-24 |x|; a . b is the sum of the six plane products of order >= 2^-16
+// (hi.hi, hi.mid, mid.hi, mid.mid, hi.lo, lo.hi), the three dropped ones are <= 2^-23 |a b|
+// together (with the split residuals <= ~2^-22 |a b|, the order of f32 rounding), and every
+// product of two bf16 is exact in the f32 accumulator.  Cost: one 16-deep block of a 32 x 32 tile
+// is six v_mfma_f32_32x32x16_bf16 (32 cycles each) against eight v_mfma_f32_32x32x2_f32 (64
+// cycles each), 192 against 512 cycles.  Weights are split once per update on the host side
+// (a2c_vec.pack_policy_weights), activations when they are written to LDS.
+constexpr int NP = 3;                              // bf16 planes per f32 value
+// bf16 row strides of the activation planes [env][k] (k + 8: the 16-byte fragment reads of 16
+// consecutive lanes hit distinct banks); plane sizes
+constexpr int XSA = A_DPAD + 8, XSC = C_DPAD + 8, HSA = HID / 2 + 8, HSC = HID + 8;
+constexpr int XPA = TA * XSA, XPC = TC * XSC, HPA = TA * HSA, HPC = TC * HSC;
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int X_BYTES = cmax(NP * XPA, NP * XPC) * 2;
+constexpr int H_BYTES = cmax(cmax(NP * HPA, NP * HPC) * 2, NWAVE * 8 * TA * 4);   // also the logit partials
+constexpr int W3_BYTES = 8 * HID * 4;
+constexpr int LDS_BYTES = X_BYTES + H_BYTES + W3_BYTES;
+static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
 
 __constant__ int c_obs_off[NAG] = {0, 7, 20, 23, 26, 29, 32, 35};
 __constant__ int c_obs_dim[NAG] = {7, 13, 3, 3, 3, 3, 3, 3};
@@ -54,198 +92,387 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t z) {
     return z;
 }
 
-// MFMA A operands are packed per row tile t in groups of 4 k-steps: element (t, q, l, j) =
-// W[32 t + (l & 31)][2 (4 q + j) + (l >> 5)], so one 16-byte load per lane fetches the A
-// fragments of 4 consecutive k-steps (a coalesced 1 KB per wave instruction).
-// acc[i][j] += W(row tile rt0 + i) . act(col tile j); act = LDS [K][TILE] (rows = k), KS = K / 2.
-template <int NT, int KS>
-__device__ __forceinline__ void mfma_rows(const float* __restrict__ wp, int rt0, const float* act, int lane,
-                                          f32x16 acc[NT][NCOL]) {
-    static_assert(KS % 4 == 0, "k-steps come in groups of 4");
-    constexpr int NQ = KS / 4;
-    const float4* a[NT];
+__device__ __forceinline__ void split3(float v, __bf16& hi, __bf16& mid, __bf16& lo) {
+    hi = (__bf16)v;
+    const float r = v - (float)hi;
+    mid = (__bf16)r;
+    lo = (__bf16)(r - (float)mid);
+}
+
+// acc += a . b over one 16-deep block, small products first
+__device__ __forceinline__ f32x16 mfma6(const bf16x8 a[NP], const bf16x8 b[NP], f32x16 acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+
+// Weight blocks of one row tile in flight: a register ring of D + 1 blocks x NP planes.
+constexpr int WPD = 1;
+template <int KB>
+struct WRing {
+    static constexpr int D = KB < WPD ? KB : WPD;
+    bf16x8 w[D + 1][NP];
+};
+// W packed [row tiles][KBT][NP][64 lanes][8] bf16, element (t, kb, p, l, j) = plane p of
+// W[32 t + (l & 31)][16 kb + 8 (l >> 5) + j] (the A-operand lane order of the 32x32x16 MFMA: one
+// coalesced 1 KB load per plane and block).  Blocks kb0 .. kb0 + KB - 1 of row tile rt:
+template <int KB, int KBT>
+__device__ __forceinline__ const bf16x8* wblocks(const bf16x8* __restrict__ wp, int rt, int kb0, int lane) {
+    return wp + ((size_t)rt * KBT + kb0) * NP * 64 + lane;
+}
+// Issue the ring's first D blocks, ahead of the barrier before the layer.
+template <int KB>
+__device__ __forceinline__ void wring_start(WRing<KB>& R, const bf16x8* __restrict__ a) {
 #pragma unroll
-    for (int i = 0; i < NT; i++) a[i] = reinterpret_cast<const float4*>(wp) + (size_t)(rt0 + i) * NQ * 64 + lane;
-    const int kr = lane >> 5, cl = lane & 31;
-    constexpr int PF = NQ < 2 ? NQ : 2;   // groups in flight (3, 4, 6 in a register ring: no faster, r03)
-    float4 buf[PF][NT];
+    for (int q = 0; q < WRing<KB>::D; q++)
 #pragma unroll
-    for (int p = 0; p < PF; p++)
+        for (int p = 0; p < NP; p++) R.w[q][p] = a[(q * NP + p) * 64];
+}
+
+// acc[c] += W(blocks at a) . act(env columns c0 + 32 c .. + 31), c < NC, over KB 16-deep blocks;
+// act = LDS planes [NP][env][ST] (plane size PL), k contiguous from the first block (lane l
+// reads its 8 k of column l & 31 as one 16-byte B fragment).  R holds blocks 0..D-1
+// (wring_start).  Fully unrolled so that the rings are registers without copies (a rotating copy
+// made the compiler wait for each weight load right after issuing it): weight blocks D ahead,
+// B fragments one MFMA group ahead, each pinned by a scheduling barrier (the scheduler otherwise
+// sinks the loads to their first use).
+template <int KB, int ST, int PL, int NC>
+__device__ __forceinline__ void mfma_rows(WRing<KB>& R, const bf16x8* __restrict__ a, const __bf16* act, int c0, int lane,
+                                          f32x16 acc[NC]) {
+    constexpr int D = WRing<KB>::D;
+    const __bf16* bq = act + (c0 + (lane & 31)) * ST + 8 * (lane >> 5);
+    bf16x8 fb[2][NP];
 #pragma unroll
-        for (int i = 0; i < NT; i++) buf[p][i] = a[i][p * 64];
-#pragma unroll 2
-    for (int q = 0; q < NQ; q++) {
-        float4 cur[NT];
+    for (int p = 0; p < NP; p++) fb[0][p] = *reinterpret_cast<const bf16x8*>(bq + p * PL);
 #pragma unroll
-        for (int i = 0; i < NT; i++) cur[i] = buf[q % PF][i];
-        if (q + PF < NQ) {
+    for (int kb = 0; kb < KB; kb++) {
+        if (kb + D < KB) {
 #pragma unroll
-            for (int i = 0; i < NT; i++) buf[q % PF][i] = a[i][(q + PF) * 64];
+            for (int p = 0; p < NP; p++) R.w[(kb + D) % (D + 1)][p] = a[((kb + D) * NP + p) * 64];
         }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int k = 2 * (4 * q + j) + kr;
-            float b[NCOL];
+        for (int c = 0; c < NC; c++) {
+            const int g = kb * NC + c;
+            if (g + 1 < KB * NC) {
+                const int kn = (g + 1) / NC, cn = (g + 1) % NC;
 #pragma unroll
-            for (int c = 0; c < NCOL; c++) b[c] = act[k * TILE + 32 * c + cl];
-#pragma unroll
-            for (int i = 0; i < NT; i++) {
-                const float fa = j == 0 ? cur[i].x : j == 1 ? cur[i].y : j == 2 ? cur[i].z : cur[i].w;
-#pragma unroll
-                for (int c = 0; c < NCOL; c++) acc[i][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, b[c], acc[i][c], 0, 0, 0);
+                for (int p = 0; p < NP; p++)
+                    fb[(g + 1) & 1][p] = *reinterpret_cast<const bf16x8*>(bq + 32 * cn * ST + 16 * kn + p * PL);
             }
+            __builtin_amdgcn_sched_barrier(0);
+            acc[c] = mfma6(R.w[kb % (D + 1)], fb[g & 1], acc[c]);
         }
     }
 }
 
-template <int NT>
-__device__ __forceinline__ void zero_acc(f32x16 acc[NT][NCOL]) {
+template <int NC>
+__device__ __forceinline__ void zero_acc(f32x16 acc[NC]) {
 #pragma unroll
-    for (int i = 0; i < NT; i++)
+    for (int j = 0; j < NC; j++)
 #pragma unroll
-        for (int j = 0; j < NCOL; j++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.0f;
+        for (int r = 0; r < 16; r++) acc[j][r] = 0.0f;
 }
 
-// relu(acc + bias) -> out LDS [rows][TILE]; C/D layout of the 32x32 f32 MFMA: col = lane & 31,
-// row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).
-__device__ __forceinline__ void store_tile(const f32x16& acc, int row0, int col0, const float* __restrict__ bias,
-                                           float* out, int lane) {
+// C/D layout of the 32x32 MFMAs: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5), so
+// a lane's 16 rows of a tile at row0 are four runs of 4: row0 + 8 g + 4 (lane >> 5) + i, r = 4 g + i.
+// Per-row f32 vectors (biases, the value head) for those rows:
+struct Row16 {
+    float4 v[4];
+    __device__ __forceinline__ float operator[](int r) const {
+        const float4& q = v[r >> 2];
+        return (r & 3) == 0 ? q.x : (r & 3) == 1 ? q.y : (r & 3) == 2 ? q.z : q.w;
+    }
+};
+__device__ __forceinline__ Row16 load_rows(const float* __restrict__ B, int row0, int lane) {
+    Row16 r;
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-        const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const float v = acc[r] + bias[row];
-        out[row * TILE + col0 + (lane & 31)] = v > 0.0f ? v : 0.0f;
+    for (int g = 0; g < 4; g++) r.v[g] = *reinterpret_cast<const float4*>(B + row0 + 8 * g + 4 * (lane >> 5));
+    return r;
+}
+__device__ __forceinline__ float relu(float v) { return v > 0.0f ? v : 0.0f; }
+// relu(acc + bias) of a tile -> rows k0 .. k0 + 31, env columns col0 .. col0 + 31 of the bf16
+// planes [NP][env][ST] (4 consecutive k per store)
+template <int ST, int PL>
+__device__ __forceinline__ void store_planes(const f32x16& acc, int k0, int col0, const Row16& bias, __bf16* out, int lane) {
+    const int col = col0 + (lane & 31);
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const int k = k0 + 8 * g + 4 * (lane >> 5);
+        bf16x4 ph, pm, pl;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            __bf16 x0, x1, x2;
+            split3(relu(acc[4 * g + i] + bias[4 * g + i]), x0, x1, x2);
+            ph[i] = x0;
+            pm[i] = x1;
+            pl[i] = x2;
+        }
+        *reinterpret_cast<bf16x4*>(out + col * ST + k) = ph;
+        *reinterpret_cast<bf16x4*>(out + PL + col * ST + k) = pm;
+        *reinterpret_cast<bf16x4*>(out + 2 * PL + col * ST + k) = pl;
     }
 }
-template <int NT>
-__device__ __forceinline__ void store_rows(const f32x16 acc[NT][NCOL], int row0, const float* __restrict__ bias, float* out,
-                                           int lane) {
-#pragma unroll
-    for (int i = 0; i < NT; i++)
-#pragma unroll
-        for (int j = 0; j < NCOL; j++) store_tile(acc[i][j], row0 + 32 * i, 32 * j, bias, out, lane);
-}
 
-// Hidden layers 1 and 2 of a 256-wide MLP on the tile (x in s_x [DPAD][TILE]) -> s_h [256][TILE].
-template <int DPAD>
-__device__ __forceinline__ void hidden256(const float* __restrict__ W, const float* s_x, float* s_h, int wave, int lane) {
-    const float* W1 = W;                         // packed [8][DPAD/8][64][4]
-    const float* B1 = W1 + 256 * DPAD;           // [256]
-    const float* W2 = B1 + 256;                  // packed [8][32][64][4]
-    const float* B2 = W2 + 256 * 256;            // [256]
-    f32x16 acc[1][NCOL];
-    zero_acc<1>(acc);
-    mfma_rows<1, DPAD / 2>(W1, wave, s_x, lane, acc);
-    store_rows<1>(acc, 32 * wave, B1, s_h, lane);
-    __syncthreads();
-    zero_acc<1>(acc);
-    mfma_rows<1, 128>(W2, wave, s_h, lane, acc);
-    __syncthreads();                             // every wave has read h1
-    store_rows<1>(acc, 32 * wave, B2, s_h, lane);
-    __syncthreads();
-}
-
-__global__ void __launch_bounds__(NTHR, 4) k_policy(const float* __restrict__ feats, const int8_t* __restrict__ masks,
-                                                   int n, const float* __restrict__ actor_w,
-                                                   const float* __restrict__ critic_w, const uint64_t* __restrict__ seedp,
-                                                   uint32_t gid0, uint32_t step, int deterministic, uint8_t* __restrict__ actions,
-                                                   float* __restrict__ values, float* __restrict__ probs_out, int role0) {
-    __shared__ float s_x[FJSP_POLICY_CRITIC_DPAD * TILE];   // inputs; later the logits [8][TILE]
-    __shared__ float s_h[HID * TILE];                        // h1, then h2 (then critic h3)
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // the critic (the heaviest role: 848 MFMAs per wave against 544) first: 576 workgroups run
-    // on 512 two-per-CU slots, and the ones left for the second round should be the short ones
-    // (measured: 83.8 -> 75.0 us per launch at 4 096 envs)
-    const int y = (int)blockIdx.y + role0;   // role0 = 1: the actors only (no values wanted)
-    const int role = y == 0 ? NAG : y - 1;
-    const int e0 = blockIdx.x * TILE;
-    const bool critic = role == NAG;
-    if (!critic) {
-        // a tile in which the agent has exactly one valid action in every env: the draw (and
-        // argmax) returns that action whatever the network says, and the masked probabilities
-        // are exactly one-hot (p / p, or the uniform fallback over one action) -- skip the MLP.
-        // The station agents are forced in 96-100 % of an A2C collect's samples and whole
-        // tiles in 38-100 % (scripts/diag_forced_actions.py)
-        const int na = c_nact[role], mo = c_mask_off[role];
-        int forced = 1, only = 0;
-        if (tid < TILE && e0 + tid < n) {
-            int cnt = 0;
+// The logits' partial sums of this wave's 32 rows of h2 = relu(acc + b2) (rows of the C/D
+// layout) for NA actions -> s_part[wave][j][env]: per lane its 16 rows, then the other
+// half-wave's 16 (lane ^ 32).  Actions in chunks of up to 4 (all 8 at once spilled at 128 VGPRs).
+template <int NA>
+__device__ __forceinline__ void logit_partials(const f32x16 acc[2], const Row16& b2, const float* s_w3, float* s_part,
+                                               int wave, int lane) {
+    constexpr int CH = NA < 4 ? NA : 4;
+    static_assert(NA % CH == 0, "action chunks");
 #pragma unroll
-            for (int j = 0; j < 8; j++)
-                if (j < na && masks[(size_t)(mo + j) * n + e0 + tid] != 0) { cnt++; only = j; }
-            forced = cnt == 1;
-        }
-        if (__syncthreads_and(forced)) {
-            if (tid < TILE && e0 + tid < n) {
-                const int e = e0 + tid;
-                actions[(size_t)role * n + e] = (uint8_t)only;
-                if (probs_out)
-                    for (int j = 0; j < 8; j++) probs_out[((size_t)role * 8 + j) * n + e] = j == only ? 1.0f : 0.0f;
+    for (int c = 0; c < 2; c++) {
+        float h[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) h[r] = relu(acc[c][r] + b2[r]);
+#pragma unroll
+        for (int j0 = 0; j0 < NA; j0 += CH) {
+            float l[CH];
+#pragma unroll
+            for (int j = 0; j < CH; j++) l[j] = 0.0f;
+#pragma unroll
+            for (int g = 0; g < 4; g++)
+#pragma unroll
+                for (int j = 0; j < CH; j++) {
+                    const float4 w =
+                        *reinterpret_cast<const float4*>(s_w3 + (j0 + j) * HID + 32 * wave + 8 * g + 4 * (lane >> 5));
+                    l[j] = fmaf(w.x, h[4 * g], l[j]);
+                    l[j] = fmaf(w.y, h[4 * g + 1], l[j]);
+                    l[j] = fmaf(w.z, h[4 * g + 2], l[j]);
+                    l[j] = fmaf(w.w, h[4 * g + 3], l[j]);
+                }
+#pragma unroll
+            for (int j = 0; j < CH; j++) {
+                const float t = l[j] + __shfl_xor(l[j], 32);
+                if (lane < 32) s_part[(wave * 8 + j0 + j) * TA + 32 * c + lane] = t;
             }
-            return;
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
-    const int din = critic ? 38 : c_obs_dim[role];
-    const int off = critic ? 0 : c_obs_off[role];
-    const int dpad = critic ? FJSP_POLICY_CRITIC_DPAD : FJSP_POLICY_ACTOR_DPAD;
-    for (int i = tid; i < dpad * TILE; i += NTHR) {
-        const int k = i / TILE, c = i % TILE;
-        s_x[i] = (k < din && e0 + c < n) ? feats[(size_t)(off + k) * n + e0 + c] : 0.0f;
+}
+
+// The tile's inputs: din feature rows from row off of the [38][n] slab, zero-padded to DPAD, for
+// the tile's T envs -> registers (issued first: they overlap the mask check) -> the bf16 planes
+// [NP][T][DPAD + 8].
+constexpr int XI = cmax(C_DPAD * TC, A_DPAD * TA) / NTHR;
+template <int T, int DPAD>
+__device__ __forceinline__ void inputs_load(const float* __restrict__ feats, int n, int e0, int off, int din, int tid,
+                                            float v[XI]) {
+#pragma unroll
+    for (int q = 0; q < XI; q++) {
+        const int i = tid + q * NTHR, k = i / T, c = i % T;
+        v[q] = (i < DPAD * T && k < din && e0 + c < n) ? feats[(size_t)(off + k) * n + e0 + c] : 0.0f;
     }
+}
+template <int T, int DPAD>
+__device__ __forceinline__ void inputs_store(const float v[XI], int tid, __bf16* s_x) {
+    constexpr int S = DPAD + 8, PL = T * S;
+#pragma unroll
+    for (int q = 0; q < XI; q++) {
+        const int i = tid + q * NTHR, k = i / T, c = i % T;
+        if (i < DPAD * T) {
+            __bf16 x0, x1, x2;
+            split3(v[q], x0, x1, x2);
+            s_x[c * S + k] = x0;
+            s_x[PL + c * S + k] = x1;
+            s_x[2 * PL + c * S + k] = x2;
+        }
+    }
+}
+
+struct PolicyArgs {
+    const float* feats;
+    const int8_t* masks;
+    int n;
+    const float* actor_w;
+    const float* critic_w;
+    const uint64_t* seedp;
+    uint32_t gid0, step;
+    int deterministic;
+    uint8_t* actions;
+    float* values;
+    float* probs_out;
+    int nc, na;   // critic / actor workgroups per role
+};
+
+// The critic on a tile of 32 envs: layers 1 and 2 one 32-row tile per wave, layer 3 (128 rows)
+// on waves 0..3, the value head from layer 3's accumulators.
+__device__ __forceinline__ void critic_tile(const PolicyArgs& A, int tile, unsigned char* s_mem, int tid, int lane,
+                                            int wave) {
+    __bf16* s_x = reinterpret_cast<__bf16*>(s_mem);              // inputs [NP][TC][XSC]
+    __bf16* s_h = reinterpret_cast<__bf16*>(s_mem + X_BYTES);    // h1, then h2 [NP][TC][HSC]
+    float* s_part = reinterpret_cast<float*>(s_mem);             // value partials [4][TC] (after layer 1)
+    const int n = A.n, e0 = tile * TC;
+    const float* wb = A.critic_w;
+    const bf16x8* W1 = reinterpret_cast<const bf16x8*>(wb);
+    const float* B1 = wb + NP * HID * C_DPAD / 2;
+    const bf16x8* W2 = reinterpret_cast<const bf16x8*>(B1 + HID);
+    const float* B2 = B1 + HID + NP * HID * HID / 2;
+    const bf16x8* W3 = reinterpret_cast<const bf16x8*>(B2 + HID);     // [4 row tiles][16][NP][64][8]
+    const float* B3 = B2 + HID + NP * 128 * HID / 2;                  // [128]
+    const float* W4 = B3 + 128;                                       // [128]
+    const float* B4 = W4 + 128;                                       // [1]
+    float xv[XI];
+    inputs_load<TC, C_DPAD>(A.feats, n, e0, 0, 38, tid, xv);
+    WRing<C_DPAD / 16> r1;
+    wring_start(r1, wblocks<C_DPAD / 16, C_DPAD / 16>(W1, wave, 0, lane));
+    const Row16 b1 = load_rows(B1, 32 * wave, lane);
+    inputs_store<TC, C_DPAD>(xv, tid, s_x);
     __syncthreads();
-    if (critic) {
-        hidden256<FJSP_POLICY_CRITIC_DPAD>(critic_w, s_x, s_h, wave, lane);
-        const float* W3 = critic_w + 256 * FJSP_POLICY_CRITIC_DPAD + 256 + 256 * 256 + 256;   // packed [4][32][64][4]
-        const float* B3 = W3 + 128 * HID;                  // [128]
-        const float* W4 = B3 + 128;                        // [128]
-        const float* B4 = W4 + 128;                        // [1]
-        f32x16 acc[1][NCOL];
-        if (wave < 4) {                                    // 128 rows = 4 row tiles
-            zero_acc<1>(acc);
-            mfma_rows<1, 128>(W3, wave, s_h, lane, acc);
-        }
-        __syncthreads();
-        if (wave < 4) store_rows<1>(acc, 32 * wave, B3, s_h, lane);   // h3 [128][TILE]
-        __syncthreads();
-        if (tid < TILE && e0 + tid < n) {
-            float v = B4[0];
-            for (int k = 0; k < 128; k++) v = fmaf(W4[k], s_h[k * TILE + tid], v);
-            values[e0 + tid] = v;
+    PST(3, __builtin_amdgcn_s_memtime());
+    f32x16 a[1];
+    zero_acc<1>(a);
+    mfma_rows<C_DPAD / 16, XSC, XPC, 1>(r1, wblocks<C_DPAD / 16, C_DPAD / 16>(W1, wave, 0, lane), s_x, 0, lane, a);
+    PST(4, __builtin_amdgcn_s_memtime());
+    WRing<HID / 16> r2;
+    wring_start(r2, wblocks<HID / 16, HID / 16>(W2, wave, 0, lane));
+    store_planes<HSC, HPC>(a[0], 32 * wave, 0, b1, s_h, lane);
+    const Row16 b2 = load_rows(B2, 32 * wave, lane);
+    __syncthreads();
+    PST(5, __builtin_amdgcn_s_memtime());
+    zero_acc<1>(a);
+    mfma_rows<HID / 16, HSC, HPC, 1>(r2, wblocks<HID / 16, HID / 16>(W2, wave, 0, lane), s_h, 0, lane, a);
+    PST(6, __builtin_amdgcn_s_memtime());
+    const int rt3 = wave & 3;
+    WRing<HID / 16> r3;
+    wring_start(r3, wblocks<HID / 16, HID / 16>(W3, rt3, 0, lane));
+    const Row16 b3 = load_rows(B3, 32 * rt3, lane), w4 = load_rows(W4, 32 * rt3, lane);
+    __syncthreads();                               // every wave has read h1
+    store_planes<HSC, HPC>(a[0], 32 * wave, 0, b2, s_h, lane);
+    __syncthreads();
+    PST(7, __builtin_amdgcn_s_memtime());
+    if (wave < 4) {
+        zero_acc<1>(a);
+        mfma_rows<HID / 16, HSC, HPC, 1>(r3, wblocks<HID / 16, HID / 16>(W3, rt3, 0, lane), s_h, 0, lane, a);
+        // the value head: this lane's 16 rows of h3, the other half-wave's (lane ^ 32), then the
+        // four row tiles through LDS
+        float v = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; r++) v = fmaf(w4[r], relu(a[0][r] + b3[r]), v);
+        v += __shfl_xor(v, 32);
+        if (lane < 32) s_part[wave * TC + lane] = v;
+    }
+    PST(8, __builtin_amdgcn_s_memtime());
+    __syncthreads();
+    if (tid < TC && e0 + tid < n) {
+        float val = B4[0];
+#pragma unroll
+        for (int w = 0; w < 4; w++) val += s_part[w * TC + tid];
+        A.values[e0 + tid] = val;
+    }
+}
+
+// Actor `role` on a tile of 64 envs.  Layer 1 is computed per K half of layer 2 (rows 0..127,
+// then 128..255: one 32 x 32 tile per wave each), each half stored as the bf16 planes of layer
+// 2's input and summed into layer 2's accumulators (32 rows x 64 envs per wave), so only half of
+// h1 is ever in LDS.
+__device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int tile, unsigned char* s_mem, int tid,
+                                           int lane, int wave) {
+    __bf16* s_x = reinterpret_cast<__bf16*>(s_mem);                      // inputs [NP][TA][XSA]
+    __bf16* s_h = reinterpret_cast<__bf16*>(s_mem + X_BYTES);            // an h1 half [NP][TA][HSA]
+    float* s_part = reinterpret_cast<float*>(s_mem + X_BYTES);           // logit partials [8][8][TA] (after layer 2)
+    float* s_w3 = reinterpret_cast<float*>(s_mem + X_BYTES + H_BYTES);   // logit weights [8][256]
+    const int n = A.n, e0 = tile * TA;
+    const float* wb = A.actor_w + (size_t)role * FJSP_POLICY_ACTOR_FLOATS;
+    const bf16x8* W1 = reinterpret_cast<const bf16x8*>(wb);
+    const float* B1 = wb + NP * HID * A_DPAD / 2;
+    const bf16x8* W2 = reinterpret_cast<const bf16x8*>(B1 + HID);
+    const float* B2 = B1 + HID + NP * HID * HID / 2;
+    const float* W3 = B2 + HID;                                          // f32 [8][256]
+    const float* B3 = W3 + 8 * HID;                                      // [8]
+    float xv[XI];
+    inputs_load<TA, A_DPAD>(A.feats, n, e0, c_obs_off[role], c_obs_dim[role], tid, xv);
+    const float4 w3v = reinterpret_cast<const float4*>(W3)[tid];
+    const int na = c_nact[role], mo = c_mask_off[role];
+    // a tile in which the agent has exactly one valid action in every env: the draw (and argmax)
+    // returns that action whatever the network says, and the masked probabilities are exactly
+    // one-hot (p / p, or the uniform fallback over one action) -- skip the MLP.  The station
+    // agents are forced in 96-100 % of an A2C collect's samples and whole tiles in 38-100 %
+    // (scripts/diag_forced_actions.py)
+    uint32_t mbits = 0;   // the env's valid actions (threads < TA)
+    int forced = 1;
+    if (tid < TA && e0 + tid < n) {
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (j < na && A.masks[(size_t)(mo + j) * n + e0 + tid] != 0) mbits |= 1u << j;
+        forced = __builtin_popcount(mbits) == 1;
+    }
+    if (__syncthreads_and(forced)) {
+        PST(13, role | 256);
+        PST(9, __builtin_amdgcn_s_memtime());
+        PST(10, __builtin_amdgcn_s_memrealtime());
+        if (tid < TA && e0 + tid < n) {
+            const int e = e0 + tid, only = __builtin_ctz(mbits | 256u);
+            A.actions[(size_t)role * n + e] = (uint8_t)only;
+            if (A.probs_out)
+                for (int j = 0; j < 8; j++) A.probs_out[((size_t)role * 8 + j) * n + e] = j == only ? 1.0f : 0.0f;
         }
         return;
     }
-    const float* W = actor_w + (size_t)role * FJSP_POLICY_ACTOR_FLOATS;
-    hidden256<FJSP_POLICY_ACTOR_DPAD>(W, s_x, s_h, wave, lane);
-    // layer 3: logits [8][TILE]; wave -> action row, lane -> env; weights wave-uniform
-    const float* W3 = W + 256 * FJSP_POLICY_ACTOR_DPAD + 256 + 256 * 256 + 256;   // [8][256]
-    const float* B3 = W3 + 8 * HID;                                                // [8]
-    float* s_logit = s_x;
-    static_assert(NWAVE == 8 && TILE == 64, "one logit row per wave, one env per lane");
-    {
-        const int c = lane, r = wave;
-        float l = B3[r];
-        for (int k = 0; k < HID; k++) l = fmaf(W3[r * HID + k], s_h[k * TILE + c], l);
-        s_logit[r * TILE + c] = l;
-    }
+    PST(2, __builtin_amdgcn_s_memtime());
+    reinterpret_cast<float4*>(s_w3)[tid] = w3v;
+    inputs_store<TA, A_DPAD>(xv, tid, s_x);
+    const int rt1 = wave & 3, ct1 = wave >> 2;   // layer-1 tile of each half
+    WRing<1> r1;
+    wring_start(r1, wblocks<1, 1>(W1, rt1, 0, lane));
+    Row16 b1 = load_rows(B1, 32 * rt1, lane);
     __syncthreads();
-    if (tid < TILE && e0 + tid < n) {
-        const int c = tid, e = e0 + tid;
-        const int na = c_nact[role], mo = c_mask_off[role];
-        float p[8], m[8];
+    PST(3, __builtin_amdgcn_s_memtime());
+    f32x16 acc[2];
+    zero_acc<2>(acc);
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+        f32x16 a1[1];
+        zero_acc<1>(a1);
+        mfma_rows<1, XSA, XPA, 1>(r1, wblocks<1, 1>(W1, 4 * half + rt1, 0, lane), s_x, 32 * ct1, lane, a1);
+        WRing<HID / 32> r2;
+        wring_start(r2, wblocks<HID / 32, HID / 16>(W2, wave, 8 * half, lane));
+        store_planes<HSA, HPA>(a1[0], 32 * rt1, 32 * ct1, b1, s_h, lane);
+        __syncthreads();
+        PST(4 + 2 * half, __builtin_amdgcn_s_memtime());
+        mfma_rows<HID / 32, HSA, HPA, 2>(r2, wblocks<HID / 32, HID / 16>(W2, wave, 8 * half, lane), s_h, 0, lane, acc);
+        if (half == 0) {                           // the second half's layer-1 weights and biases
+            wring_start(r1, wblocks<1, 1>(W1, 4 + rt1, 0, lane));
+            b1 = load_rows(B1, 128 + 32 * rt1, lane);
+        }
+        __syncthreads();                           // every wave has read this half
+        PST(5 + 2 * half, __builtin_amdgcn_s_memtime());
+    }
+    // layer 3, the logits, straight from the accumulators
+    const Row16 b2 = load_rows(B2, 32 * wave, lane);
+    if (na == 8) logit_partials<8>(acc, b2, s_w3, s_part, wave, lane);
+    else logit_partials<3>(acc, b2, s_w3, s_part, wave, lane);
+    __syncthreads();
+    PST(8, __builtin_amdgcn_s_memtime());
+    if (tid < TA && e0 + tid < n) {
+        const int e = e0 + tid;
+        float lg[8], p[8], m[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            float v = 0.0f;
+            if (j < na) {
+                v = B3[j];
+#pragma unroll
+                for (int w = 0; w < NWAVE; w++) v += s_part[(w * 8 + j) * TA + tid];
+            }
+            lg[j] = v;
+        }
         float mx = -INFINITY;
         // fixed 8-trip loops guarded by na: fully unrolled, the arrays stay in registers
 #pragma unroll
-        for (int j = 0; j < 8; j++) if (j < na) mx = fmaxf(mx, s_logit[j * TILE + c]);
+        for (int j = 0; j < 8; j++) if (j < na) mx = fmaxf(mx, lg[j]);
         float s = 0.0f;
 #pragma unroll
-        for (int j = 0; j < 8; j++) { p[j] = j < na ? expf(s_logit[j * TILE + c] - mx) : 0.0f; s += p[j]; }
+        for (int j = 0; j < 8; j++) { p[j] = j < na ? expf(lg[j] - mx) : 0.0f; s += p[j]; }
         float s2 = 0.0f, ms = 0.0f;
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-            m[j] = j < na ? (float)masks[(size_t)(mo + j) * n + e] : 0.0f;
+            m[j] = j < na && ((mbits >> j) & 1u) ? 1.0f : 0.0f;
             p[j] = (p[j] / s) * m[j];
             s2 += p[j];
             ms += m[j];
@@ -253,14 +480,14 @@ __global__ void __launch_bounds__(NTHR, 4) k_policy(const float* __restrict__ fe
 #pragma unroll
         for (int j = 0; j < 8; j++) p[j] = s2 > 0.0f ? p[j] / s2 : m[j] / ms;
         int act = 0;
-        if (deterministic) {
+        if (A.deterministic) {
             float best = p[0];
 #pragma unroll
             for (int j = 1; j < 8; j++) if (j < na && p[j] > best) { best = p[j]; act = j; }
         } else {
-            const uint64_t seed = *seedp;
+            const uint64_t seed = *A.seedp;
             // keyed by the env's GLOBAL id: shards of a multi-GPU job draw independent streams
-            const uint64_t h = fmix64(seed ^ fmix64(((uint64_t)(gid0 + (uint32_t)e) << 32) | step) ^
+            const uint64_t h = fmix64(seed ^ fmix64(((uint64_t)(A.gid0 + (uint32_t)e) << 32) | A.step) ^
                                       (uint64_t)(role + 1) * 0x9E3779B97F4A7C15ull);
             const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
             float tot = 0.0f, cdf[8];
@@ -271,10 +498,29 @@ __global__ void __launch_bounds__(NTHR, 4) k_policy(const float* __restrict__ fe
             for (int j = 0; j < 8; j++) act += (j < na && cdf[j] < x) ? 1 : 0;
             if (act >= na) act = na - 1;
         }
-        actions[(size_t)role * n + e] = (uint8_t)act;
-        if (probs_out)
-            for (int j = 0; j < 8; j++) probs_out[((size_t)role * 8 + j) * n + e] = j < na ? p[j] : 0.0f;
+        A.actions[(size_t)role * n + e] = (uint8_t)act;
+        if (A.probs_out)
+            for (int j = 0; j < 8; j++) A.probs_out[((size_t)role * 8 + j) * n + e] = j < na ? p[j] : 0.0f;
     }
+}
+
+// Packed weights (floats; the bf16 blocks are NP * rows * K / 2 floats), see include/fjsp.h.
+__global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) k_policy(PolicyArgs A) {
+    __shared__ __attribute__((aligned(16))) unsigned char s_mem[LDS_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // (critic first or last, the AGV's workgroups first: within 3 %, profiles/r03/experiments)
+    const int b = blockIdx.x;
+    const int role = b < A.nc ? NAG : (b - A.nc) / A.na;
+    PST(0, __builtin_amdgcn_s_memrealtime());
+    PST(1, __builtin_amdgcn_s_memtime());
+    PST(11, __builtin_amdgcn_s_getreg(4 | (31 << 11)));
+    PST(12, __builtin_amdgcn_s_getreg(20 | (31 << 11)));
+    PST(13, role);
+    if (role == NAG) critic_tile(A, b, s_mem, tid, lane, wave);
+    else actor_tile(A, role, (b - A.nc) % A.na, s_mem, tid, lane, wave);
+    PST(9, __builtin_amdgcn_s_memtime());
+    PST(10, __builtin_amdgcn_s_memrealtime());
 }
 
 // Keys of the A2C update's grouping of repeated inputs (a2c_vec.row_keys, the same hash): per
@@ -620,6 +866,17 @@ extern "C" int fjsp_a2c_value_head_grad(const float* y, const float* gv, const f
     return 0;
 }
 
+#ifdef FJSP_STAMPS
+extern "C" int fjsp_debug_policy_stamps(unsigned long long* out, int32_t clear) {   // out[2048 * 16]
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pstamps), sizeof(unsigned long long) * 2048 * 16) != hipSuccess) return -2;
+    if (clear) {
+        static unsigned long long z[2048 * 16];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_pstamps), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
+
 extern "C" int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const float* actor_w,
                                const float* critic_w, const uint64_t* seed, uint32_t env_gid0, uint32_t step,
                                int32_t deterministic,
@@ -627,12 +884,11 @@ extern "C" int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t 
     if (n <= 0) return fjsp_internal_fail("fjsp_a2c_policy: n must be > 0");
     if (!feats || (!actions && !values) || (values && !critic_w) || (actions && (!masks || !actor_w || !seed)))
         return fjsp_internal_fail("fjsp_a2c_policy: null buffer");
-    // roles: y = 0 the critic, 1..8 the actors; without actions only the critic (values), without
-    // values only the actors
-    const int role0 = values ? 0 : 1, role1 = actions ? NAG + 1 : 1;
-    dim3 grid((n + TILE - 1) / TILE, role1 - role0);
-    hipLaunchKernelGGL(k_policy, grid, dim3(NTHR), 0, (hipStream_t)stream, feats, masks, n, actor_w, critic_w, seed, env_gid0,
-                       step, deterministic, actions, values, probs, role0);
+    // workgroups: the critic on 32-env tiles (values wanted), then each actor on 64-env tiles
+    // (actions wanted)
+    PolicyArgs A{feats, masks, n, actor_w, critic_w, seed, env_gid0, step, deterministic, actions, values, probs,
+                 values ? (n + TC - 1) / TC : 0, actions ? (n + TA - 1) / TA : 0};
+    hipLaunchKernelGGL(k_policy, dim3((unsigned)(A.nc + NAG * A.na)), dim3(NTHR), 0, (hipStream_t)stream, A);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

@@ -317,3 +317,21 @@ def test_grouped_update_equals_dense_update():
     ref = torch.zeros(3, g.U[0]).index_add_(1, g.inv[0], w[0])
     assert torch.allclose(y.grad[0], ref, rtol=1e-5, atol=1e-5)
     assert A.group_columns(x, torch.zeros(x.shape[1], dtype=torch.int64)) is None
+
+
+def test_policy_weight_packing_planes_and_lane_order():
+    """pack_mfma (the fused policy kernel's weight layout, include/fjsp.h): three bf16 planes
+    whose sum is the f32 weight within 2^-24 relative, in the 32x32x16 MFMA A-operand lane order
+    (t, kb, p, l, j) = plane p of W[32 t + (l & 31)][16 kb + 8 (l >> 5) + j]."""
+    g = torch.Generator().manual_seed(5)
+    W = torch.randn(64, 48, generator=g) * torch.logspace(-3, 2, 48)[None, :]
+    hi, mid, lo = A.split_bf16x3(W)
+    back = hi.double() + mid.double() + lo.double()
+    assert float(((back - W.double()).abs() / W.double().abs()).max()) <= 2.0 ** -24
+    Pk = A.pack_mfma(W).view(torch.bfloat16).reshape(2, 3, 3, 64, 8)   # t, kb, p, l, j
+    planes = (hi, mid, lo)
+    for t, kb, p, l, j in [(0, 0, 0, 0, 0), (1, 2, 1, 37, 5), (1, 1, 2, 63, 7), (0, 2, 0, 31, 3)]:
+        r, k = 32 * t + (l & 31), 16 * kb + 8 * (l >> 5) + j
+        assert Pk[t, kb, p, l, j].item() == planes[p][r, k].item()
+    a, c = A.pack_policy_weights(*A.init_networks(seed=0))
+    assert a.numel() == 8 * A.nat.POLICY_ACTOR_FLOATS and c.numel() == A.nat.POLICY_CRITIC_FLOATS
