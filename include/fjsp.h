@@ -261,6 +261,13 @@ int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const fl
                     const uint64_t* seed, uint32_t env_gid0, uint32_t step, int32_t deterministic, uint8_t* actions,
                     float* values,
                     float* probs, void* stream);
+/* The critic's forward over n samples for the A2C update (a2c.py:692-699 critic(global_states)
+ * over the batch; a2c_vec._CriticGrouped): x f32 [38][n] (feature rows, as fjsp_a2c_policy's
+ * feats), critic_w packed as for fjsp_a2c_policy -> values f32 [n] and the post-ReLU hidden
+ * layers the backward reads, h1 / h2 f32 [n][256], h3 f32 [n][128] (sample-major).  Same
+ * arithmetic as fjsp_a2c_policy's values.  Stream-ordered. */
+int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* critic_w, float* h1, float* h2, float* h3,
+                            float* values, void* stream);
 /* Grouping keys of the A2C update (a2c.py:647-703 _update over a batch; a2c_vec.A2CLosses
  * dedup): feats f32 [T][38][n] (the rollout's a2c features) -> keys u64 [9][T * n], row a < 8
  * a hash of actor a's padded input (its a2c.py:118-134 observation block, zero-padded to 13

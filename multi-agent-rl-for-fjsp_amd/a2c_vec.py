@@ -26,6 +26,7 @@ Padding is exact: padded input columns are zero and their weights receive zero g
 padded action logits are -inf before the softmax.
 """
 import ctypes
+import os
 import math
 
 import torch
@@ -152,6 +153,60 @@ def _relu_bias_grad(gy, y):
     V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     nat.check(nat.lib().fjsp_a2c_relu_bias_grad(V(gy), V(y), B, C, V(g), V(part), ctypes.c_void_p(stream)))
     return g, part.sum(0)
+
+
+class _CriticGrouped(torch.autograd.Function):
+    """The critic (38 -> 256 -> 256 -> 128 -> 1, ReLUs) over a long batch of distinct global states
+    on the GPU: the forward in one fused kernel (fjsp_a2c_critic_forward: f32 operands as bf16
+    planes on the matrix cores, as the policy kernel's values), which also writes the hidden
+    layers; the backward as _ValueHead / _LinearSplitK's (value-head kernel, ReLU + bias-gradient
+    kernel, split-K weight gradients).  xT f32 [38, U] -> v [U]."""
+
+    @staticmethod
+    def forward(ctx, xT, W1, b1, W2, b2, W3, b3, W4, b4):
+        U = xT.shape[1]
+        dev = xT.device
+        cw = pack_critic_weights(W1, b1, W2, b2, W3, b3, W4, b4)
+        h1 = torch.empty(U, W2.shape[1], dtype=torch.float32, device=dev)
+        h2 = torch.empty(U, W2.shape[0], dtype=torch.float32, device=dev)
+        h3 = torch.empty(U, W3.shape[0], dtype=torch.float32, device=dev)
+        v = torch.empty(U, dtype=torch.float32, device=dev)
+        V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        nat.check(nat.lib().fjsp_a2c_critic_forward(V(xT), U, V(cw), V(h1), V(h2), V(h3), V(v), ctypes.c_void_p(stream)))
+        ctx.save_for_backward(xT, W2, W3, W4, h1, h2, h3)
+        return v
+
+    @staticmethod
+    def backward(ctx, gv):
+        xT, W2, W3, W4, h1, h2, h3 = ctx.saved_tensors
+        B, C = h3.shape
+        gvc = gv.reshape(-1).contiguous()
+        w4 = W4.reshape(-1).contiguous()
+        g3 = torch.empty_like(h3)
+        part = torch.empty(-(-B // 128), 2 * C + 4, dtype=torch.float32, device=h3.device)
+        stream = torch.cuda.current_stream(h3.device).cuda_stream
+        V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        nat.check(nat.lib().fjsp_a2c_value_head_grad(V(h3), V(gvc), V(w4), B, V(g3), V(part), ctypes.c_void_p(stream)))
+        ps = part.sum(0)
+        gW3 = _splitk_wgrad(g3, h2)
+        g2, gb2 = _relu_bias_grad((g3 @ W3).contiguous(), h2)
+        gW2 = _splitk_wgrad(g2, h1)
+        g1, gb1 = _relu_bias_grad((g2 @ W2).contiguous(), h1)
+        gW1 = _splitk_wgrad(g1, xT.t())
+        return (None, gW1, gb1, gW2, gb2, gW3, ps[:C], ps[C:2 * C].view(1, C), ps[2 * C:2 * C + 1])
+
+
+# the grouped update's critic through the fused forward kernel (FJSP_CRITIC_FUSED=0: PyTorch GEMMs,
+# for A/B runs)
+critic_fused = os.environ.get("FJSP_CRITIC_FUSED", "1") != "0"
+
+
+def critic_grouped(critic, xT):
+    """v [U] of the critic over the columns of xT f32 [38, U] (distinct global states)."""
+    n = critic.net
+    return _CriticGrouped.apply(xT.contiguous(), n[0].weight, n[0].bias, n[2].weight, n[2].bias, n[4].weight,
+                                n[4].bias, n[6].weight, n[6].bias)
 
 
 def mlp_forward(seq, x):
@@ -677,7 +732,10 @@ class A2CLosses:
             return c[gidx[agents], torch.arange(k, device=idx.device)[:, None], :]
         # the critic first: its GEMMs keep the GPU busy while the host issues the actors' many
         # small launches (after the grouping's host synchronisations the queue is empty)
-        if gc is not None:
+        if gc is not None and feats.is_cuda and gc.first.shape[1] >= 65536 and critic_fused:
+            vu = critic_grouped(critic, gt[:, gc.first[0]]).reshape(1, 1, -1)
+            v = gc.gather(vu).reshape(-1)                            # [S]
+        elif gc is not None:
             vu = mlp_forward(critic.net, gt[:, gc.first[0]].t()).reshape(1, 1, -1)
             v = gc.gather(vu).reshape(-1)                            # [S]
         else:
@@ -739,6 +797,16 @@ def pack_mfma(W):
 
 
 @torch.no_grad()
+def pack_critic_weights(W1, b1, W2, b2, W3, b3, W4, b4):
+    """The critic's layers (networks.CentralizedCriticNetwork: 38 -> 256 -> 256 -> 128 -> 1) -> the
+    flat buffer fjsp_a2c_policy / fjsp_a2c_critic_forward read (include/fjsp.h)."""
+    z = W1.new_zeros
+    w1 = torch.cat([W1, z(W1.shape[0], nat.POLICY_CRITIC_DPAD - W1.shape[1])], dim=1)   # [256, 48]
+    return torch.cat([pack_mfma(w1).reshape(-1), b1.reshape(-1), pack_mfma(W2).reshape(-1), b2.reshape(-1),
+                      pack_mfma(W3).reshape(-1), b3.reshape(-1), W4.reshape(-1), torch.cat([b4.reshape(-1), z(15)])])
+
+
+@torch.no_grad()
 def pack_policy_weights(actors, critic, out_actor=None, out_critic=None):
     """Actor stack + critic -> the flat buffers fjsp_a2c_policy reads (include/fjsp.h): the MFMA
     layers' weights as bf16 planes in lane order, biases and the VALU layers as f32."""
@@ -748,11 +816,7 @@ def pack_policy_weights(actors, critic, out_actor=None, out_critic=None):
     b3 = torch.cat([actors.b3[:, :, 0], z(NA, 8)], dim=1)                                     # [8, 16]
     a = torch.cat([pack_mfma(w1).reshape(NA, -1), actors.b1.reshape(NA, -1), pack_mfma(actors.W2).reshape(NA, -1),
                    actors.b2.reshape(NA, -1), actors.W3.reshape(NA, -1), b3], dim=1).reshape(-1)
-    n = critic.net
-    cw1 = torch.cat([n[0].weight, z(256, nat.POLICY_CRITIC_DPAD - n[0].weight.shape[1])], dim=1)   # [256, 48]
-    c = torch.cat([pack_mfma(cw1).reshape(-1), n[0].bias,
-                   pack_mfma(n[2].weight).reshape(-1), n[2].bias, pack_mfma(n[4].weight).reshape(-1), n[4].bias,
-                   n[6].weight.reshape(-1), torch.cat([n[6].bias, z(15)])])
+    c = pack_critic_weights(*[m for i in (0, 2, 4, 6) for m in (critic.net[i].weight, critic.net[i].bias)])
     assert a.numel() == NA * nat.POLICY_ACTOR_FLOATS and c.numel() == nat.POLICY_CRITIC_FLOATS
     if out_actor is None:
         return a.contiguous(), c.contiguous()

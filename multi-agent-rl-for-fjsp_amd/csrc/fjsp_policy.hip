@@ -217,6 +217,21 @@ __device__ __forceinline__ void store_planes(const f32x16& acc, int k0, int col0
     }
 }
 
+// relu(acc + bias) of a tile -> rows (features) row0 .. row0 + 31 of the sample-major f32 matrix
+// out [samples][ld] for samples col0 .. col0 + 31 (< n): four 16-byte stores per lane
+__device__ __forceinline__ void store_rows_f32(const f32x16& acc, int row0, const Row16& bias, float* __restrict__ out,
+                                               int ld, int col0, int n, int lane) {
+    const int col = col0 + (lane & 31);
+    if (col >= n) return;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const int r = 4 * g;
+        *reinterpret_cast<float4*>(out + (size_t)col * ld + row0 + 8 * g + 4 * (lane >> 5)) =
+            make_float4(relu(acc[r] + bias[r]), relu(acc[r + 1] + bias[r + 1]), relu(acc[r + 2] + bias[r + 2]),
+                        relu(acc[r + 3] + bias[r + 3]));
+    }
+}
+
 // The logits' partial sums of this wave's 32 rows of h2 = relu(acc + b2) (rows of the C/D
 // layout) for NA actions -> s_part[wave][j][env]: per lane its 16 rows, then the other
 // half-wave's 16 (lane ^ 32).  Actions in chunks of up to 4 (all 8 at once spilled at 128 VGPRs).
@@ -301,9 +316,17 @@ struct PolicyArgs {
 };
 
 // The critic on a tile of 32 envs: layers 1 and 2 one 32-row tile per wave, layer 3 (128 rows)
-// on waves 0..3, the value head from layer 3's accumulators.
+// on waves 0..3, the value head from layer 3's accumulators.  SAVE (the A2C update's forward,
+// fjsp_a2c_critic_forward): the post-ReLU hidden layers also go to HBM, h1 / h2 [n][256] and
+// h3 [n][128] f32, sample-major (what the backward reads).
+struct CriticSave {
+    float* h1;
+    float* h2;
+    float* h3;
+};
+template <bool SAVE>
 __device__ __forceinline__ void critic_tile(const PolicyArgs& A, int tile, unsigned char* s_mem, int tid, int lane,
-                                            int wave) {
+                                            int wave, const CriticSave& sv) {
     __bf16* s_x = reinterpret_cast<__bf16*>(s_mem);              // inputs [NP][TC][XSC]
     __bf16* s_h = reinterpret_cast<__bf16*>(s_mem + X_BYTES);    // h1, then h2 [NP][TC][HSC]
     float* s_part = reinterpret_cast<float*>(s_mem);             // value partials [4][TC] (after layer 1)
@@ -332,6 +355,7 @@ __device__ __forceinline__ void critic_tile(const PolicyArgs& A, int tile, unsig
     WRing<HID / 16> r2;
     wring_start(r2, wblocks<HID / 16, HID / 16>(W2, wave, 0, lane));
     store_planes<HSC, HPC>(a[0], 32 * wave, 0, b1, s_h, lane);
+    if (SAVE) store_rows_f32(a[0], 32 * wave, b1, sv.h1, HID, e0, n, lane);
     const Row16 b2 = load_rows(B2, 32 * wave, lane);
     __syncthreads();
     PST(5, __builtin_amdgcn_s_memtime());
@@ -344,11 +368,13 @@ __device__ __forceinline__ void critic_tile(const PolicyArgs& A, int tile, unsig
     const Row16 b3 = load_rows(B3, 32 * rt3, lane), w4 = load_rows(W4, 32 * rt3, lane);
     __syncthreads();                               // every wave has read h1
     store_planes<HSC, HPC>(a[0], 32 * wave, 0, b2, s_h, lane);
+    if (SAVE) store_rows_f32(a[0], 32 * wave, b2, sv.h2, HID, e0, n, lane);
     __syncthreads();
     PST(7, __builtin_amdgcn_s_memtime());
     if (wave < 4) {
         zero_acc<1>(a);
         mfma_rows<HID / 16, HSC, HPC, 1>(r3, wblocks<HID / 16, HID / 16>(W3, rt3, 0, lane), s_h, 0, lane, a);
+        if (SAVE) store_rows_f32(a[0], 32 * rt3, b3, sv.h3, 128, e0, n, lane);
         // the value head: this lane's 16 rows of h3, the other half-wave's (lane ^ 32), then the
         // four row tiles through LDS
         float v = 0.0f;
@@ -517,10 +543,19 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
     PST(11, __builtin_amdgcn_s_getreg(4 | (31 << 11)));
     PST(12, __builtin_amdgcn_s_getreg(20 | (31 << 11)));
     PST(13, role);
-    if (role == NAG) critic_tile(A, b, s_mem, tid, lane, wave);
+    if (role == NAG) critic_tile<false>(A, b, s_mem, tid, lane, wave, CriticSave{});
     else actor_tile(A, role, (b - A.nc) % A.na, s_mem, tid, lane, wave);
     PST(9, __builtin_amdgcn_s_memtime());
     PST(10, __builtin_amdgcn_s_memrealtime());
+}
+
+// The critic's forward over n samples for the A2C update (values + the saved hidden layers).
+__global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)))
+k_critic_fwd(PolicyArgs A, CriticSave sv) {
+    __shared__ __attribute__((aligned(16))) unsigned char s_mem[LDS_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    critic_tile<true>(A, (int)blockIdx.x, s_mem, tid, lane, wave, sv);
 }
 
 // Keys of the A2C update's grouping of repeated inputs (a2c_vec.row_keys, the same hash): per
@@ -876,6 +911,20 @@ extern "C" int fjsp_debug_policy_stamps(unsigned long long* out, int32_t clear) 
     return 0;
 }
 #endif
+
+extern "C" int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* critic_w, float* h1, float* h2,
+                                       float* h3, float* values, void* stream) {
+    if (n <= 0) return fjsp_internal_fail("fjsp_a2c_critic_forward: n must be > 0");
+    if (!x || !critic_w || !h1 || !h2 || !h3 || !values) return fjsp_internal_fail("fjsp_a2c_critic_forward: null buffer");
+    PolicyArgs A{x, nullptr, n, nullptr, critic_w, nullptr, 0u, 0u, 0, nullptr, values, nullptr, (n + TC - 1) / TC, 0};
+    hipLaunchKernelGGL(k_critic_fwd, dim3((unsigned)A.nc), dim3(NTHR), 0, (hipStream_t)stream, A, CriticSave{h1, h2, h3});
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
+}
 
 extern "C" int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const float* actor_w,
                                const float* critic_w, const uint64_t* seed, uint32_t env_gid0, uint32_t step,

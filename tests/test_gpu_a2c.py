@@ -477,3 +477,38 @@ def test_graphed_update_equals_eager_update(M):
     assert runs[1][0] == runs[0][0]
     assert runs[1][1] == runs[0][1]
     assert torch.equal(runs[1][2], runs[0][2])
+
+
+def test_fused_critic_forward_backward_matches_torch(M):
+    """The grouped update's critic (a2c_vec._CriticGrouped: fjsp_a2c_critic_forward, then the
+    value-head / ReLU-bias kernels and split-K weight gradients) against a float64 evaluation of
+    the same network, beside the PyTorch-GEMM path (mlp_forward): values at most 3x that f32
+    path's error (+1e-7 relative), every parameter gradient within max(3x its error, 3e-3)
+    relative.  Both f32 paths flip a ReLU unit here and there whose pre-activation is within
+    rounding of 0 (scripts/diag_critic_fused.py: one per layer of 70 001 x 256 for either path, the
+    activations themselves within 7e-7 of float64), and one flipped unit of one sample moves a
+    weight gradient summed over 70 001 samples by ~3e-4 relative; a layout or indexing error
+    moves it by O(1)."""
+    import copy
+    A = M["A"]
+    torch.manual_seed(3)
+    _, critic = A.init_networks(seed=1, device="cuda")
+    U = 70001
+    xT = (torch.rand(38, U, device="cuda") * torch.randint(0, 30, (38, 1), device="cuda")).float()
+    w = torch.randn(U, device="cuda")
+    c64 = copy.deepcopy(critic).double()
+    v64 = c64.net(xT.double().t()).reshape(-1)
+    (v64 * w.double()).sum().backward()
+    g64 = [p.grad for p in c64.parameters()]
+    res = {}
+    for name, fwd in (("fused", lambda: A.critic_grouped(critic, xT)),
+                      ("torch", lambda: A.mlp_forward(critic.net, xT.t()).reshape(-1))):
+        critic.zero_grad(set_to_none=True)
+        v = fwd()
+        (v * w).sum().backward()
+        res[name] = (float((v.double() - v64).abs().max() / v64.abs().max()),
+                     [float((p.grad.double() - g).norm() / g.norm()) for p, g in zip(critic.parameters(), g64)])
+    ef, et = res["fused"], res["torch"]
+    assert ef[0] <= 3 * et[0] + 1e-7, (ef[0], et[0])
+    for a, b in zip(ef[1], et[1]):
+        assert a <= max(3 * b, 3e-3), (ef[1], et[1])
