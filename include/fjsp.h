@@ -268,6 +268,14 @@ int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const fl
  * arithmetic as fjsp_a2c_policy's values.  Stream-ordered. */
 int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* critic_w, float* h1, float* h2, float* h3,
                             float* values, void* stream);
+/* The critic's backward through its two 256-wide ReLU layers for the A2C update (a2c.py:692-699
+ * critic_loss.backward(); a2c_vec._CriticGrouped): g3 f32 [n][128] (layer 3's pre-activation
+ * gradient, fjsp_a2c_value_head_grad), h1 / h2 from fjsp_a2c_critic_forward, w3t / w2t = W3^T
+ * [256][128] / W2^T [256][256] packed as the forward's weights -> g2 = (g3 W3) * [h2 > 0], g1 =
+ * (g2 W2) * [h1 > 0] f32 [n][256] and their column sums per 32-sample tile, bias_part2 /
+ * bias_part1 f32 [ceil(n / 32)][256].  Stream-ordered. */
+int fjsp_a2c_critic_backward(const float* g3, const float* h1, const float* h2, int32_t n, const float* w3t,
+                             const float* w2t, float* g2, float* g1, float* bias_part2, float* bias_part1, void* stream);
 /* Grouping keys of the A2C update (a2c.py:647-703 _update over a batch; a2c_vec.A2CLosses
  * dedup): feats f32 [T][38][n] (the rollout's a2c features) -> keys u64 [9][T * n], row a < 8
  * a hash of actor a's padded input (its a2c.py:118-134 observation block, zero-padded to 13

@@ -159,8 +159,9 @@ class _CriticGrouped(torch.autograd.Function):
     """The critic (38 -> 256 -> 256 -> 128 -> 1, ReLUs) over a long batch of distinct global states
     on the GPU: the forward in one fused kernel (fjsp_a2c_critic_forward: f32 operands as bf16
     planes on the matrix cores, as the policy kernel's values), which also writes the hidden
-    layers; the backward as _ValueHead / _LinearSplitK's (value-head kernel, ReLU + bias-gradient
-    kernel, split-K weight gradients).  xT f32 [38, U] -> v [U]."""
+    layers; the backward: the value-head kernel, both 256-wide ReLU layers' input gradients in one
+    kernel (fjsp_a2c_critic_backward, the same split arithmetic), split-K weight gradients.
+    xT f32 [38, U] -> v [U]."""
 
     @staticmethod
     def forward(ctx, xT, W1, b1, W2, b2, W3, b3, W4, b4):
@@ -190,9 +191,20 @@ class _CriticGrouped(torch.autograd.Function):
         nat.check(nat.lib().fjsp_a2c_value_head_grad(V(h3), V(gvc), V(w4), B, V(g3), V(part), ctypes.c_void_p(stream)))
         ps = part.sum(0)
         gW3 = _splitk_wgrad(g3, h2)
-        g2, gb2 = _relu_bias_grad((g3 @ W3).contiguous(), h2)
+        if critic_bwd_fused:
+            # both 256-wide ReLU layers' input gradients in one pass (fjsp_a2c_critic_backward)
+            w3t, w2t = pack_mfma(W3.t().contiguous()).reshape(-1), pack_mfma(W2.t().contiguous()).reshape(-1)
+            g2, g1 = torch.empty_like(h2), torch.empty_like(h1)
+            nt = -(-B // 32)
+            bp2 = torch.empty(nt, h2.shape[1], dtype=torch.float32, device=h2.device)
+            bp1 = torch.empty(nt, h1.shape[1], dtype=torch.float32, device=h1.device)
+            nat.check(nat.lib().fjsp_a2c_critic_backward(V(g3), V(h1), V(h2), B, V(w3t), V(w2t), V(g2), V(g1), V(bp2),
+                                                         V(bp1), ctypes.c_void_p(stream)))
+            gb2, gb1 = bp2.sum(0), bp1.sum(0)
+        else:
+            g2, gb2 = _relu_bias_grad((g3 @ W3).contiguous(), h2)
+            g1, gb1 = _relu_bias_grad((g2 @ W2).contiguous(), h1)
         gW2 = _splitk_wgrad(g2, h1)
-        g1, gb1 = _relu_bias_grad((g2 @ W2).contiguous(), h1)
         gW1 = _splitk_wgrad(g1, xT.t())
         return (None, gW1, gb1, gW2, gb2, gW3, ps[:C], ps[C:2 * C].view(1, C), ps[2 * C:2 * C + 1])
 
@@ -200,6 +212,8 @@ class _CriticGrouped(torch.autograd.Function):
 # the grouped update's critic through the fused forward kernel (FJSP_CRITIC_FUSED=0: PyTorch GEMMs,
 # for A/B runs)
 critic_fused = os.environ.get("FJSP_CRITIC_FUSED", "1") != "0"
+# its backward through the two 256-wide layers in one kernel (FJSP_CRITIC_BWD=0: GEMMs + ReLU kernels)
+critic_bwd_fused = os.environ.get("FJSP_CRITIC_BWD", "1") != "0"
 
 
 def critic_grouped(critic, xT):

@@ -558,6 +558,137 @@ k_critic_fwd(PolicyArgs A, CriticSave sv) {
     critic_tile<true>(A, (int)blockIdx.x, s_mem, tid, lane, wave, sv);
 }
 
+// The critic's backward through layers 3 and 2 for the A2C update (a2c_vec._CriticGrouped): on a
+// tile of 32 samples, g2 = (g3 W3) * [h2 > 0] and g1 = (g2 W2) * [h1 > 0], the input gradients of
+// the two 256-wide ReLU layers, with W3^T / W2^T packed like the forward's weights and the
+// upstream gradient split into bf16 planes in LDS; g2 and g1 go to HBM (the split-K weight
+// gradients read them) with per-tile column sums (the bias gradients).  One pass instead of two
+// GEMMs and two ReLU / bias-gradient passes.
+struct CriticBwd {
+    const float* g3;    // [n][128] layer 3's pre-activation gradient (fjsp_a2c_value_head_grad)
+    const float* h1;    // [n][256] post-ReLU hidden layers of the forward
+    const float* h2;
+    const float* w3t;   // P(W3^T [256][128]), NP * 256 * 128 / 2 floats
+    const float* w2t;   // P(W2^T [256][256])
+    float* g2;          // [n][256]
+    float* g1;
+    float* bp2;         // [tiles][256] column sums of g2 / g1 per tile
+    float* bp1;
+    int n;
+};
+constexpr int GS3 = 128 + 8;   // bf16 stride of the g3 planes [NP][TC][GS3]
+static_assert(NP * TC * GS3 * 2 <= H_BYTES && NP * HPC * 2 <= H_BYTES, "backward planes");
+// this lane's 16 values of rows row0.. (C/D layout) at sample column col of a sample-major
+// [n][ld] f32 matrix (0 past n)
+__device__ __forceinline__ void load_tile_rows(const float* __restrict__ m, int ld, int col, int n, int row0, int lane,
+                                               float v[16]) {
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (col < n) q = *reinterpret_cast<const float4*>(m + (size_t)col * ld + row0 + 8 * g + 4 * (lane >> 5));
+        v[4 * g] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
+    }
+}
+// g = acc * [h > 0] -> HBM (sample-major [n][256]) and, for the tile's 32 samples, the column
+// sums into bp[row] (lanes 0 / 32 after a butterfly over each half-wave)
+__device__ __forceinline__ void relu_grad_out(f32x16& acc, const float h[16], float* __restrict__ g, float* __restrict__ bp,
+                                              int col, int n, int row0, int lane) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[r] = h[r] > 0.0f ? acc[r] : 0.0f;
+    if (col < n) {
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            *reinterpret_cast<float4*>(g + (size_t)col * HID + row0 + 8 * q + 4 * (lane >> 5)) =
+                make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+    }
+    float t[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) t[r] = acc[r];   // columns past n are 0 (h loaded as 0)
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1)
+#pragma unroll
+        for (int r = 0; r < 16; r++) t[r] += __shfl_xor(t[r], o);
+    if ((lane & 31) == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            *reinterpret_cast<float4*>(bp + row0 + 8 * q + 4 * (lane >> 5)) =
+                make_float4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
+    }
+}
+// a tile's f32 gradient (rows row0.., the C/D layout) -> bf16 planes [NP][TC][ST] (no ReLU, no bias)
+template <int ST, int PL>
+__device__ __forceinline__ void store_planes_raw(const f32x16& acc, int k0, __bf16* out, int lane) {
+    const int col = lane & 31;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const int k = k0 + 8 * g + 4 * (lane >> 5);
+        bf16x4 ph, pm, pl;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            __bf16 x0, x1, x2;
+            split3(acc[4 * g + i], x0, x1, x2);
+            ph[i] = x0;
+            pm[i] = x1;
+            pl[i] = x2;
+        }
+        *reinterpret_cast<bf16x4*>(out + col * ST + k) = ph;
+        *reinterpret_cast<bf16x4*>(out + PL + col * ST + k) = pm;
+        *reinterpret_cast<bf16x4*>(out + 2 * PL + col * ST + k) = pl;
+    }
+}
+__global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) k_critic_bwd(CriticBwd B) {
+    __shared__ __attribute__((aligned(16))) __bf16 s_g[H_BYTES / 2];   // g3 planes, then g2 planes
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tile = blockIdx.x, e0 = tile * TC, n = B.n;
+    const int col = e0 + (lane & 31);
+    const bf16x8* W3T = reinterpret_cast<const bf16x8*>(B.w3t);
+    const bf16x8* W2T = reinterpret_cast<const bf16x8*>(B.w2t);
+    WRing<8> r3;
+    wring_start(r3, wblocks<8, 8>(W3T, wave, 0, lane));
+    float hv[16];
+    load_tile_rows(B.h2, HID, col, n, 32 * wave, lane, hv);
+    // g3 [32 samples][128] -> planes: thread t: sample t / 16, 8 consecutive features
+    {
+        const int sl = tid >> 4, f0 = (tid & 15) * 8, c = e0 + sl;
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i] = 0.0f;
+        if (c < n) {
+            const float4 a = *reinterpret_cast<const float4*>(B.g3 + (size_t)c * 128 + f0);
+            const float4 b = *reinterpret_cast<const float4*>(B.g3 + (size_t)c * 128 + f0 + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        }
+        bf16x8 ph, pm, pl;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            __bf16 x0, x1, x2;
+            split3(v[i], x0, x1, x2);
+            ph[i] = x0;
+            pm[i] = x1;
+            pl[i] = x2;
+        }
+        constexpr int PL3 = TC * GS3;
+        *reinterpret_cast<bf16x8*>(s_g + sl * GS3 + f0) = ph;
+        *reinterpret_cast<bf16x8*>(s_g + PL3 + sl * GS3 + f0) = pm;
+        *reinterpret_cast<bf16x8*>(s_g + 2 * PL3 + sl * GS3 + f0) = pl;
+    }
+    __syncthreads();
+    f32x16 a[1];
+    zero_acc<1>(a);
+    mfma_rows<8, GS3, TC * GS3, 1>(r3, wblocks<8, 8>(W3T, wave, 0, lane), s_g, 0, lane, a);
+    WRing<16> r2;
+    wring_start(r2, wblocks<16, 16>(W2T, wave, 0, lane));
+    relu_grad_out(a[0], hv, B.g2, B.bp2 + (size_t)tile * HID, col, n, 32 * wave, lane);
+    load_tile_rows(B.h1, HID, col, n, 32 * wave, lane, hv);
+    __syncthreads();                               // every wave has read the g3 planes
+    store_planes_raw<HSC, HPC>(a[0], 32 * wave, s_g, lane);
+    __syncthreads();
+    zero_acc<1>(a);
+    mfma_rows<16, HSC, HPC, 1>(r2, wblocks<16, 16>(W2T, wave, 0, lane), s_g, 0, lane, a);
+    relu_grad_out(a[0], hv, B.g1, B.bp1 + (size_t)tile * HID, col, n, 32 * wave, lane);
+}
+
 // Keys of the A2C update's grouping of repeated inputs (a2c_vec.row_keys, the same hash): per
 // sample s = t * n + e of feats f32 [T][38][n], key a < 8 over actor a's 13 padded input columns
 // (its OBS_DIMS[a] a2c features, then zeros), key 8 over all 38; k = fmix64(k * MUL + bits(x_c)
@@ -918,6 +1049,22 @@ extern "C" int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* c
     if (!x || !critic_w || !h1 || !h2 || !h3 || !values) return fjsp_internal_fail("fjsp_a2c_critic_forward: null buffer");
     PolicyArgs A{x, nullptr, n, nullptr, critic_w, nullptr, 0u, 0u, 0, nullptr, values, nullptr, (n + TC - 1) / TC, 0};
     hipLaunchKernelGGL(k_critic_fwd, dim3((unsigned)A.nc), dim3(NTHR), 0, (hipStream_t)stream, A, CriticSave{h1, h2, h3});
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int fjsp_a2c_critic_backward(const float* g3, const float* h1, const float* h2, int32_t n, const float* w3t,
+                                        const float* w2t, float* g2, float* g1, float* bias_part2, float* bias_part1,
+                                        void* stream) {
+    if (n <= 0) return fjsp_internal_fail("fjsp_a2c_critic_backward: n must be > 0");
+    if (!g3 || !h1 || !h2 || !w3t || !w2t || !g2 || !g1 || !bias_part2 || !bias_part1)
+        return fjsp_internal_fail("fjsp_a2c_critic_backward: null buffer");
+    const CriticBwd B{g3, h1, h2, w3t, w2t, g2, g1, bias_part2, bias_part1, n};
+    hipLaunchKernelGGL(k_critic_bwd, dim3((unsigned)((n + TC - 1) / TC)), dim3(NTHR), 0, (hipStream_t)stream, B);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));
