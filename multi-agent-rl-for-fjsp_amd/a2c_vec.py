@@ -143,6 +143,23 @@ class _ValueHead(torch.autograd.Function):
         return gh, _splitk_wgrad(g, h), ps[:C], ps[C:2 * C].view(1, C), ps[2 * C:2 * C + 1]
 
 
+def critic_wgrad(g, x, feature_major=False, parts=256):
+    """gW = g^T x over a long batch on the matrix cores (fjsp_a2c_critic_wgrad): g f32 [S, m]
+    contiguous, x f32 [S, nx] contiguous or, feature_major, [nx, S] (the feature slab); the
+    kernel's per-workgroup partial sums are added here (a fixed order: deterministic)."""
+    S, m = g.shape
+    nx = x.shape[0] if feature_major else x.shape[1]
+    npad = 64 if feature_major else nx
+    parts = max(1, min(int(parts), -(-S // 32)))
+    part = torch.empty(parts, m, npad, dtype=torch.float32, device=g.device)
+    stream = torch.cuda.current_stream(g.device).cuda_stream
+    V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    nat.check(nat.lib().fjsp_a2c_critic_wgrad(V(g), m, V(x), nx, int(bool(feature_major)), S, V(part), parts,
+                                              ctypes.c_void_p(stream)))
+    gw = part.sum(0)
+    return gw[:, :nx] if npad != nx else gw
+
+
 def _relu_bias_grad(gy, y):
     """(gy where y > 0 else 0, its column sums) for y [B, C] = a ReLU output, gy [B, C]
     contiguous f32 on the GPU: fjsp_a2c_relu_bias_grad."""
@@ -160,7 +177,8 @@ class _CriticGrouped(torch.autograd.Function):
     on the GPU: the forward in one fused kernel (fjsp_a2c_critic_forward: f32 operands as bf16
     planes on the matrix cores, as the policy kernel's values), which also writes the hidden
     layers; the backward: the value-head kernel, both 256-wide ReLU layers' input gradients in one
-    kernel (fjsp_a2c_critic_backward, the same split arithmetic), split-K weight gradients.
+    kernel (fjsp_a2c_critic_backward, the same split arithmetic), split-K weight gradients
+    (hipBLASLt; fjsp_a2c_critic_wgrad on the matrix cores is opt-in).
     xT f32 [38, U] -> v [U]."""
 
     @staticmethod
@@ -190,7 +208,9 @@ class _CriticGrouped(torch.autograd.Function):
         V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         nat.check(nat.lib().fjsp_a2c_value_head_grad(V(h3), V(gvc), V(w4), B, V(g3), V(part), ctypes.c_void_p(stream)))
         ps = part.sum(0)
-        gW3 = _splitk_wgrad(g3, h2)
+        wg = critic_wgrad if critic_wgrad_fused else (lambda g, x, feature_major=False:   # noqa: E731
+                                                      _splitk_wgrad(g, x.t() if feature_major else x))
+        gW3 = wg(g3, h2)
         if critic_bwd_fused:
             # both 256-wide ReLU layers' input gradients in one pass (fjsp_a2c_critic_backward)
             w3t, w2t = pack_mfma(W3.t().contiguous()).reshape(-1), pack_mfma(W2.t().contiguous()).reshape(-1)
@@ -204,8 +224,8 @@ class _CriticGrouped(torch.autograd.Function):
         else:
             g2, gb2 = _relu_bias_grad((g3 @ W3).contiguous(), h2)
             g1, gb1 = _relu_bias_grad((g2 @ W2).contiguous(), h1)
-        gW2 = _splitk_wgrad(g2, h1)
-        gW1 = _splitk_wgrad(g1, xT.t())
+        gW2 = wg(g2, h1)
+        gW1 = wg(g1, xT, feature_major=True)
         return (None, gW1, gb1, gW2, gb2, gW3, ps[:C], ps[C:2 * C].view(1, C), ps[2 * C:2 * C + 1])
 
 
@@ -214,6 +234,9 @@ class _CriticGrouped(torch.autograd.Function):
 critic_fused = os.environ.get("FJSP_CRITIC_FUSED", "1") != "0"
 # its backward through the two 256-wide layers in one kernel (FJSP_CRITIC_BWD=0: GEMMs + ReLU kernels)
 critic_bwd_fused = os.environ.get("FJSP_CRITIC_BWD", "1") != "0"
+# its weight gradients on the matrix cores (fjsp_a2c_critic_wgrad, FJSP_CRITIC_WGRAD=1): opt-in, measured
+# slower than hipBLASLt's split-K GEMMs (1.6 ms against ~1 ms per update, profiles/r03/wgrad/)
+critic_wgrad_fused = os.environ.get("FJSP_CRITIC_WGRAD", "0") == "1"
 
 
 def critic_grouped(critic, xT):
