@@ -272,9 +272,8 @@ int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* critic_w, fl
  * critic_loss.backward(); a2c_vec._CriticGrouped): g3 f32 [n][128] (layer 3's pre-activation
  * gradient, fjsp_a2c_value_head_grad), h1 / h2 from fjsp_a2c_critic_forward, w3t / w2t = W3^T
  * [256][128] / W2^T [256][256] packed as the forward's weights -> g2 = (g3 W3) * [h2 > 0], g1 =
- * (g2 W2) * [h1 > 0] f32 [n][256] and their column sums per tile of 64 samples, bias_part2 /
- * bias_part1 f32 [ceil(n / 64)][256] (ABI 6; 32-sample tiles, [ceil(n / 32)][256], when the
- * environment sets FJSP_CRITIC_TILE=32).  Stream-ordered. */
+ * (g2 W2) * [h1 > 0] f32 [n][256] and their column sums per 32-sample tile, bias_part2 /
+ * bias_part1 f32 [ceil(n / 32)][256].  Stream-ordered. */
 int fjsp_a2c_critic_backward(const float* g3, const float* h1, const float* h2, int32_t n, const float* w3t,
                              const float* w2t, float* g2, float* g1, float* bias_part2, float* bias_part1, void* stream);
 /* The critic's weight gradients for the A2C update (a2c.py:692-699 critic_loss.backward(), the

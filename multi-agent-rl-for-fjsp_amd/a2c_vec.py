@@ -215,7 +215,7 @@ class _CriticGrouped(torch.autograd.Function):
             # both 256-wide ReLU layers' input gradients in one pass (fjsp_a2c_critic_backward)
             w3t, w2t = pack_mfma(W3.t().contiguous()).reshape(-1), pack_mfma(W2.t().contiguous()).reshape(-1)
             g2, g1 = torch.empty_like(h2), torch.empty_like(h1)
-            nt = -(-B // critic_tile())                # bias partials per sample tile of the kernels
+            nt = -(-B // 32)
             bp2 = torch.empty(nt, h2.shape[1], dtype=torch.float32, device=h2.device)
             bp1 = torch.empty(nt, h1.shape[1], dtype=torch.float32, device=h1.device)
             nat.check(nat.lib().fjsp_a2c_critic_backward(V(g3), V(h1), V(h2), B, V(w3t), V(w2t), V(g2), V(g1), V(bp2),
@@ -234,12 +234,6 @@ class _CriticGrouped(torch.autograd.Function):
 critic_fused = os.environ.get("FJSP_CRITIC_FUSED", "1") != "0"
 # its backward through the two 256-wide layers in one kernel (FJSP_CRITIC_BWD=0: GEMMs + ReLU kernels)
 critic_bwd_fused = os.environ.get("FJSP_CRITIC_BWD", "1") != "0"
-# samples per tile of the fused critic kernels (64; FJSP_CRITIC_TILE=32: the first version, for A/B runs;
-# libfjsp reads the same variable)
-def critic_tile():
-    return 32 if os.environ.get("FJSP_CRITIC_TILE", "64") == "32" else 64
-
-
 # its weight gradients on the matrix cores (fjsp_a2c_critic_wgrad, FJSP_CRITIC_WGRAD=1): opt-in, measured
 # slower than hipBLASLt's split-K GEMMs (1.6 ms against ~1 ms per update, profiles/r03/wgrad/)
 critic_wgrad_fused = os.environ.get("FJSP_CRITIC_WGRAD", "0") == "1"

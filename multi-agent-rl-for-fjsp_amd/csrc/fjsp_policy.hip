@@ -26,7 +26,6 @@
 // reference's greedy actions on its trained policy.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 #include "../../include/fjsp.h"
 #include "fjsp_stamps.h"
@@ -233,49 +232,6 @@ __device__ __forceinline__ void store_rows_f32(const f32x16& acc, int row0, cons
     }
 }
 
-// acc as is (already activated) -> the same rows of the sample-major f32 matrix
-__device__ __forceinline__ void store_rows_raw(const f32x16& acc, int row0, float* __restrict__ out, int ld, int col0,
-                                               int n, int lane) {
-    const int col = col0 + (lane & 31);
-    if (col >= n) return;
-#pragma unroll
-    for (int g = 0; g < 4; g++)
-        *reinterpret_cast<float4*>(out + (size_t)col * ld + row0 + 8 * g + 4 * (lane >> 5)) =
-            make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
-}
-
-// a tile's f32 gradient (rows row0.., the C/D layout) -> bf16 planes [NP][TC][ST] (no ReLU, no bias)
-template <int ST, int PL>
-__device__ __forceinline__ void store_planes_raw(const f32x16& acc, int k0, __bf16* out, int lane, int col0 = 0) {
-    const int col = col0 + (lane & 31);
-#pragma unroll
-    for (int g = 0; g < 4; g++) {
-        const int k = k0 + 8 * g + 4 * (lane >> 5);
-        bf16x4 ph, pm, pl;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            __bf16 x0, x1, x2;
-            split3(acc[4 * g + i], x0, x1, x2);
-            ph[i] = x0;
-            pm[i] = x1;
-            pl[i] = x2;
-        }
-        *reinterpret_cast<bf16x4*>(out + col * ST + k) = ph;
-        *reinterpret_cast<bf16x4*>(out + PL + col * ST + k) = pm;
-        *reinterpret_cast<bf16x4*>(out + 2 * PL + col * ST + k) = pl;
-    }
-}
-// this lane's 16 values of rows row0.. (C/D layout) at sample column col of a sample-major
-// [n][ld] f32 matrix (0 past n)
-__device__ __forceinline__ void load_tile_rows(const float* __restrict__ m, int ld, int col, int n, int row0, int lane,
-                                               float v[16]) {
-#pragma unroll
-    for (int g = 0; g < 4; g++) {
-        float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (col < n) q = *reinterpret_cast<const float4*>(m + (size_t)col * ld + row0 + 8 * g + 4 * (lane >> 5));
-        v[4 * g] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
-    }
-}
 // The logits' partial sums of this wave's 32 rows of h2 = relu(acc + b2) (rows of the C/D
 // layout) for NA actions -> s_part[wave][j][env]: per lane its 16 rows, then the other
 // half-wave's 16 (lane ^ 32).  Actions in chunks of up to 4 (all 8 at once spilled at 128 VGPRs).
@@ -602,125 +558,6 @@ k_critic_fwd(PolicyArgs A, CriticSave sv) {
     critic_tile<true>(A, (int)blockIdx.x, s_mem, tid, lane, wave, sv);
 }
 
-// The same forward on tiles of 64 samples (the update's default): every weight fragment loaded
-// feeds two MFMAs (the two 32-sample column tiles), so a tile's 0.66 MB of split weights is
-// fetched once per 64 samples instead of per 32 (the 32-sample kernel above read ~17 GB from L2
-// per update).  Layers 2 and 3 are each summed over two K halves of their input, so one half
-// buffer [NP][64][128 + 8] serves both (as actor_tile's layer 2) and two workgroups fit a CU;
-// every wave owns 32 rows of layer 2 x 64 samples and one 32 x 32 tile of layer 3 (the
-// 32-sample kernel ran layer 3 on four of its eight waves).
-constexpr int XSC64 = C_DPAD + 8, XPC64 = 64 * XSC64;
-constexpr int CF64_LDS = NP * XPC64 * 2 + NP * HPA * 2;
-static_assert(2 * CF64_LDS <= 160 * 1024 && 4 * 64 * 4 <= NP * XPC64 * 2, "critic fwd64 LDS");
-__global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)))
-k_critic_fwd64(PolicyArgs A, CriticSave sv) {
-    __shared__ __attribute__((aligned(16))) unsigned char s_mem[CF64_LDS];
-    __bf16* s_x = reinterpret_cast<__bf16*>(s_mem);                    // inputs [NP][64][XSC64]
-    __bf16* s_h = reinterpret_cast<__bf16*>(s_mem + NP * XPC64 * 2);   // a half of h1, then of h2 [NP][64][HSA]
-    float* s_part = reinterpret_cast<float*>(s_mem);                   // value partials [4][64] (after layer 1)
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int n = A.n, e0 = (int)blockIdx.x * 64;
-    const float* wb = A.critic_w;
-    const bf16x8* W1 = reinterpret_cast<const bf16x8*>(wb);
-    const float* B1 = wb + NP * HID * C_DPAD / 2;
-    const bf16x8* W2 = reinterpret_cast<const bf16x8*>(B1 + HID);
-    const float* B2 = B1 + HID + NP * HID * HID / 2;
-    const bf16x8* W3 = reinterpret_cast<const bf16x8*>(B2 + HID);
-    const float* B3 = B2 + HID + NP * 128 * HID / 2;
-    const float* W4 = B3 + 128;
-    const float* B4 = W4 + 128;
-    constexpr int KB1 = C_DPAD / 16;
-    constexpr int XI64 = C_DPAD * 64 / NTHR;
-    {   // inputs: 38 feature rows, zero-padded to C_DPAD, 64 samples -> bf16 planes
-        float v[XI64];
-#pragma unroll
-        for (int q = 0; q < XI64; q++) {
-            const int i = tid + q * NTHR, k = i / 64, c = i % 64;
-            v[q] = (k < 38 && e0 + c < n) ? A.feats[(size_t)k * n + e0 + c] : 0.0f;
-        }
-#pragma unroll
-        for (int q = 0; q < XI64; q++) {
-            const int i = tid + q * NTHR, k = i / 64, c = i % 64;
-            __bf16 x0, x1, x2;
-            split3(v[q], x0, x1, x2);
-            s_x[c * XSC64 + k] = x0;
-            s_x[XPC64 + c * XSC64 + k] = x1;
-            s_x[2 * XPC64 + c * XSC64 + k] = x2;
-        }
-    }
-    const int rt1 = wave & 3, ct1 = wave >> 2;   // layer-1 tile of each half; layer 3's tile
-    WRing<KB1> r1;
-    wring_start(r1, wblocks<KB1, KB1>(W1, rt1, 0, lane));
-    Row16 b1 = load_rows(B1, 32 * rt1, lane);
-    __syncthreads();
-    f32x16 acc[2];
-    zero_acc<2>(acc);
-#pragma unroll
-    for (int half = 0; half < 2; half++) {
-        f32x16 a1[1];
-        zero_acc<1>(a1);
-        mfma_rows<KB1, XSC64, XPC64, 1>(r1, wblocks<KB1, KB1>(W1, 4 * half + rt1, 0, lane), s_x, 32 * ct1, lane, a1);
-        WRing<HID / 32> r2;
-        wring_start(r2, wblocks<HID / 32, HID / 16>(W2, wave, 8 * half, lane));
-        store_planes<HSA, HPA>(a1[0], 32 * rt1, 32 * ct1, b1, s_h, lane);
-        store_rows_f32(a1[0], 128 * half + 32 * rt1, b1, sv.h1, HID, e0 + 32 * ct1, n, lane);
-        __syncthreads();
-        mfma_rows<HID / 32, HSA, HPA, 2>(r2, wblocks<HID / 32, HID / 16>(W2, wave, 8 * half, lane), s_h, 0, lane, acc);
-        if (half == 0) {
-            wring_start(r1, wblocks<KB1, KB1>(W1, 4 + rt1, 0, lane));
-            b1 = load_rows(B1, 128 + 32 * rt1, lane);
-        }
-        __syncthreads();                           // every wave has read this half
-    }
-    {   // h2 = relu(acc + b2) in place (the same values store_planes would form)
-        const Row16 b2 = load_rows(B2, 32 * wave, lane);
-#pragma unroll
-        for (int c = 0; c < 2; c++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) acc[c][r] = relu(acc[c][r] + b2[r]);
-    }
-#pragma unroll
-    for (int c = 0; c < 2; c++) store_rows_raw(acc[c], 32 * wave, sv.h2, HID, e0 + 32 * c, n, lane);
-    f32x16 a3[1];
-    zero_acc<1>(a3);
-#pragma unroll
-    for (int half = 0; half < 2; half++) {
-        WRing<HID / 32> r3;
-        wring_start(r3, wblocks<HID / 32, HID / 16>(W3, rt1, 8 * half, lane));
-        if ((wave >> 2) == half) {   // this half of h2 (rows 128 half ..), read back from HBM: the
-                                     // accumulators held through half 0 spilled
-#pragma unroll
-            for (int c = 0; c < 2; c++) {
-                f32x16 t;
-                float v[16];
-                load_tile_rows(sv.h2, HID, e0 + 32 * c + (lane & 31), n, 32 * wave, lane, v);
-#pragma unroll
-                for (int r = 0; r < 16; r++) t[r] = v[r];
-                store_planes_raw<HSA, HPA>(t, 32 * rt1, s_h, lane, 32 * c);
-            }
-        }
-        __syncthreads();
-        mfma_rows<HID / 32, HSA, HPA, 1>(r3, wblocks<HID / 32, HID / 16>(W3, rt1, 8 * half, lane), s_h, 32 * ct1, lane,
-                                         a3);
-        __syncthreads();                           // every wave has read this half
-    }
-    const Row16 b3 = load_rows(B3, 32 * rt1, lane), w4 = load_rows(W4, 32 * rt1, lane);
-    store_rows_f32(a3[0], 32 * rt1, b3, sv.h3, 128, e0 + 32 * ct1, n, lane);
-    float v = 0.0f;
-#pragma unroll
-    for (int r = 0; r < 16; r++) v = fmaf(w4[r], relu(a3[0][r] + b3[r]), v);
-    v += __shfl_xor(v, 32);
-    if (lane < 32) s_part[rt1 * 64 + 32 * ct1 + lane] = v;
-    __syncthreads();
-    if (tid < 64 && e0 + tid < n) {
-        float val = B4[0];
-#pragma unroll
-        for (int w = 0; w < 4; w++) val += s_part[w * 64 + tid];
-        A.values[e0 + tid] = val;
-    }
-}
-
 // The critic's backward through layers 3 and 2 for the A2C update (a2c_vec._CriticGrouped): on a
 // tile of 32 samples, g2 = (g3 W3) * [h2 > 0] and g1 = (g2 W2) * [h1 > 0], the input gradients of
 // the two 256-wide ReLU layers, with W3^T / W2^T packed like the forward's weights and the
@@ -741,6 +578,17 @@ struct CriticBwd {
 };
 constexpr int GS3 = 128 + 8;   // bf16 stride of the g3 planes [NP][TC][GS3]
 static_assert(NP * TC * GS3 * 2 <= H_BYTES && NP * HPC * 2 <= H_BYTES, "backward planes");
+// this lane's 16 values of rows row0.. (C/D layout) at sample column col of a sample-major
+// [n][ld] f32 matrix (0 past n)
+__device__ __forceinline__ void load_tile_rows(const float* __restrict__ m, int ld, int col, int n, int row0, int lane,
+                                               float v[16]) {
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (col < n) q = *reinterpret_cast<const float4*>(m + (size_t)col * ld + row0 + 8 * g + 4 * (lane >> 5));
+        v[4 * g] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
+    }
+}
 // g = acc * [h > 0] -> HBM (sample-major [n][256]) and, for the tile's 32 samples, the column
 // sums into bp[row] (lanes 0 / 32 after a butterfly over each half-wave)
 __device__ __forceinline__ void relu_grad_out(f32x16& acc, const float h[16], float* __restrict__ g, float* __restrict__ bp,
@@ -765,6 +613,27 @@ __device__ __forceinline__ void relu_grad_out(f32x16& acc, const float h[16], fl
         for (int q = 0; q < 4; q++)
             *reinterpret_cast<float4*>(bp + row0 + 8 * q + 4 * (lane >> 5)) =
                 make_float4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
+    }
+}
+// a tile's f32 gradient (rows row0.., the C/D layout) -> bf16 planes [NP][TC][ST] (no ReLU, no bias)
+template <int ST, int PL>
+__device__ __forceinline__ void store_planes_raw(const f32x16& acc, int k0, __bf16* out, int lane) {
+    const int col = lane & 31;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const int k = k0 + 8 * g + 4 * (lane >> 5);
+        bf16x4 ph, pm, pl;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            __bf16 x0, x1, x2;
+            split3(acc[4 * g + i], x0, x1, x2);
+            ph[i] = x0;
+            pm[i] = x1;
+            pl[i] = x2;
+        }
+        *reinterpret_cast<bf16x4*>(out + col * ST + k) = ph;
+        *reinterpret_cast<bf16x4*>(out + PL + col * ST + k) = pm;
+        *reinterpret_cast<bf16x4*>(out + 2 * PL + col * ST + k) = pl;
     }
 }
 __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) k_critic_bwd(CriticBwd B) {
@@ -931,122 +800,6 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2)
 #pragma unroll
         for (int r = 0; r < 16; r++) out[(32 * rt + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * NPAD + col] = acc[c][r];
     }
-}
-
-// The same backward on tiles of 64 samples (the update's default, with k_critic_fwd64): each
-// weight fragment feeds two MFMAs; layer 2's input gradient is summed over two K halves of g2
-// (rows 0..127 from waves 0..3, then 128..255 from waves 4..7) through one half buffer.  g2 / g1
-// equal the 32-sample kernel's bit for bit (the same MFMA order per tile); the bias partials are
-// per 64 samples, bias_part[ceil(n / 64)][256].
-// g = acc * [h > 0] for the two column tiles -> HBM, and their column sums over the 64 samples
-__device__ __forceinline__ uint32_t relu_bits(const float h[16]) {
-    uint32_t m = 0;
-#pragma unroll
-    for (int r = 0; r < 16; r++) m |= (h[r] > 0.0f ? 1u : 0u) << r;
-    return m;
-}
-__device__ __forceinline__ void relu_grad_out2(f32x16 acc[2], const uint32_t hm[2], float* __restrict__ g,
-                                               float* __restrict__ bp, int col0, int n, int row0, int lane) {
-    float t[16];
-#pragma unroll
-    for (int c = 0; c < 2; c++) {
-        const int col = col0 + 32 * c + (lane & 31);
-#pragma unroll
-        for (int r = 0; r < 16; r++) acc[c][r] = ((hm[c] >> r) & 1u) ? acc[c][r] : 0.0f;
-        if (col < n) {
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                *reinterpret_cast<float4*>(g + (size_t)col * HID + row0 + 8 * q + 4 * (lane >> 5)) =
-                    make_float4(acc[c][4 * q], acc[c][4 * q + 1], acc[c][4 * q + 2], acc[c][4 * q + 3]);
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < 16; r++) t[r] = acc[0][r] + acc[1][r];   // columns past n are 0 (h loaded as 0)
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1)
-#pragma unroll
-        for (int r = 0; r < 16; r++) t[r] += __shfl_xor(t[r], o);
-    if ((lane & 31) == 0) {
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            *reinterpret_cast<float4*>(bp + row0 + 8 * q + 4 * (lane >> 5)) =
-                make_float4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
-    }
-}
-__global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) k_critic_bwd64(CriticBwd B) {
-    __shared__ __attribute__((aligned(16))) __bf16 s_g[NP * 64 * GS3];   // g3 planes, then a half of g2 [NP][64][HSA]
-    static_assert(GS3 == HSA, "one buffer for both");
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int tile = blockIdx.x, e0 = tile * 64, n = B.n;
-    const bf16x8* W3T = reinterpret_cast<const bf16x8*>(B.w3t);
-    const bf16x8* W2T = reinterpret_cast<const bf16x8*>(B.w2t);
-    WRing<8> r3;
-    wring_start(r3, wblocks<8, 8>(W3T, wave, 0, lane));
-    float hv[2][16];
-#pragma unroll
-    for (int c = 0; c < 2; c++) load_tile_rows(B.h2, HID, e0 + 32 * c + (lane & 31), n, 32 * wave, lane, hv[c]);
-    // g3 [64 samples][128] -> planes: item i = sample i / 16, 8 consecutive features
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-        const int i = tid + q * NTHR, sl = i >> 4, f0 = (i & 15) * 8, c = e0 + sl;
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = 0.0f;
-        if (c < n) {
-            const float4 a = *reinterpret_cast<const float4*>(B.g3 + (size_t)c * 128 + f0);
-            const float4 b = *reinterpret_cast<const float4*>(B.g3 + (size_t)c * 128 + f0 + 4);
-            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        }
-        bf16x8 ph, pm, pl;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            __bf16 x0, x1, x2;
-            split3(v[j], x0, x1, x2);
-            ph[j] = x0;
-            pm[j] = x1;
-            pl[j] = x2;
-        }
-        constexpr int PL3 = 64 * GS3;
-        *reinterpret_cast<bf16x8*>(s_g + sl * GS3 + f0) = ph;
-        *reinterpret_cast<bf16x8*>(s_g + PL3 + sl * GS3 + f0) = pm;
-        *reinterpret_cast<bf16x8*>(s_g + 2 * PL3 + sl * GS3 + f0) = pl;
-    }
-    __syncthreads();
-    uint32_t hm[2];   // the ReLU masks as bits (16 registers each as floats: the MFMAs below spilled)
-#pragma unroll
-    for (int c = 0; c < 2; c++) hm[c] = relu_bits(hv[c]);
-    f32x16 a[2];
-    zero_acc<2>(a);
-    mfma_rows<8, GS3, 64 * GS3, 2>(r3, wblocks<8, 8>(W3T, wave, 0, lane), s_g, 0, lane, a);
-    relu_grad_out2(a, hm, B.g2, B.bp2 + (size_t)tile * HID, e0, n, 32 * wave, lane);
-    f32x16 a1[2];
-    zero_acc<2>(a1);
-#pragma unroll
-    for (int half = 0; half < 2; half++) {
-        WRing<HID / 32> r2;
-        wring_start(r2, wblocks<HID / 32, HID / 16>(W2T, wave, 8 * half, lane));
-        __syncthreads();                           // every wave has read the g3 planes / the previous half
-        if ((wave >> 2) == half) {   // this half of g2, read back from HBM (held in registers it spilled)
-#pragma unroll
-            for (int c = 0; c < 2; c++) {
-                f32x16 t;
-                float v[16];
-                load_tile_rows(B.g2, HID, e0 + 32 * c + (lane & 31), n, 32 * wave, lane, v);
-#pragma unroll
-                for (int r = 0; r < 16; r++) t[r] = v[r];
-                store_planes_raw<HSA, HPA>(t, 32 * (wave & 3), s_g, lane, 32 * c);
-            }
-        }
-        __syncthreads();
-        mfma_rows<HID / 32, HSA, HPA, 2>(r2, wblocks<HID / 32, HID / 16>(W2T, wave, 8 * half, lane), s_g, 0, lane, a1);
-    }
-#pragma unroll
-    for (int c = 0; c < 2; c++) {
-        load_tile_rows(B.h1, HID, e0 + 32 * c + (lane & 31), n, 32 * wave, lane, hv[c]);
-        hm[c] = relu_bits(hv[c]);
-    }
-    relu_grad_out2(a1, hm, B.g1, B.bp1 + (size_t)tile * HID, e0, n, 32 * wave, lane);
 }
 
 // Keys of the A2C update's grouping of repeated inputs (a2c_vec.row_keys, the same hash): per
@@ -1403,23 +1156,12 @@ extern "C" int fjsp_debug_policy_stamps(unsigned long long* out, int32_t clear) 
 }
 #endif
 
-// Sample tile of the update's critic kernels: 64 (default) or 32 (FJSP_CRITIC_TILE=32, the r03 first
-// version, for A/B runs; a2c_vec reads the same variable for the bias partials' row count).
-static int critic_tile_samples() {
-    const char* v = getenv("FJSP_CRITIC_TILE");   // read per call: a test compares both in one process
-    return (v && atoi(v) == 32) ? 32 : 64;
-}
-
 extern "C" int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* critic_w, float* h1, float* h2,
                                        float* h3, float* values, void* stream) {
     if (n <= 0) return fjsp_internal_fail("fjsp_a2c_critic_forward: n must be > 0");
     if (!x || !critic_w || !h1 || !h2 || !h3 || !values) return fjsp_internal_fail("fjsp_a2c_critic_forward: null buffer");
     PolicyArgs A{x, nullptr, n, nullptr, critic_w, nullptr, 0u, 0u, 0, nullptr, values, nullptr, (n + TC - 1) / TC, 0};
-    if (critic_tile_samples() == 64)
-        hipLaunchKernelGGL(k_critic_fwd64, dim3((unsigned)((n + 63) / 64)), dim3(NTHR), 0, (hipStream_t)stream, A,
-                           CriticSave{h1, h2, h3});
-    else
-        hipLaunchKernelGGL(k_critic_fwd, dim3((unsigned)A.nc), dim3(NTHR), 0, (hipStream_t)stream, A, CriticSave{h1, h2, h3});
+    hipLaunchKernelGGL(k_critic_fwd, dim3((unsigned)A.nc), dim3(NTHR), 0, (hipStream_t)stream, A, CriticSave{h1, h2, h3});
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));
@@ -1435,10 +1177,7 @@ extern "C" int fjsp_a2c_critic_backward(const float* g3, const float* h1, const 
     if (!g3 || !h1 || !h2 || !w3t || !w2t || !g2 || !g1 || !bias_part2 || !bias_part1)
         return fjsp_internal_fail("fjsp_a2c_critic_backward: null buffer");
     const CriticBwd B{g3, h1, h2, w3t, w2t, g2, g1, bias_part2, bias_part1, n};
-    if (critic_tile_samples() == 64)
-        hipLaunchKernelGGL(k_critic_bwd64, dim3((unsigned)((n + 63) / 64)), dim3(NTHR), 0, (hipStream_t)stream, B);
-    else
-        hipLaunchKernelGGL(k_critic_bwd, dim3((unsigned)((n + TC - 1) / TC)), dim3(NTHR), 0, (hipStream_t)stream, B);
+    hipLaunchKernelGGL(k_critic_bwd, dim3((unsigned)((n + TC - 1) / TC)), dim3(NTHR), 0, (hipStream_t)stream, B);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

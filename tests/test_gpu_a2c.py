@@ -534,44 +534,3 @@ def test_critic_wgrad_kernel_matches_float64(M, m, nx, fm, S):
     et = float(((g.t() @ (x.t() if fm else x)).double() - ref).norm() / ref.norm())
     assert e <= max(3 * et, 2e-6), (e, et)
     assert torch.equal(gw, A.critic_wgrad(g, x, feature_major=fm))
-
-
-def test_critic_kernels_64_sample_tiles_equal_32(M, monkeypatch):
-    """The update's critic forward / backward on 64-sample tiles (default) against the 32-sample
-    kernels (FJSP_CRITIC_TILE=32): the same MFMA order per 32 x 32 tile, so hidden layers, values
-    and both input gradients are bit-identical; the bias partials are per 64 samples and their
-    sums agree to f32 rounding.  A ragged count (70 001 = 1 093 x 64 + 49)."""
-    import ctypes
-    A = M["A"]
-    nat = importlib.import_module("multi-agent-rl-for-fjsp_amd._native")
-    torch.manual_seed(7)
-    _, critic = A.init_networks(seed=2, device="cuda")
-    U = 70001
-    xT = (torch.rand(38, U, device="cuda") * torch.randint(0, 30, (38, 1), device="cuda")).float().contiguous()
-    n_ = critic.net
-    cw = A.pack_critic_weights(n_[0].weight, n_[0].bias, n_[2].weight, n_[2].bias, n_[4].weight, n_[4].bias,
-                               n_[6].weight, n_[6].bias)
-    w3t = A.pack_mfma(n_[4].weight.detach().t().contiguous()).reshape(-1)
-    w2t = A.pack_mfma(n_[2].weight.detach().t().contiguous()).reshape(-1)
-    g3 = torch.randn(U, 128, device="cuda")
-    V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    out = {}
-    for tile in (32, 64):
-        monkeypatch.setenv("FJSP_CRITIC_TILE", str(tile))
-        h = [torch.empty(U, 256, device="cuda"), torch.empty(U, 256, device="cuda"), torch.empty(U, 128, device="cuda")]
-        v = torch.empty(U, device="cuda")
-        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        nat.check(nat.lib().fjsp_a2c_critic_forward(V(xT), U, V(cw), V(h[0]), V(h[1]), V(h[2]), V(v), st))
-        nt = -(-U // tile)
-        g2, g1 = torch.empty(U, 256, device="cuda"), torch.empty(U, 256, device="cuda")
-        b2, b1 = torch.empty(nt, 256, device="cuda"), torch.empty(nt, 256, device="cuda")
-        nat.check(nat.lib().fjsp_a2c_critic_backward(V(g3), V(h[0]), V(h[1]), U, V(w3t), V(w2t), V(g2), V(g1), V(b2),
-                                                     V(b1), st))
-        torch.cuda.synchronize()
-        out[tile] = (h, v, g2, g1, b2.double().sum(0), b1.double().sum(0))
-    a, b = out[32], out[64]
-    for x, y in zip(a[0], b[0]):
-        assert torch.equal(x, y)
-    assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
-    for x, y in zip(a[4:], b[4:]):
-        assert float((x - y).abs().max() / x.abs().max()) < 1e-5
