@@ -631,8 +631,8 @@ def _run_sums(g, gy):
     """gy [R, C, S] per sample -> [R, C, Umax] per group of the RowGroups g: runs of the sorted
     order summed (an f64 prefix sum differenced at the run ends)."""
     R, C, S = gy.shape
-    cs = _prefix_sum(torch.gather(gy, 2, g.perm[:, None, :].expand(R, C, S)).double())
-    ce = torch.gather(cs, 2, (g.ends - 1)[:, None, :].expand(R, C, g.ends.shape[1]))
+    ce = _prefix_at(torch.gather(gy, 2, g.perm[:, None, :].expand(R, C, S)),
+                    (g.ends - 1)[:, None, :].expand(R, C, g.ends.shape[1]))
     return torch.cat([ce[..., :1], ce[..., 1:] - ce[..., :-1]], dim=-1).to(gy.dtype)
 
 
@@ -673,8 +673,7 @@ class _ActorHead(torch.autograd.Function):
             torch.gather(grad[o:o + k], 1, g.perm[a].expand(k, S), out=srt[o:o + k])
         row_agent = _index_tensor(tuple(a for a in range(NA) for _ in range(N_ACTIONS[a])), grad.device)
         srt.mul_(gl.to(grad.dtype)[row_agent, None])
-        cs = _prefix_sum(srt.double())
-        ce = torch.gather(cs, 1, (g.ends - 1)[row_agent])
+        ce = _prefix_at(srt, (g.ends - 1)[row_agent])
         rs = torch.cat([ce[:, :1], ce[:, 1:] - ce[:, :-1]], dim=1).to(grad.dtype)    # [29, Umax]
         out = torch.zeros(NA * 8, umax, dtype=grad.dtype, device=grad.device)
         out[_valid_rows(grad.device)] = rs
@@ -710,6 +709,20 @@ def _valid_rows(device):
         _VALID_ROWS[device] = torch.tensor([a * 8 + j for a in range(NA) for j in range(N_ACTIONS[a])],
                                            device=device)
     return _VALID_ROWS[device]
+
+
+def _prefix_at(w, idx, block=1024):
+    """The f64 inclusive prefix sums of w [..., S] along the last dim at positions idx [..., K]
+    only: _prefix_sum(w.double()) gathered at idx, bit for bit (the same block scans, the same
+    block offsets added), without casting w to f64 in a pass of its own (the scan casts) or
+    adding the block offsets to all S sums (only the K gathered ones)."""
+    *lead, S = w.shape
+    P = -(-S // block) * block
+    wp = w if P == S else torch.nn.functional.pad(w, (0, P - S))
+    c = wp.reshape(*lead, P // block, block).cumsum(-1, dtype=torch.float64)
+    tot = c[..., -1]
+    off = tot.cumsum(-1) - tot                                   # exclusive block offsets
+    return torch.gather(c.view(*lead, P), -1, idx) + torch.gather(off, -1, idx // block)
 
 
 def _prefix_sum(w, block=1024):

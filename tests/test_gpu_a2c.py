@@ -534,3 +534,14 @@ def test_critic_wgrad_kernel_matches_float64(M, m, nx, fm, S):
     et = float(((g.t() @ (x.t() if fm else x)).double() - ref).norm() / ref.norm())
     assert e <= max(3 * et, 2e-6), (e, et)
     assert torch.equal(gw, A.critic_wgrad(g, x, feature_major=fm))
+
+
+def test_prefix_at_equals_full_prefix_sum_on_gpu(M):
+    """_prefix_at (the run sums' prefix values at the run ends only, the f64 cast inside the scan)
+    is bit-identical to the full f64 prefix sum gathered at the same positions, on the GPU's scan."""
+    A = M["A"]
+    torch.manual_seed(11)
+    for S in (1048576, 70001):
+        w = torch.randn(29, S, device="cuda")
+        idx = torch.sort(torch.randint(0, S, (29, 4000), device="cuda"), -1).values
+        assert torch.equal(torch.gather(A._prefix_sum(w.double()), -1, idx), A._prefix_at(w, idx))
