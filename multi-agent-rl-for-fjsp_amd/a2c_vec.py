@@ -553,12 +553,13 @@ class RowGroups:
         perm = (fperm.view(R, S) - torch.arange(R, device=dev, dtype=torch.int64)[:, None] * S)
         new = torch.ones(R, S, dtype=torch.bool, device=dev)
         new[:, 1:] = sk[:, 1:] != sk[:, :-1]
-        seg = _prefix_sum(new.to(torch.int64)) - 1
+        seg = _prefix_sum(new, dtype=torch.int64, add=-1).contiguous()   # each sorted position's group
         self.U = (seg[:, -1] + 1).tolist()                        # the one host sync
         umax = bucket(max(self.U))
-        idx = torch.where(new, seg, torch.full_like(seg, umax))
-        pos = torch.arange(S, device=dev).expand(R, S)
-        starts = torch.full((R, umax + 1), S, dtype=torch.int64, device=dev).scatter_(1, idx, pos)[:, :umax]
+        # each group's first sorted position (S for padding groups): a binary search of the
+        # non-decreasing seg (a scatter of every position's group start sent ~10^7 stores of the
+        # non-first positions to one sink column)
+        starts = torch.searchsorted(seg, torch.arange(umax, device=dev).expand(R, umax).contiguous())
         self.ends = torch.cat([starts[:, 1:], torch.full((R, 1), S, dtype=torch.int64, device=dev)], 1)
         self.first = torch.gather(perm, 1, starts.clamp(max=S - 1))
         self.inv = torch.empty_like(perm).scatter_(1, perm, seg)
@@ -725,15 +726,18 @@ def _prefix_at(w, idx, block=1024):
     return torch.gather(c.view(*lead, P), -1, idx) + torch.gather(off, -1, idx // block)
 
 
-def _prefix_sum(w, block=1024):
-    """Inclusive prefix sum along the last dim, blocked so every scan runs over many short
-    rows (a scan over a few 10^6-long rows is one slow row per row)."""
+def _prefix_sum(w, block=1024, dtype=None, add=0):
+    """Inclusive prefix sum along the last dim (in dtype, + add), blocked so every scan runs over
+    many short rows (a scan over a few 10^6-long rows is one slow row per row)."""
     *lead, S = w.shape
     P = -(-S // block) * block
-    wp = w if P == S else torch.nn.functional.pad(w, (0, P - S))
-    c = wp.reshape(*lead, P // block, block).cumsum(-1)
+    wp = w if P == S else torch.nn.functional.pad(w if dtype is None else w.to(dtype), (0, P - S))
+    c = wp.reshape(*lead, P // block, block).cumsum(-1, dtype=dtype)
     tot = c[..., -1]
-    c = c + (tot.cumsum(-1) - tot)[..., None]
+    off = tot.cumsum(-1) - tot
+    if add:
+        off = off + add
+    c = c + off[..., None]
     return c.view(*lead, P)[..., :S]
 
 
