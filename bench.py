@@ -40,7 +40,9 @@ HBM_PEAK_GBS = 8000.0                     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU).  Under torch.distributed.run it must equal WORLD_SIZE; "
+                         "without it, N > 1 starts N rank processes itself (launch_ranks)")
     ap.add_argument("--steps", type=int, default=None, help="bench steps: default 20 rollout batches (step) / 4 A2C batches (a2c)")
     ap.add_argument("--warmup", type=int, default=None, help="default 5 rollout batches (step) / 3 A2C batches (a2c)")
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
@@ -188,6 +190,7 @@ def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    check_faults(env)
     if dist:
         t = torch.tensor([elapsed, tc], device=env.device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -223,9 +226,46 @@ def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=
     return out
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` (N > 1) outside a torch.distributed.run environment: start N fresh rank
+    processes through torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) with this
+    script's own arguments, relay their output (rank 0 prints the JSON line) and return their
+    exit code.  Runs before this process makes any GPU call; the ranks are children, never an
+    exec of this process."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def check_faults(env):
+    """A bounded hand-off wait that gave up leaves its envs' outputs invalid (fjsp_faults bit 0):
+    a number measured over them is not reported."""
+    w = env.faults()
+    if w:
+        raise SystemExit(f"bench: the step kernels reported fault word {w:#x} "
+                         "(a hand-off wait gave up); no value reported")
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus is not None and args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus))
+    elif args.gpus is not None and args.gpus != int(env_world):
+        sys.exit(f"bench: --gpus {args.gpus} but WORLD_SIZE={env_world}")
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -307,6 +347,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    check_faults(env)
     if dist:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

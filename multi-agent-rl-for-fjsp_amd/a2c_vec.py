@@ -1202,6 +1202,10 @@ class VecMultiAgentA2C:
         optimisers stay at their initial state), so a run that later switches to "allreduce"
         or resumes an optimiser must take it from the learner rank."""
         from . import distributed as D
+        fw = self.env.faults()             # synchronises; the update has host syncs of its own
+        if fw:
+            raise RuntimeError(f"fjsp step kernels reported fault word {fw:#x} (a hand-off wait gave up): "
+                               "the batch's transitions are invalid")
         res = None
         if self.exchange == "gather" and D.active(self.group):
             al, cl = self._update_gathered()

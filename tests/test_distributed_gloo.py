@@ -118,6 +118,9 @@ class _CpuEnv:
         self.num_envs = n
         self.env_id_base = base
 
+    def faults(self, clear=False):
+        return 0
+
 
 def _gae_cpu(rewards, values, done, gamma, lamb, use_gae=True):
     """transition_memory.py:83-105 in torch fp64 (test stand-in for the GAE kernel)."""
