@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define FJSP_ABI_VERSION 6
+#define FJSP_ABI_VERSION 7
 
 #define FJSP_NUM_AGENTS 8      /* pickup, agv, small, big, pkg_blue_1, pkg_blue_2, pkg_red, pkg_green */
 #define FJSP_OBS_I32 20        /* pickup 7 + agv 13 (position = 2) int32 observation fields */
@@ -218,6 +218,13 @@ int fjsp_mt_set(fjsp_handle* h, int32_t env, const uint32_t* key, int32_t pos);
 int fjsp_gae_f64(const double* rewards, const double* values, const uint8_t* done, const double* boot,
                  int32_t T, int32_t N, int32_t M, double gamma, double lamb, double* ret, double* adv,
                  void* hip_stream);
+/* The same scan with one value per env shared by its agents (the batched A2C: every agent's memory
+ * holds the critic's value of the env's global state, a2c.py:300-310,321-332): values f32
+ * [T + 1][N], row T = the bootstrap value after t = T-1; rewards / ret / adv f64 [T][agents * N],
+ * columns m = a*N + e.  Bit-identical to fjsp_gae with values[t][a*N + e] = values[t][e] and
+ * boot[a*N + e] = (double)values[T][e]. */
+int fjsp_gae_shared(const double* rewards, const float* values, const uint8_t* done, int32_t T, int32_t N,
+                    int32_t agents, double gamma, double lamb, double* ret, double* adv, void* hip_stream);
 
 /* Synchronous host copy of one env's state summary (debug / facade use). */
 int fjsp_read_env(fjsp_handle* h, int32_t env, fjsp_env_view* out);
@@ -276,16 +283,6 @@ int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* critic_w, fl
  * bias_part1 f32 [ceil(n / 32)][256].  Stream-ordered. */
 int fjsp_a2c_critic_backward(const float* g3, const float* h1, const float* h2, int32_t n, const float* w3t,
                              const float* w2t, float* g2, float* g1, float* bias_part2, float* bias_part1, void* stream);
-/* The critic's weight gradients for the A2C update (a2c.py:692-699 critic_loss.backward(), the
- * nn.Linear weight gradients gW = g^T x over the batch; a2c_vec._CriticGrouped): g f32
- * [samples][m] (a layer's pre-activation gradient), x its input: sample-major f32 [samples][nx]
- * (x_feature_major = 0; m 256 or 128 with nx 256) or feature-major f32 [nx][samples]
- * (x_feature_major = 1, the [38][n] feature slab; m 256, nx <= 64).  Out: part f32
- * [parts][m][npad] (npad = 256, or 64 feature-major), the partial sums of `parts` workgroups
- * over consecutive runs of samples; gW = the sum over parts of part[:, :, :nx] (the caller adds
- * them).  f32-level products (split-bf16 MFMA, as fjsp_a2c_policy).  Stream-ordered. */
-int fjsp_a2c_critic_wgrad(const float* g, int32_t m, const float* x, int32_t nx, int32_t x_feature_major,
-                          int64_t samples, float* part, int32_t parts, void* stream);
 /* Grouping keys of the A2C update (a2c.py:647-703 _update over a batch; a2c_vec.A2CLosses
  * dedup): feats f32 [T][38][n] (the rollout's a2c features) -> keys u64 [9][T * n], row a < 8
  * a hash of actor a's padded input (its a2c.py:118-134 observation block, zero-padded to 13

@@ -143,23 +143,6 @@ class _ValueHead(torch.autograd.Function):
         return gh, _splitk_wgrad(g, h), ps[:C], ps[C:2 * C].view(1, C), ps[2 * C:2 * C + 1]
 
 
-def critic_wgrad(g, x, feature_major=False, parts=256):
-    """gW = g^T x over a long batch on the matrix cores (fjsp_a2c_critic_wgrad): g f32 [S, m]
-    contiguous, x f32 [S, nx] contiguous or, feature_major, [nx, S] (the feature slab); the
-    kernel's per-workgroup partial sums are added here (a fixed order: deterministic)."""
-    S, m = g.shape
-    nx = x.shape[0] if feature_major else x.shape[1]
-    npad = 64 if feature_major else nx
-    parts = max(1, min(int(parts), -(-S // 32)))
-    part = torch.empty(parts, m, npad, dtype=torch.float32, device=g.device)
-    stream = torch.cuda.current_stream(g.device).cuda_stream
-    V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    nat.check(nat.lib().fjsp_a2c_critic_wgrad(V(g), m, V(x), nx, int(bool(feature_major)), S, V(part), parts,
-                                              ctypes.c_void_p(stream)))
-    gw = part.sum(0)
-    return gw[:, :nx] if npad != nx else gw
-
-
 def _relu_bias_grad(gy, y):
     """(gy where y > 0 else 0, its column sums) for y [B, C] = a ReLU output, gy [B, C]
     contiguous f32 on the GPU: fjsp_a2c_relu_bias_grad."""
@@ -178,7 +161,7 @@ class _CriticGrouped(torch.autograd.Function):
     planes on the matrix cores, as the policy kernel's values), which also writes the hidden
     layers; the backward: the value-head kernel, both 256-wide ReLU layers' input gradients in one
     kernel (fjsp_a2c_critic_backward, the same split arithmetic), split-K weight gradients
-    (hipBLASLt; fjsp_a2c_critic_wgrad on the matrix cores is opt-in).
+    (hipBLASLt; a matrix-core kernel for them measured slower).
     xT f32 [38, U] -> v [U]."""
 
     @staticmethod
@@ -208,9 +191,7 @@ class _CriticGrouped(torch.autograd.Function):
         V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         nat.check(nat.lib().fjsp_a2c_value_head_grad(V(h3), V(gvc), V(w4), B, V(g3), V(part), ctypes.c_void_p(stream)))
         ps = part.sum(0)
-        wg = critic_wgrad if critic_wgrad_fused else (lambda g, x, feature_major=False:   # noqa: E731
-                                                      _splitk_wgrad(g, x.t() if feature_major else x))
-        gW3 = wg(g3, h2)
+        gW3 = _splitk_wgrad(g3, h2)
         if critic_bwd_fused:
             # both 256-wide ReLU layers' input gradients in one pass (fjsp_a2c_critic_backward)
             w3t, w2t = pack_mfma(W3.t().contiguous()).reshape(-1), pack_mfma(W2.t().contiguous()).reshape(-1)
@@ -224,8 +205,8 @@ class _CriticGrouped(torch.autograd.Function):
         else:
             g2, gb2 = _relu_bias_grad((g3 @ W3).contiguous(), h2)
             g1, gb1 = _relu_bias_grad((g2 @ W2).contiguous(), h1)
-        gW2 = wg(g2, h1)
-        gW1 = wg(g1, xT, feature_major=True)
+        gW2 = _splitk_wgrad(g2, h1)
+        gW1 = _splitk_wgrad(g1, xT.t())
         return (None, gW1, gb1, gW2, gb2, gW3, ps[:C], ps[C:2 * C].view(1, C), ps[2 * C:2 * C + 1])
 
 
@@ -234,9 +215,6 @@ class _CriticGrouped(torch.autograd.Function):
 critic_fused = os.environ.get("FJSP_CRITIC_FUSED", "1") != "0"
 # its backward through the two 256-wide layers in one kernel (FJSP_CRITIC_BWD=0: GEMMs + ReLU kernels)
 critic_bwd_fused = os.environ.get("FJSP_CRITIC_BWD", "1") != "0"
-# its weight gradients on the matrix cores (fjsp_a2c_critic_wgrad, FJSP_CRITIC_WGRAD=1): opt-in, measured
-# slower than hipBLASLt's split-K GEMMs (1.6 ms against ~1 ms per update, profiles/r03/wgrad/)
-critic_wgrad_fused = os.environ.get("FJSP_CRITIC_WGRAD", "0") == "1"
 
 
 def critic_grouped(critic, xT):
@@ -945,15 +923,11 @@ def batch_advantages(rewards, values, done, gamma, lamb, use_gae=True):
     GAE kernel.  rewards f64 [T, 8, N], values f32 [T + 1, N] (row T = V(s_T), the batch-end
     bootstrap, a2c.py:321-332), done u8/bool [T, N] (an episode end bootstraps 0, a2c.py:357).
     Returns ret, adv f64 [T, 8, N]."""
-    from .vec_env import gae
+    from .vec_env import gae_shared
     T, _, N = rewards.shape
-    vals = values[:T, None, :].expand(T, NA, N).contiguous()
-    boot = values[T].double()[None, :].expand(NA, N).contiguous()
-    ret, adv = gae(rewards.contiguous().view(T, NA * N), vals.view(T, NA * N), done.to(torch.uint8).contiguous(),
-                   boot.view(NA * N), gamma, lamb)
-    ret, adv = ret.view(T, NA, N), adv.view(T, NA, N)
+    ret, adv = gae_shared(rewards, values, done, gamma, lamb)
     if not use_gae:
-        adv = ret - vals.double()
+        adv = ret - values[:T, None, :].double()
     return ret, adv
 
 

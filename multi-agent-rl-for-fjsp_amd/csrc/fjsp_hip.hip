@@ -1929,32 +1929,92 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     )
 }
 
-// transition_memory.py:83-105 over a [T][M] rollout buffer; column m = a*N + e
-template <class VT>
-__global__ void __launch_bounds__(256) k_gae(const double* __restrict__ r, const VT* __restrict__ v,
-                                             const uint8_t* __restrict__ done, const double* __restrict__ boot, int T,
-                                             int N, int M, double gamma, double lamb, double* __restrict__ ret,
-                                             double* __restrict__ adv) {
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+// transition_memory.py:83-105 over a [T][M] rollout buffer; column m = a*N + e, one lane per
+// column, the scan in the reference's operation order (backwards over t).  The scan is one
+// dependent chain per column and the chip holds only M / 64 waves of them (512 at 8 x 4 096
+// columns: 2 per CU), so the loads are software-pipelined: the inputs of GAE_U timesteps go out
+// in one batch into registers (buffer A), the next GAE_U (buffer B) are issued before A's scan,
+// and so on — two batches of independent loads in flight per wave instead of one dependent
+// round trip per timestep.  Only the loads move; the arithmetic is the same sequence per column.
+// SHARED: values f32/f64 [T + 1][N] shared by the agents of an env (the critic's value, a2c.py:
+// 321-332), boot = row T; else values [T][M] and boot [M].
+constexpr int GAE_U = 16;
+template <class VT, bool SHARED>
+struct GaeChunk {
+    double r[GAE_U];
+    VT v[GAE_U];
+    uint8_t d[GAE_U];
+};
+// Loads of the GAE_U timesteps t0, t0 - 1, ... (rows below 0 clamped to row 0: never used, and
+// no branch around a load — a load under a branch made the compiler drain every load at the join).
+template <class VT, bool SHARED>
+__device__ __forceinline__ void gae_load(GaeChunk<VT, SHARED>& c, const double* __restrict__ r,
+                                         const VT* __restrict__ v, const uint8_t* __restrict__ done, int t0, int N,
+                                         int M, int m, int e) {
+#pragma unroll
+    for (int j = 0; j < GAE_U; j++) {
+        const int t = t0 - j > 0 ? t0 - j : 0;
+        c.r[j] = __builtin_nontemporal_load(r + (size_t)t * M + m);
+        c.v[j] = v[SHARED ? (size_t)t * N + e : (size_t)t * M + m];
+        c.d[j] = done[(size_t)t * N + e];
+    }
+}
+// The scan over timesteps t0, t0 - 1, ... down to max(t0 - GAE_U + 1, 0) (FULL: all GAE_U).
+template <class VT, bool SHARED, bool FULL>
+__device__ __forceinline__ void gae_scan(const GaeChunk<VT, SHARED>& c, int t0, int T, int M, int m, double bootv,
+                                         double gamma, double gl, double& nv, double& rr, double& gae,
+                                         double* __restrict__ ret, double* __restrict__ adv) {
+#pragma unroll
+    for (int j = 0; j < GAE_U; j++) {
+        const int t = t0 - j;
+        if (FULL || t >= 0) {
+            if (t == T - 1 || c.d[j]) {   // a trajectory ends at t
+                nv = (t == T - 1 && !c.d[j]) ? bootv : 0.0;
+                rr = nv;
+                gae = 0.0;
+            }
+            const size_t i = (size_t)t * M + m;
+            const double rt = c.r[j];
+            const double vt = (double)c.v[j];
+            rr = rt + gamma * rr;
+            __builtin_nontemporal_store(rr, ret + i);
+            const double td = rt + gamma * nv - vt;
+            gae = td + gl * gae;
+            __builtin_nontemporal_store(gae, adv + i);
+            nv = vt;
+        }
+    }
+}
+template <class VT, bool SHARED>
+__device__ __forceinline__ void gae_scan_any(const GaeChunk<VT, SHARED>& c, int t0, int T, int M, int m, double bootv,
+                                             double gamma, double gl, double& nv, double& rr, double& gae,
+                                             double* __restrict__ ret, double* __restrict__ adv) {
+    if (t0 >= GAE_U - 1) gae_scan<VT, SHARED, true>(c, t0, T, M, m, bootv, gamma, gl, nv, rr, gae, ret, adv);
+    else gae_scan<VT, SHARED, false>(c, t0, T, M, m, bootv, gamma, gl, nv, rr, gae, ret, adv);
+}
+template <class VT, bool SHARED>
+__global__ void __launch_bounds__(64) k_gae(const double* __restrict__ r, const VT* __restrict__ v,
+                                            const uint8_t* __restrict__ done, const double* __restrict__ boot, int T,
+                                            int N, int M, double gamma, double lamb, double* __restrict__ ret,
+                                            double* __restrict__ adv) {
+    const int m = blockIdx.x * 64 + threadIdx.x;
     if (m >= M) return;
     const int e = m % N;
     const double gl = gamma * lamb;
+    const double bootv = SHARED ? (double)v[(size_t)T * N + e] : boot[m];
     double nv = 0.0, rr = 0.0, gae = 0.0;
-    for (int t = T - 1; t >= 0; t--) {
-        const size_t i = (size_t)t * M + m;
-        if (t == T - 1 || done[(size_t)t * N + e]) {   // a trajectory ends at t
-            nv = (t == T - 1 && !done[(size_t)t * N + e]) ? boot[m] : 0.0;
-            rr = nv;
-            gae = 0.0;
-        }
-        const double rt = r[i];
-        const double vt = (double)v[i];
-        rr = rt + gamma * rr;
-        ret[i] = rr;
-        const double td = rt + gamma * nv - vt;
-        gae = td + gl * gae;
-        adv[i] = gae;
-        nv = vt;
+    GaeChunk<VT, SHARED> A, B;
+    int t0 = T - 1;
+    gae_load(A, r, v, done, t0, N, M, m, e);
+    for (;;) {   // A holds t0.., B is loaded before A's scan, and the other way round
+        gae_load(B, r, v, done, t0 - GAE_U, N, M, m, e);
+        gae_scan_any(A, t0, T, M, m, bootv, gamma, gl, nv, rr, gae, ret, adv);
+        t0 -= GAE_U;
+        if (t0 < 0) break;
+        gae_load(A, r, v, done, t0 - GAE_U, N, M, m, e);
+        gae_scan_any(B, t0, T, M, m, bootv, gamma, gl, nv, rr, gae, ret, adv);
+        t0 -= GAE_U;
+        if (t0 < 0) break;
     }
 }
 
@@ -2361,9 +2421,8 @@ int fjsp_gae(const double* rewards, const float* values, const uint8_t* done, co
              int32_t M, double gamma, double lamb, double* ret, double* adv, void* stream) {
     if (T <= 0 || N <= 0 || M <= 0 || M % N) return fail("bad GAE shape (T > 0, N > 0, M multiple of N)");
     if (!rewards || !values || !done || !boot || !ret || !adv) return fail("null GAE buffer");
-    dim3 grid((M + 255) / 256);
-    hipLaunchKernelGGL(k_gae<float>, grid, dim3(256), 0, (hipStream_t)stream, rewards, values, done, boot, T, N, M, gamma,
-                       lamb, ret, adv);
+    hipLaunchKernelGGL((k_gae<float, false>), dim3((M + 63) / 64), dim3(64), 0, (hipStream_t)stream, rewards, values,
+                       done, boot, T, N, M, gamma, lamb, ret, adv);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -2372,9 +2431,20 @@ int fjsp_gae_f64(const double* rewards, const double* values, const uint8_t* don
                  int32_t N, int32_t M, double gamma, double lamb, double* ret, double* adv, void* stream) {
     if (T <= 0 || N <= 0 || M <= 0 || M % N) return fail("bad GAE shape (T > 0, N > 0, M multiple of N)");
     if (!rewards || !values || !done || !boot || !ret || !adv) return fail("null GAE buffer");
-    dim3 grid((M + 255) / 256);
-    hipLaunchKernelGGL(k_gae<double>, grid, dim3(256), 0, (hipStream_t)stream, rewards, values, done, boot, T, N, M, gamma,
-                       lamb, ret, adv);
+    hipLaunchKernelGGL((k_gae<double, false>), dim3((M + 63) / 64), dim3(64), 0, (hipStream_t)stream, rewards, values,
+                       done, boot, T, N, M, gamma, lamb, ret, adv);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int fjsp_gae_shared(const double* rewards, const float* values, const uint8_t* done, int32_t T, int32_t N,
+                    int32_t agents, double gamma, double lamb, double* ret, double* adv, void* stream) {
+    if (T <= 0 || N <= 0 || agents <= 0 || (int64_t)agents * N > INT32_MAX)
+        return fail("bad GAE shape (T > 0, N > 0, agents > 0)");
+    if (!rewards || !values || !done || !ret || !adv) return fail("null GAE buffer");
+    const int M = agents * N;
+    hipLaunchKernelGGL((k_gae<float, true>), dim3((M + 63) / 64), dim3(64), 0, (hipStream_t)stream, rewards, values,
+                       done, nullptr, T, N, M, gamma, lamb, ret, adv);
     HIPCHK(hipGetLastError());
     return 0;
 }

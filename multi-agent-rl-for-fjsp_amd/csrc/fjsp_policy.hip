@@ -689,119 +689,6 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
     relu_grad_out(a[0], hv, B.g1, B.bp1 + (size_t)tile * HID, col, n, 32 * wave, lane);
 }
 
-// The critic's weight gradients for the A2C update (a2c_vec._CriticGrouped.backward, a2c.py:692-699
-// critic_loss.backward() over the batch's distinct global states): gW [M][N] = sum_s G[s][m] X[s][n]
-// with K = the samples (~5 x 10^5).  Each workgroup owns a contiguous run of 32-sample stages and
-// the whole [M][NPAD] output (M / 32 row tiles x NPAD / 32 column tiles dealt over the 8 waves, the
-// accumulators live for the run), and writes its partial sum; the caller adds the partials (a
-// deterministic order).  Per stage both operands go HBM -> registers (loaded one stage ahead) ->
-// bf16 planes in LDS transposed to [feature][sample] (samples are the MFMA's K: a lane's 8
-// consecutive samples are one 16-byte fragment), then six split-bf16 MFMAs per 16-deep block as in
-// the policy kernel (f32-level products).  G is sample-major [S][M]; X sample-major [S][NPAD]
-// (XSM, the hidden layers) or feature-major [nx][S] (the first layer's input slab).
-struct WgradArgs {
-    const float* g;
-    const float* x;
-    int nx;              // X's real features (<= NPAD); X's row length when feature-major is S
-    long long S;         // samples
-    int chunk;           // stages per workgroup
-    float* part;         // [gridDim.x][M][NPAD]
-};
-constexpr int WKC = 32, WKS = WKC + 8;   // samples per stage; bf16 stride of an LDS feature row
-// four consecutive samples s0.. x four consecutive features f0.. of an operand -> v[sample][feature]
-template <bool SM>
-__device__ __forceinline__ void wg_load(const float* __restrict__ p, int ld, int nf, long long S, long long s0, int f0,
-                                        float v[4][4]) {
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const long long s = s0 + i;
-        if (SM) {
-            float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (s < S && f0 < nf) q = *reinterpret_cast<const float4*>(p + (size_t)s * ld + f0);
-            v[i][0] = q.x; v[i][1] = q.y; v[i][2] = q.z; v[i][3] = q.w;
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; j++) v[i][j] = (s < S && f0 + j < nf) ? p[(size_t)(f0 + j) * S + s] : 0.0f;
-        }
-    }
-}
-// v[sample][feature] -> planes [NP][F][WKS] at features f0.., samples 4 sg.. (one 8-byte store per
-// feature and plane)
-template <int F>
-__device__ __forceinline__ void wg_store(const float v[4][4], int f0, int sg, __bf16* s) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        bf16x4 ph, pm, pl;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            __bf16 x0, x1, x2;
-            split3(v[i][j], x0, x1, x2);
-            ph[i] = x0;
-            pm[i] = x1;
-            pl[i] = x2;
-        }
-        __bf16* d = s + (f0 + j) * WKS + 4 * sg;
-        *reinterpret_cast<bf16x4*>(d) = ph;
-        *reinterpret_cast<bf16x4*>(d + F * WKS) = pm;
-        *reinterpret_cast<bf16x4*>(d + 2 * F * WKS) = pl;
-    }
-}
-template <int M, int NPAD, bool XSM>
-__global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2))) k_wgrad(WgradArgs A) {
-    constexpr int TR = M / 32, TCN = NPAD / 32, CPW = TR * TCN / NWAVE;
-    static_assert(TR <= NWAVE && TR * TCN % NWAVE == 0 && CPW >= 1, "tiles over the waves");
-    constexpr int GB = M / 4 * (WKC / 4), XB = NPAD / 4 * (WKC / 4);   // 4 x 4 blocks per stage
-    static_assert(GB <= NTHR && XB <= NTHR, "one block per thread");
-    __shared__ __attribute__((aligned(16))) __bf16 s_a[NP * M * WKS];
-    __shared__ __attribute__((aligned(16))) __bf16 s_b[NP * NPAD * WKS];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int rt = wave % TR, ct0 = (wave / TR) * CPW;
-    const long long nst = (A.S + WKC - 1) / WKC;
-    const long long st0 = (long long)blockIdx.x * A.chunk;
-    const long long st1 = st0 + A.chunk < nst ? st0 + A.chunk : nst;
-    // this thread's 4 x 4 block of each operand in a stage
-    const int gf = 4 * (tid % (M / 4)), gs = tid / (M / 4);
-    const int xf = 4 * (tid % (NPAD / 4)), xs = tid / (NPAD / 4);
-    f32x16 acc[CPW];
-    zero_acc<CPW>(acc);
-    float gv[4][4], xv[4][4];
-    auto load = [&](long long st) __attribute__((always_inline)) {
-        if (tid < GB) wg_load<true>(A.g, M, M, A.S, st * WKC + 4 * gs, gf, gv);
-        if (tid < XB) wg_load<XSM>(A.x, NPAD, A.nx, A.S, st * WKC + 4 * xs, xf, xv);
-    };
-    if (st0 < st1) load(st0);
-    for (long long st = st0; st < st1; st++) {
-        __syncthreads();                       // the previous stage's fragments are read
-        if (tid < GB) wg_store<M>(gv, gf, gs, s_a);
-        if (tid < XB) wg_store<NPAD>(xv, xf, xs, s_b);
-        __syncthreads();
-        if (st + 1 < st1) load(st + 1);        // in flight during this stage's MFMAs
-#pragma unroll
-        for (int kb = 0; kb < WKC / 16; kb++) {
-            bf16x8 fa[NP];
-            const __bf16* pa = s_a + (32 * rt + (lane & 31)) * WKS + 16 * kb + 8 * (lane >> 5);
-#pragma unroll
-            for (int p = 0; p < NP; p++) fa[p] = *reinterpret_cast<const bf16x8*>(pa + p * M * WKS);
-#pragma unroll
-            for (int c = 0; c < CPW; c++) {
-                bf16x8 fb[NP];
-                const __bf16* pb = s_b + (32 * (ct0 + c) + (lane & 31)) * WKS + 16 * kb + 8 * (lane >> 5);
-#pragma unroll
-                for (int p = 0; p < NP; p++) fb[p] = *reinterpret_cast<const bf16x8*>(pb + p * NPAD * WKS);
-                acc[c] = mfma6(fa, fb, acc[c]);
-            }
-        }
-    }
-    float* out = A.part + (size_t)blockIdx.x * M * NPAD;
-#pragma unroll
-    for (int c = 0; c < CPW; c++) {
-        const int col = 32 * (ct0 + c) + (lane & 31);
-#pragma unroll
-        for (int r = 0; r < 16; r++) out[(32 * rt + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * NPAD + col] = acc[c][r];
-    }
-}
-
 // Keys of the A2C update's grouping of repeated inputs (a2c_vec.row_keys, the same hash): per
 // sample s = t * n + e of feats f32 [T][38][n], key a < 8 over actor a's 13 padded input columns
 // (its OBS_DIMS[a] a2c features, then zeros), key 8 over all 38; k = fmix64(k * MUL + bits(x_c)
@@ -1178,31 +1065,6 @@ extern "C" int fjsp_a2c_critic_backward(const float* g3, const float* h1, const 
         return fjsp_internal_fail("fjsp_a2c_critic_backward: null buffer");
     const CriticBwd B{g3, h1, h2, w3t, w2t, g2, g1, bias_part2, bias_part1, n};
     hipLaunchKernelGGL(k_critic_bwd, dim3((unsigned)((n + TC - 1) / TC)), dim3(NTHR), 0, (hipStream_t)stream, B);
-    const hipError_t err = hipGetLastError();
-    if (err != hipSuccess) {
-        fjsp_internal_fail(hipGetErrorString(err));
-        return -2;
-    }
-    return 0;
-}
-
-extern "C" int fjsp_a2c_critic_wgrad(const float* g, int32_t m, const float* x, int32_t nx, int32_t x_feature_major,
-                                     int64_t samples, float* part, int32_t parts, void* stream) {
-    if (samples <= 0 || parts <= 0) return fjsp_internal_fail("fjsp_a2c_critic_wgrad: samples and parts must be > 0");
-    if (!g || !x || !part) return fjsp_internal_fail("fjsp_a2c_critic_wgrad: null buffer");
-    const long long nst = (samples + WKC - 1) / WKC;
-    const int chunk = (int)((nst + parts - 1) / parts);
-    const WgradArgs A{g, x, nx, (long long)samples, chunk, part};
-    const dim3 grid((unsigned)parts), block(NTHR);
-    if (!x_feature_major && nx == HID && m == HID)
-        hipLaunchKernelGGL((k_wgrad<HID, HID, true>), grid, block, 0, (hipStream_t)stream, A);
-    else if (!x_feature_major && nx == HID && m == HID / 2)
-        hipLaunchKernelGGL((k_wgrad<HID / 2, HID, true>), grid, block, 0, (hipStream_t)stream, A);
-    else if (x_feature_major && nx > 0 && nx <= 64 && m == HID)
-        hipLaunchKernelGGL((k_wgrad<HID, 64, false>), grid, block, 0, (hipStream_t)stream, A);
-    else
-        return fjsp_internal_fail("fjsp_a2c_critic_wgrad: unsupported shape (m 256 / 128 with sample-major nx 256, "
-                                  "or m 256 with feature-major nx <= 64)");
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

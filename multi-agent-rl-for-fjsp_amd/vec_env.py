@@ -283,4 +283,20 @@ def gae(rewards, values, done, boot, gamma, lamb, out_ret=None, out_adv=None):
     return ret, adv
 
 
-__all__ = ["FJSPVecEnv", "Buffers", "gae", "AGENTS"]
+def gae_shared(rewards, values, done, gamma, lamb, out_ret=None, out_adv=None):
+    """gae() with one value per env shared by its agents (fjsp_gae_shared): rewards f64
+    [T, A, N], values f32 [T + 1, N] (row T = the bootstrap value), done u8/bool [T, N] ->
+    ret, adv f64 [T, A, N]."""
+    T, A, N = rewards.shape
+    if values.dtype != torch.float32 or tuple(values.shape) != (T + 1, N) or tuple(done.shape) != (T, N):
+        raise ValueError("gae_shared: values f32 [T + 1, N] and done [T, N] expected")
+    ret = out_ret if out_ret is not None else torch.empty_like(rewards)
+    adv = out_adv if out_adv is not None else torch.empty_like(rewards)
+    r = rewards.contiguous(); v = values.contiguous(); d = done.to(torch.uint8).contiguous()
+    stream = torch.cuda.current_stream(rewards.device).cuda_stream
+    nat.check(nat.lib().fjsp_gae_shared(_ptr(r), _ptr(v), _ptr(d), T, N, A, float(gamma), float(lamb),
+                                        _ptr(ret), _ptr(adv), ctypes.c_void_p(stream)))
+    return ret, adv
+
+
+__all__ = ["FJSPVecEnv", "Buffers", "gae", "gae_shared", "AGENTS"]

@@ -182,6 +182,37 @@ def test_gae_vs_oracle_large(G):
         assert P.bits_equal(adv[:, m], aa[:, 0]), m
 
 
+@pytest.mark.parametrize("T,N", [(256, 4096), (1, 70), (15, 64), (16, 130), (17, 1), (33, 257), (200, 1000)])
+def test_gae_shared_equals_gae(G, T, N):
+    """fjsp_gae_shared (one value per env shared by its 8 agents, bootstrap = row T; the A2C's
+    call) == fjsp_gae over the expanded values, bit for bit, for batch lengths around the
+    kernel's 16-step load batches; and the generic scan == the oracle on sampled columns."""
+    A = 8
+    g = torch.Generator().manual_seed(T * 1000 + N)
+    rw = (torch.randn(T, A, N, generator=g, dtype=torch.float64) * 24).round() / 8
+    v = torch.randn(T + 1, N, generator=g) * 5
+    done = (torch.rand(T, N, generator=g) < 0.02).to(torch.uint8)
+    done[T // 2, : N // 3] = 1
+    ret_s, adv_s = G.vec_env.gae_shared(rw.cuda(), v.cuda(), done.cuda(), 0.99, 0.95)
+    vx = v[:T, None, :].expand(T, A, N).reshape(T, A * N).contiguous()
+    boot = v[T].double()[None, :].expand(A, N).reshape(-1).contiguous()
+    ret, adv = G.vec_env.gae(rw.reshape(T, A * N).cuda(), vx.cuda(), done.cuda(), boot.cuda(), 0.99, 0.95)
+    assert torch.equal(ret_s.reshape(T, A * N).cpu(), ret.cpu())
+    assert torch.equal(adv_s.reshape(T, A * N).cpu(), adv.cpu())
+    ret, adv = ret.cpu().numpy(), adv.cpu().numpy()
+    rwn, vn, dn = rw.reshape(T, A * N).numpy(), vx.numpy(), done.numpy()
+    for m in np.random.default_rng(T + N).choice(A * N, min(16, A * N), replace=False):
+        e = m % N
+        se = dn[:, e].copy()
+        se[-1] = 1
+        boots = np.zeros(int(se.sum()))
+        if not dn[-1, e]:
+            boots[-1] = float(boot[m])
+        rr, aa = O.gae(rwn[:, m:m + 1], vn[:, m:m + 1], boots.reshape(-1, 1), se, 0.99, 0.95)
+        assert P.bits_equal(ret[:, m], rr[:, 0]), m
+        assert P.bits_equal(adv[:, m], aa[:, 0]), m
+
+
 def test_reset_tables_and_read_env(G):
     d = np.load(f"{P.GOLDEN}/reset_tables.npz")
     n = 256
