@@ -14,7 +14,8 @@ REPO = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("FJSP_LIB") or os.path.join(HERE, "libfjsp.so")
 SRC = os.path.join(HERE, "csrc", "fjsp_hip.hip")
 SRCS = [SRC, os.path.join(HERE, "csrc", "fjsp_policy.hip")]
-HEADERS = [os.path.join(HERE, "csrc", "fjsp_env.h"), os.path.join(REPO, "include", "fjsp.h")]
+HEADERS = [os.path.join(HERE, "csrc", h) for h in ("fjsp_env.h", "fjsp_stepdev.h", "fjsp_stamps.h")] + [
+    os.path.join(REPO, "include", "fjsp.h")]
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
