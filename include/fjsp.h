@@ -268,6 +268,20 @@ int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const fl
                     const uint64_t* seed, uint32_t env_gid0, uint32_t step, int32_t deterministic, uint8_t* actions,
                     float* values,
                     float* probs, void* stream);
+/* One vector step of the A2C collect in ONE launch (a2c.py:284-309: predict -> env.step ->
+ * memory): fjsp_a2c_policy's actions (and, when values != NULL, the critic's values) for the
+ * handle's n envs, then FJSPSimulation.step (fjsp_step, canonical agent order) of every 64-env
+ * tile with those actions, run inside the same launch by the tile's last actor workgroup.
+ * feats / masks = the current observation ([38][n] / [29][n]); actions u8 [8][n] and values f32
+ * [n] as fjsp_a2c_policy writes them (probabilities are not available here).  out: the step's
+ * outputs of this one step, limited to rewards, term, trunc, status, next_masks and feats (each
+ * [F][n], any may be NULL; the other fields must be NULL).  Results equal fjsp_a2c_policy
+ * followed by fjsp_step with the same arguments, byte for byte.  Stream-ordered on the handle's
+ * stream; replaces fjsp_a2c_policy + fjsp_step per vector step (one launch instead of two). */
+int fjsp_a2c_policy_step(fjsp_handle* h, const float* feats, const int8_t* masks, const float* actor_w,
+                         const float* critic_w, const uint64_t* seed, uint32_t env_gid0, uint32_t step,
+                         int32_t deterministic, uint8_t* actions, float* values, int32_t autoreset,
+                         const fjsp_out* out);
 /* The critic's forward over n samples for the A2C update (a2c.py:692-699 critic(global_states)
  * over the batch; a2c_vec._CriticGrouped): x f32 [38][n] (feature rows, as fjsp_a2c_policy's
  * feats), critic_w packed as for fjsp_a2c_policy -> values f32 [n] and the post-ReLU hidden

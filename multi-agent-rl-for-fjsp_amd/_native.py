@@ -67,7 +67,8 @@ EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_c
            "fjsp_snapshot_bytes", "fjsp_snapshot", "fjsp_restore", "fjsp_last_kernel", "fjsp_a2c_policy",
            "fjsp_a2c_group_keys", "fjsp_a2c_group_verify", "fjsp_a2c_actor_head",
            "fjsp_a2c_relu_bias_grad", "fjsp_a2c_value_head_grad", "fjsp_faults", "fjsp_a2c_critic_forward",
-           "fjsp_a2c_critic_backward", "fjsp_gae_shared"]
+           "fjsp_a2c_critic_backward", "fjsp_gae_shared",
+           "fjsp_a2c_policy_step"]
 POLICY_ACTOR_DPAD, POLICY_CRITIC_DPAD = 16, 48
 POLICY_ACTOR_FLOATS = 3 * 256 * 16 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 8 * 256 + 16
 POLICY_CRITIC_FLOATS = 3 * 256 * 48 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 3 * 128 * 256 // 2 + 128 + 128 + 16
@@ -146,6 +147,7 @@ def lib():
         "fjsp_a2c_critic_forward": (I, [P, I, P, P, P, P, P, P]),
         "fjsp_a2c_critic_backward": (I, [P, P, P, I, P, P, P, P, P, P, P]),
         "fjsp_gae_shared": (I, [P, P, P, I, I, I, D, D, P, P, P]),
+        "fjsp_a2c_policy_step": (I, [P, P, P, P, P, P, U32, U32, I, P, P, I, ctypes.POINTER(fjsp_out)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

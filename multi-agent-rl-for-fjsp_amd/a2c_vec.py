@@ -972,6 +972,9 @@ class VecMultiAgentA2C:
         self.use_graph = bool(use_graph) and self.device.type == "cuda"
         # fused policy kernel (csrc/fjsp_policy.hip): one launch per vector step
         self.fused_policy = bool(fused_policy) and self.device.type == "cuda" and hidden == 256
+        # ... with the env step inside the same launch (fjsp_a2c_policy_step; False: the policy
+        # kernel, then fjsp_step, two launches per vector step, the same bytes)
+        self.fused_step = self.fused_policy
         # sampling key: (seed, batch) -> counter hash per (global env id, step, agent); the same
         # on every rank, the env's global id separates the shards
         self._rng_host = int.from_bytes(__import__("os").urandom(7), "little") if seed is None else int(seed)
@@ -1056,6 +1059,18 @@ class VecMultiAgentA2C:
                                        P(act_out), P(val_out), P(probs_out), ctypes.c_void_p(stream))
         nat.check(rc)
 
+    def policy_step(self, t, deterministic):
+        """Vector step t of the collect in one launch (fjsp_a2c_policy_step): the fused policy's
+        actions and values, then the env step of each 64-env tile by its last actor workgroup,
+        writing rewards / term / trunc / status and the next observation's masks and features into
+        the rollout slab (bytes equal to policy_fused + fjsp_step)."""
+        b = self._bufs
+        P = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+        nat.check(nat.lib().fjsp_a2c_policy_step(self.env.handle, P(b["feats"][t]), P(b["masks"][t]), P(self._pw_actor),
+                                                 P(self._pw_critic), P(self._rng), int(self.env.env_id_base), int(t),
+                                                 int(bool(deterministic)), P(b["actions"][t]), P(b["values"][t]), 1,
+                                                 ctypes.byref(b["outs"][t])))
+
     def repack(self):
         """Refresh the fused kernel's packed weights (after an update / load)."""
         if self.fused_policy:
@@ -1123,6 +1138,9 @@ class VecMultiAgentA2C:
         self.env._sync_stream()
         T = self.batch_size
         for t in range(T):
+            if self.fused_step and action_fn is None:
+                self.policy_step(t, deterministic)
+                continue
             if self.fused_policy and action_fn is None:
                 self.policy_fused(b["feats"][t], b["masks"][t], t, deterministic, b["actions"][t], b["values"][t])
             else:

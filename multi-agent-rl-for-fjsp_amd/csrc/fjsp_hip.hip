@@ -1741,6 +1741,10 @@ struct fjsp_handle {
     int ag_epw;      // k_step_ag envs per workgroup: 64 / 32 / 16, 0 = auto (FJSP_AG_EPW / "ag_envs")
     const char* last_kernel;   // name of the last step kernel launched (fjsp_last_kernel)
     uint32_t env_id_base;      // global id of env 0 (fjsp_set_option "env_id_base")
+    // fjsp_a2c_policy_step's tile hand-off: [ntiles] arrival counters (zero between launches),
+    // then [ntiles][8][16] action words; outside the state block (not part of a snapshot)
+    uint32_t* tiles;
+    int ntiles;
 };
 
 static thread_local std::string g_err;
@@ -1766,6 +1770,9 @@ static int hip_fail(const char* what, hipError_t e) {
         hipError_t _e = (x);                      \
         if (_e != hipSuccess) return hip_fail(#x, _e); \
     } while (0)
+
+// words of the tile hand-off block: counters (padded to 64 words), then the action words
+static size_t tile_words(int ntiles) { return (((size_t)ntiles + 63) & ~(size_t)63) + (size_t)ntiles * 8 * 16; }
 
 struct DeviceGuard {
     int prev = -1;
@@ -1902,6 +1909,11 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     if (e != hipSuccess) { h->ev1 = nullptr; return bail("hipEventCreate", e); }
     e = hipMalloc(&h->lut_dev, sizeof(double) * RLUT_SIZE);
     if (e != hipSuccess) { h->lut_dev = nullptr; return bail("hipMalloc(reward table)", e); }
+    h->ntiles = (num_envs + 63) / 64;
+    e = hipMalloc(&h->tiles, tile_words(h->ntiles) * 4);
+    if (e != hipSuccess) { h->tiles = nullptr; return bail("hipMalloc(tile hand-off)", e); }
+    e = hipMemsetAsync(h->tiles, 0, tile_words(h->ntiles) * 4, h->stream);
+    if (e != hipSuccess) return bail("init", e);
     {
         // the aux words: fault 0, hand-off bound ~0.1 s of sleeps (far beyond any legitimate wait)
         const uint32_t aux[AUX_WORDS] = {0u, 1u << 22, 0u, 0u};
@@ -1935,6 +1947,7 @@ int fjsp_destroy(fjsp_handle* h) {
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->lut_dev) (void)hipFree(h->lut_dev);
+    if (h->tiles) (void)hipFree(h->tiles);
     if (h->base) (void)hipFree(h->base);
     delete h;
     return 0;
@@ -2023,6 +2036,28 @@ int fjsp_step(fjsp_handle* h, const uint8_t* actions, const uint8_t* agent_order
         hipLaunchKernelGGL(k_step<false>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, packed, autoreset,
                            out ? *out : kNoOut);
     HIPCHK(hipGetLastError());
+    if (h->timing) {
+        HIPCHK(hipEventRecord(h->ev1, h->stream));
+        h->timed = 1;
+    }
+    return 0;
+}
+
+int fjsp_a2c_policy_step(fjsp_handle* h, const float* feats, const int8_t* masks, const float* actor_w,
+                         const float* critic_w, const uint64_t* seed, uint32_t env_gid0, uint32_t step,
+                         int32_t deterministic, uint8_t* actions, float* values, int32_t autoreset, const fjsp_out* out) {
+    if (!h) return fail("null handle");
+    if (!h->has_reset) return fail("fjsp_a2c_policy_step before fjsp_reset");
+    if (!feats || !masks || !actor_w || !seed || !actions || (values && !critic_w))
+        return fail("fjsp_a2c_policy_step: null buffer");
+    DeviceGuard g(h->device);
+    if (h->timing) HIPCHK(hipEventRecord(h->ev0, h->stream));
+    h->last_kernel = "k_policy_step";
+    const size_t cnt_words = ((size_t)h->ntiles + 63) & ~(size_t)63;
+    const int rc = fjsp_internal_policy_step(feats, masks, h->n, actor_w, critic_w, seed, env_gid0, step, deterministic,
+                                             actions, values, h->S, h->dcfg, out ? *out : kNoOut, h->tiles,
+                                             h->tiles + cnt_words, autoreset, h->stream);
+    if (rc) return rc;
     if (h->timing) {
         HIPCHK(hipEventRecord(h->ev1, h->stream));
         h->timed = 1;

@@ -29,6 +29,7 @@
 
 #include "../../include/fjsp.h"
 #include "fjsp_stamps.h"
+#include "fjsp_stepdev.h"
 
 namespace {
 
@@ -85,12 +86,7 @@ __constant__ int c_obs_dim[NAG] = {7, 13, 3, 3, 3, 3, 3, 3};
 __constant__ int c_mask_off[NAG] = {0, 3, 11, 14, 17, 20, 23, 26};
 __constant__ int c_nact[NAG] = {3, 8, 3, 3, 3, 3, 3, 3};
 
-__device__ __forceinline__ uint64_t fmix64(uint64_t z) {
-    z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
-    z ^= z >> 27; z *= 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return z;
-}
+using fjsp::fmix64;
 
 __device__ __forceinline__ void split3(float v, __bf16& hi, __bf16& mid, __bf16& lo) {
     hi = (__bf16)v;
@@ -398,7 +394,7 @@ __device__ __forceinline__ void critic_tile(const PolicyArgs& A, int tile, unsig
 // 2's input and summed into layer 2's accumulators (32 rows x 64 envs per wave), so only half of
 // h1 is ever in LDS.
 __device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int tile, unsigned char* s_mem, int tid,
-                                           int lane, int wave) {
+                                           int lane, int wave, int& act_out) {
     __bf16* s_x = reinterpret_cast<__bf16*>(s_mem);                      // inputs [NP][TA][XSA]
     __bf16* s_h = reinterpret_cast<__bf16*>(s_mem + X_BYTES);            // an h1 half [NP][TA][HSA]
     float* s_part = reinterpret_cast<float*>(s_mem + X_BYTES);           // logit partials [8][8][TA] (after layer 2)
@@ -435,6 +431,7 @@ __device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int ti
         if (tid < TA && e0 + tid < n) {
             const int e = e0 + tid, only = __builtin_ctz(mbits | 256u);
             A.actions[(size_t)role * n + e] = (uint8_t)only;
+            act_out = only;
             if (A.probs_out)
                 for (int j = 0; j < 8; j++) A.probs_out[((size_t)role * 8 + j) * n + e] = j == only ? 1.0f : 0.0f;
         }
@@ -525,6 +522,7 @@ __device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int ti
             if (act >= na) act = na - 1;
         }
         A.actions[(size_t)role * n + e] = (uint8_t)act;
+        act_out = act;
         if (A.probs_out)
             for (int j = 0; j < 8; j++) A.probs_out[((size_t)role * 8 + j) * n + e] = j < na ? p[j] : 0.0f;
     }
@@ -543,10 +541,122 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
     PST(11, __builtin_amdgcn_s_getreg(4 | (31 << 11)));
     PST(12, __builtin_amdgcn_s_getreg(20 | (31 << 11)));
     PST(13, role);
+    int act = 0;
     if (role == NAG) critic_tile<false>(A, b, s_mem, tid, lane, wave, CriticSave{});
-    else actor_tile(A, role, (b - A.nc) % A.na, s_mem, tid, lane, wave);
+    else actor_tile(A, role, (b - A.nc) % A.na, s_mem, tid, lane, wave, act);
     PST(9, __builtin_amdgcn_s_memtime());
     PST(10, __builtin_amdgcn_s_memrealtime());
+}
+
+// ---- the collect's vector step in one launch: policy + FJSPSimulation.step (a2c.py:284-309)
+// The step of a 64-env tile needs only that tile's eight actions (FJSPSimulation.py:144-242), so
+// it runs inside the policy launch, in the actor workgroup of the tile that finishes last: no
+// wait, no assumption about which workgroups are resident.  Hand-off (MI355X_MICROARCH.md
+// § inter-workgroup visibility, "Valid forms" table, first row): each actor workgroup stores its
+// role's 64 actions write-through (sc1, 4 envs per dword), its storing wave drains them
+// (vmcnt(0)), the workgroup's barrier, then one lane adds 1 to the tile's arrival counter
+// (agent-scope atomic); the workgroup whose add returns 7 is the tile's last, resets the counter
+// for the next launch, and its wave 0 loads the 8 x 16 action words with sc1 loads (L2-served,
+// never an L1 copy) and steps the tile's envs exactly as k_step<canon> does.  Every other load
+// of the step (state words, order table, tray-slot arena, MT rows, the reward table) reads bytes
+// no other workgroup writes in this launch.
+typedef __attribute__((address_space(1))) uint32_t gu32;
+struct StepArgs {
+    fjsp::DevState S;
+    fjsp::Cfg C;
+    // the step's outputs (row t of the collect's slabs; the collect's subset of fjsp_out, so that
+    // the kernel's arguments fit the SGPRs: any may be NULL)
+    double* rewards;
+    uint8_t* term;
+    uint8_t* trunc;
+    uint32_t* status;
+    int8_t* next_masks;
+    float* feats;
+    uint32_t* tile_cnt;    // [na] arrivals per tile (0 between launches)
+    uint32_t* tile_act;    // [na][8][16] the tile's actions, 4 envs per dword
+    int autoreset;
+};
+
+__device__ __forceinline__ void tile_step(const PolicyArgs& A, const StepArgs& St, int tile, unsigned char* s_mem,
+                                          int lane) {
+    double* s_lut = reinterpret_cast<double*>(s_mem);
+    const int e = tile * TA + lane;
+    const bool valid = e < A.n;
+    fjsp::Env E;
+    int act[NAG];
+    if (valid) {
+        fjsp::env_load(E, St.S.words, St.S.n, e);
+        const gu32* ta = (const gu32*)(St.tile_act) + (size_t)tile * NAG * 16 + (lane >> 2);
+#pragma unroll
+        for (int a = 0; a < NAG; a++)
+            act[a] = (int)((__hip_atomic_load(ta + a * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (8 * (lane & 3))) &
+                           0xFFu);
+    }
+    for (int i = lane; i < fjsp::RLUT_SIZE; i += 64) s_lut[i] = St.C.lut[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!valid) return;
+    fjsp::Cfg C = St.C;
+    C.lut = s_lut;
+    const fjsp::Tables T = fjsp::tables_of(St.S, e);
+    // k_step<canon>'s step_and_emit for the outputs the collect asks for (the observation before
+    // the auto-reset is not among them)
+    const uint32_t n = (uint32_t)St.S.n, ue = (uint32_t)e;
+    uint32_t res[NAG];
+    const double g8 = fjsp::env_advance<true>(E, T, C, act, nullptr, res);
+    if (St.rewards) {
+#pragma unroll
+        for (int a = 0; a < NAG; a++) fjsp::st32(St.rewards, (uint32_t)a * n + ue, g8 + fjsp::local_reward(C, a, res[a], act[a]));
+    }
+    const int nord = E.norders();
+    const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
+    const int truncated = E.step() >= C.max_steps;
+    if (St.term) fjsp::st32(St.term, ue, (uint8_t)all_done);
+    if (St.trunc) fjsp::st32(St.trunc, ue, (uint8_t)truncated);
+    if (St.status) fjsp::st32(St.status, ue, E.status());
+    E.set_step(E.step() + 1);
+    if (St.autoreset && (all_done || truncated)) E = fjsp::env_reset_cold(E, T, C, St.S, e, nord);
+    if (St.next_masks || St.feats) {
+        fjsp::StoreSink nsink{nullptr, nullptr, nullptr, St.next_masks, 0u, n, ue, St.feats};
+        fjsp::observe(E, C, nsink);
+    }
+    fjsp::env_store(E, St.S.words, St.S.n, e);
+}
+
+__global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) k_policy_step(PolicyArgs A, StepArgs St) {
+    __shared__ __attribute__((aligned(16))) unsigned char s_mem[LDS_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int b = blockIdx.x;
+    if (b < A.nc) {
+        critic_tile<false>(A, b, s_mem, tid, lane, wave, CriticSave{});
+        return;
+    }
+    const int role = (b - A.nc) / A.na, tile = (b - A.nc) % A.na;
+    int act = 0;
+    actor_tile(A, role, tile, s_mem, tid, lane, wave, act);
+    if (wave == 0) {
+        const uint32_t a = (uint32_t)act & 0xFFu;
+        const int l4 = 4 * (lane & 15);
+        const uint32_t w = (uint32_t)__shfl(a, l4) | ((uint32_t)__shfl(a, l4 + 1) << 8) |
+                           ((uint32_t)__shfl(a, l4 + 2) << 16) | ((uint32_t)__shfl(a, l4 + 3) << 24);
+        if (lane < 16)
+            __hip_atomic_store((gu32*)(St.tile_act) + ((size_t)tile * NAG + role) * 16 + lane, w,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();   // every wave is done with s_mem, the action words are drained
+    uint32_t* s_last = reinterpret_cast<uint32_t*>(s_mem + LDS_BYTES - 16);
+    if (tid == 0) {
+        gu32* cnt = (gu32*)(St.tile_cnt) + tile;
+        const uint32_t last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NAG - 1;
+        if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_last = last;
+    }
+    __syncthreads();
+    if (wave != 0 || !*s_last) return;
+    tile_step(A, St, tile, s_mem, lane);
 }
 
 // The critic's forward over n samples for the A2C update (values + the saved hidden layers).
@@ -952,7 +1062,29 @@ __global__ void __launch_bounds__(256) k_value_head_grad(const float* __restrict
 
 }  // namespace
 
-int fjsp_internal_fail(const char* msg);   // fjsp_hip.hip: sets fjsp_last_error()
+int fjsp_internal_fail(const char* msg);
+
+// fjsp_a2c_policy_step's launch (fjsp_hip.hip holds the handle): k_policy_step on the policy's
+// grid, the step's state / config / outputs and the tile hand-off buffers from the handle.
+int fjsp_internal_policy_step(const float* feats, const int8_t* masks, int32_t n, const float* actor_w,
+                              const float* critic_w, const uint64_t* seed, uint32_t env_gid0, uint32_t step,
+                              int32_t deterministic, uint8_t* actions, float* values, const fjsp::DevState& S,
+                              const fjsp::Cfg& C, const fjsp_out& out, uint32_t* tile_cnt, uint32_t* tile_act,
+                              int32_t autoreset, hipStream_t stream) {
+    if (out.obs_i32 || out.obs_i8 || out.obs_f32 || out.masks || out.results || out.orders_completed || out.packaged ||
+        out.sim_time || out.next_i32 || out.next_i8 || out.next_f32)
+        return fjsp_internal_fail("fjsp_a2c_policy_step: outputs limited to rewards, term, trunc, status, next_masks, feats");
+    PolicyArgs A{feats, masks, n, actor_w, critic_w, seed, env_gid0, step, deterministic, actions, values, nullptr,
+                 values ? (n + TC - 1) / TC : 0, (n + TA - 1) / TA};
+    StepArgs St{S, C, out.rewards, out.term, out.trunc, out.status, out.next_masks, out.feats, tile_cnt, tile_act, autoreset};
+    hipLaunchKernelGGL(k_policy_step, dim3((unsigned)(A.nc + NAG * A.na)), dim3(NTHR), 0, stream, A, St);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
+}   // fjsp_hip.hip: sets fjsp_last_error()
 
 extern "C" int fjsp_a2c_actor_head(const float* pu, int32_t umax, const int64_t* inv, int32_t T, int32_t n,
                                    const int8_t* masks, const int64_t* actions, const float* adv_n, float inv_count,

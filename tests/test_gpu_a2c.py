@@ -134,6 +134,35 @@ def test_graph_replay_equals_eager(M):
         assert torch.equal(runs[0][i], runs[1][i])
 
 
+@pytest.mark.parametrize("n,T,det,graph", [(1000, 210, False, True), (4096, 256, False, True), (130, 70, True, False),
+                                           (64, 230, False, True)])
+def test_policy_step_launch_equals_two_launches(M, n, T, det, graph):
+    """fjsp_a2c_policy_step (policy + env step in one launch, the step of each 64-env tile run by
+    its last actor workgroup after the write-through action hand-off) == fjsp_a2c_policy then
+    fjsp_step: every byte of the rollout slab over three batches (eager, captured, replayed),
+    partial tiles, greedy and sampled actions, across auto-resets."""
+    A, V = M["A"], M["V"]
+    keys = ("feats", "masks", "actions", "values", "rewards", "term", "trunc", "status")
+    runs = []
+    for fused in (False, True):
+        env = V.FJSPVecEnv(n)
+        L = A.VecMultiAgentA2C(env, batch_size=T, seed=21, use_graph=graph)
+        L.fused_step = fused
+        L.reset(seeds=torch.arange(n) + 7, num_orders=25)
+        out = []
+        for _ in range(3):
+            L.collect(deterministic=det)
+            out.append({k: L._bufs[k].clone() for k in keys})
+            L.roll_over()
+        assert env.last_kernel() == ("k_policy_step" if fused else "k_step<canon>")
+        runs.append(out)
+    for b in range(3):
+        for k in keys:
+            assert torch.equal(runs[0][b][k], runs[1][b][k]), (b, k)
+    ends = sum(int((r["term"] | r["trunc"]).sum()) for r in runs[1])
+    assert ends >= n                                    # every env crossed an auto-reset
+
+
 def test_eager_policy_graph_rekeys_each_batch(M):
     """The PyTorch policy path (fused_policy=False) captured into the collect graph reads the
     draw key from the device: every replay draws new actions, and each batch equals the eager
