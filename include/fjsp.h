@@ -172,7 +172,10 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
  * larger job — every env's MT19937 stream is re-seeded to np.random.seed(value + e), exactly
  * the stream env value + e of one big handle starts from; stream-ordered); "spin_cap"
  * (256..2^31-1, default 2^22: sleep iterations, checked every 256 a wave of a multi-wave step kernel waits for another
- * wave's hand-off before it gives up and flags FJSP_STATUS_SPIN_TIMEOUT / fjsp_faults). */
+ * wave's hand-off before it gives up and flags FJSP_STATUS_SPIN_TIMEOUT / fjsp_faults); "test_stall"
+ * (0..2^20, default 0; tests only: in every later multi-wave step launch, workgroup 0's owner
+ * wave sleeps value x ~8k cycles before its first step, so that the other waves' bounded waits
+ * give up and the give-up path runs).  spin_cap and test_stall are not part of a snapshot. */
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value);
 int fjsp_num_envs(const fjsp_handle* h);
 /* Bytes of device state per env (HBM footprint of the SoA state). */
@@ -239,8 +242,9 @@ int fjsp_a2c_layout(int32_t* out);
 /* Env-state snapshot (every env's packed state, order table, tray-slot arena and MT19937
  * stream): fjsp_snapshot copies fjsp_snapshot_bytes(h) bytes to `dst` (device or host
  * memory), fjsp_restore loads a snapshot taken from a handle with the same num_envs.  Both
- * are stream-ordered (hipMemcpyAsync; pinned host memory for overlap).  The role of
- * FJSPSimulation's Python objects being copied / pickled by a caller. */
+ * are stream-ordered (hipMemcpyAsync; pinned host memory for overlap).  The handle's fault
+ * word and options (spin_cap, test_stall) are not restored: they stay the handle's.  The role
+ * of FJSPSimulation's Python objects being copied / pickled by a caller. */
 int64_t fjsp_snapshot_bytes(const fjsp_handle* h);
 
 /* ---- fused A2C policy step (a2c.py:168-252 predict for all agents and envs; networks.py) ----
@@ -343,8 +347,8 @@ int fjsp_last_kernel_ms(fjsp_handle* h, float* ms);
 /* Name of the kernel variant the last fjsp_step / fjsp_step_many launched ("" before any):
  * e.g. "k_step_pipe<lds>" (rocprof shows it as k_step_pipe). */
 const char* fjsp_last_kernel(const fjsp_handle* h);
-/* Fault word of the handle's multi-wave step kernels (part of the handle's state: a snapshot /
- * restore carries it) (k_step_ag, k_step_pipe with hand-offs):
+/* Fault word of the handle's multi-wave step kernels (k_step_ag, k_step_pipe with hand-offs;
+ * not changed by fjsp_restore):
  * bit 0 = some workgroup's wave gave up a bounded wait for another wave's hand-off (its envs
  * also carry FJSP_STATUS_SPIN_TIMEOUT).  Never set by a correct kernel: the bound (option
  * "spin_cap", sleep iterations, default 2^22 ~ 0.1 s) exists so that a hand-off bug ends the

@@ -730,6 +730,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
         }
     }
     __syncthreads();
+    if (wave == 0 && blockIdx.x == 0) stall_for_test(S);
     if (wave == 0) {
         __builtin_amdgcn_s_setprio(3);   // the sim wave is the critical path: win shared issue slots
         Env E;
@@ -1254,6 +1255,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     FJSP_DIAG(
     if (threadIdx.x == 0) atomicAdd(&g_agstamps[56], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_entry));
     )
+    if (wave == AG_AM && blockIdx.x == 0) stall_for_test(S);
     if (wave == AG_AM) {
         __builtin_amdgcn_s_setprio(3);   // the machines -> AGV chain is the critical path
         Env E;
@@ -1974,6 +1976,14 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
         HIPCHK(hipMemcpy(h->S.words + (size_t)NWORDS * h->n + AUX_SPIN_CAP, &v, 4, hipMemcpyHostToDevice));
         return 0;
     }
+    if (!strcmp(name, "test_stall")) {   // tests only: see stall_for_test (fjsp_stepdev.h)
+        if (value < 0 || value > (1 << 20)) return fail("test_stall must be in 0..2^20");
+        DeviceGuard g(h->device);
+        const uint32_t v = (uint32_t)value;
+        HIPCHK(hipStreamSynchronize(h->stream));
+        HIPCHK(hipMemcpy(h->S.words + (size_t)NWORDS * h->n + AUX_TEST_STALL, &v, 4, hipMemcpyHostToDevice));
+        return 0;
+    }
     if (!strcmp(name, "env_id_base")) {
         // the handle is shard [value, value + n) of a larger job: env e's default stream becomes
         // np.random.seed(value + e), as for env value + e of one big handle (stream-ordered)
@@ -2241,7 +2251,10 @@ int fjsp_snapshot(fjsp_handle* h, void* dst) {
 int fjsp_restore(fjsp_handle* h, const void* src) {
     if (!h || !src) return fail("null argument");
     DeviceGuard g(h->device);
-    HIPCHK(hipMemcpyAsync(h->base, src, h->bytes, hipMemcpyDefault, h->stream));
+    // everything but the aux words (fault word, spin_cap, test options): those stay the handle's
+    const size_t state = (size_t)NWORDS * h->n * 4, rest = (size_t)((char*)h->S.orders - (char*)h->base);
+    HIPCHK(hipMemcpyAsync(h->base, src, state, hipMemcpyDefault, h->stream));
+    HIPCHK(hipMemcpyAsync((char*)h->base + rest, (const char*)src + rest, h->bytes - rest, hipMemcpyDefault, h->stream));
     h->has_reset = 1;
     return 0;
 }

@@ -29,8 +29,17 @@ struct DevState {
 // bit 0 = a bounded hand-off wait gave up) and the bound of those waits (option "spin_cap").
 // Not kernel arguments: a pointer or a field more in DevState / Cfg, live through the step loops,
 // pushed k_step_ag into SGPR spills (+6 % per step, measured).
-constexpr int AUX_WORDS = 4, AUX_FAULT = 0, AUX_SPIN_CAP = 1;
+// AUX_TEST_STALL: test option "test_stall" (tests/test_gpu_agents.py), see stall_for_test.
+constexpr int AUX_WORDS = 4, AUX_FAULT = 0, AUX_SPIN_CAP = 1, AUX_TEST_STALL = 2;
 __device__ __forceinline__ uint32_t* aux_words(const DevState& S) { return S.words + (size_t)NWORDS * S.n; }
+// Test option "test_stall" = s: the wave that owns a multi-wave workgroup's hand-offs sleeps
+// s x 127 x 64 cycles before its first step (called for workgroup 0 only, once per launch), so
+// the other waves' bounded waits for its first post give up — the give-up path under test.  One
+// scalar load per launch; nothing in the step loops.
+__device__ __forceinline__ void stall_for_test(const DevState& S) {
+    const uint32_t s = aux_words(S)[AUX_TEST_STALL];
+    for (uint32_t i = 0; i < s; i++) __builtin_amdgcn_s_sleep(127);
+}
 
 // ---------------------------------------------------------------- load / store of Env
 // The register state is the HBM row layout itself (fjsp_env.h, struct Env): 30 coalesced words.

@@ -8,6 +8,8 @@ mkdir -p $OUT
 bad() { [ "$1" -ge 124 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; }
 timeout -k 10 120 python3 scripts/diag_gae.py > $OUT/gae_ab.json 2> $OUT/gae_ab.err
 rc=$?; echo "gae ab rc=$rc"; cat $OUT/gae_ab.json | cut -c1-600; bad $rc && exit $rc
+timeout -k 10 120 python3 scripts/diag_collect.py 4096 > $OUT/collect_ab.json 2> $OUT/collect_ab.err
+rc=$?; echo "collect ab rc=$rc"; cat $OUT/collect_ab.json | cut -c1-400; bad $rc && exit $rc
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_bench_ranks.py tests/test_gpu_a2c.py tests/test_gpu_shards.py -m gpu -x -v --timeout 240 --timeout-method thread > $OUT/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 scripts/diag_update_stages.py 4096 > $OUT/stages.json 2> $OUT/stages.err

@@ -220,7 +220,8 @@ def test_bounded_handoff_waits(G, agents):
     sleeps, ~7 us: the first step waits that long for the tables' copy-in) a wait may give up:
     the launch still ends, and a workgroup that gave up
     flags every env it holds (status bit 0x80 | DIVERGED, fault word bit 0) while workgroups that
-    did not are byte-identical to the unbounded run."""
+    did not are byte-identical to the unbounded run; with one workgroup's owner wave held back
+    (option "test_stall") the give-up path provably runs."""
     env = _env(G, 4096, agents)
     env.reset(num_orders=30)
     st = G.to_np(env.rollout(1024, action_seed=3, policy="random"))["status"]
@@ -246,3 +247,22 @@ def test_bounded_handoff_waits(G, agents):
         assert np.array_equal(r1[k][:, ok], r0[k][:, ok]), k
     if flagged.any():
         assert ((r1["status"][-1][flagged] & 0x81) == 0x81).all()
+    # the give-up path itself: workgroup 0's owner wave (k_step_ag's AM, k_step_pipe's sim wave)
+    # sleeps ~0.25 ms before its first step (option "test_stall"), far past the 256-sleep bound
+    # of the other waves' waits for its first post: they give up, the launch still ends, the fault
+    # word says so, and exactly workgroup 0's envs are flagged (env 0 among them); every other
+    # env is byte-identical to the unbounded run
+    stalled = _env(G, n, agents)
+    G.native.check(G.native.lib().fjsp_set_option(stalled.handle, b"spin_cap", 256))
+    G.native.check(G.native.lib().fjsp_set_option(stalled.handle, b"test_stall", 64))
+    stalled.reset(num_orders=30)
+    r2 = G.to_np(stalled.rollout(64, action_seed=5, policy="random"))
+    assert stalled.faults() & 1
+    flagged = (r2["status"][-1] & 0x80) != 0
+    assert flagged[0] and not flagged[64:].any()
+    assert ((r2["status"][-1][flagged] & 0x81) == 0x81).all()
+    ok = ~flagged
+    for k in LEAN:
+        if k == "status":
+            continue
+        assert np.array_equal(r2[k][:, ok], r0[k][:, ok]), k
