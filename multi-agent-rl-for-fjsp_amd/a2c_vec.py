@@ -981,7 +981,7 @@ class VecMultiAgentA2C:
         # the draw key lives on the device for both policy paths: a captured collect reads it
         # at replay time, so every replay draws new actions
         self._rng = torch.zeros(1, dtype=torch.int64, device=self.device)
-        self._rng.fill_(self._rng_host)
+        self._rng.fill_(_s64(self._rng_host))   # the kernel's uint64 key, wrapped to int64
         role_keys(self.device)
         if self.fused_policy:
             self._pw_actor, self._pw_critic = pack_policy_weights(self.actors, self.critic)
@@ -995,7 +995,8 @@ class VecMultiAgentA2C:
         # scripts/ab_update.py), so opt-in
         self.graph_update = False
         self._ugraphs = {}
-        self._upool = None
+        self._st_ret = None
+        self._fallback_ret_adv = None      # GAE of a graphed update that fell back to the eager one
         self._eager_updates = 0
         self.grad_probe = None             # grad_probe(flat reduced grads) before clip / Adam (tests)
         self.exchange_timing = None        # dict of synchronised stage times (ms) when not None (bench)
@@ -1106,7 +1107,7 @@ class VecMultiAgentA2C:
         bootstrap value, ~40 launches per step) is captured once into a hipGraph and replayed:
         the buffers and parameters are static, Adam updates the weights in place."""
         self._rng_host += 1
-        self._rng.fill_(self._rng_host)       # re-keys the sampling of the (captured) batch
+        self._rng.fill_(_s64(self._rng_host))   # re-keys the sampling of the (captured) batch
         if action_fn is None and self.use_graph:
             if self._graph is not None and self._graph_det == deterministic:
                 self._graph.replay()
@@ -1207,7 +1208,8 @@ class VecMultiAgentA2C:
         else:
             t0 = self._start()
             if ret is None:
-                ret, adv = self.advantages()
+                fb, self._fallback_ret_adv = self._fallback_ret_adv, None
+                ret, adv = fb if fb is not None else self.advantages()
             b = self._bufs
             T = self.batch_size
             al, cl = update_step(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
@@ -1232,7 +1234,9 @@ class VecMultiAgentA2C:
         fixed shapes for a given signature of (bucketed) group counts, so it is captured once per
         signature and replayed on static copies of the batch's grouping (~430 launches become
         one; the host-side gaps between them were ~2 ms per update).  Returns (actor losses,
-        critic loss) or None when the caller must run the eager update."""
+        critic loss) or None when the caller must run the eager update (the batch's GAE is kept
+        for it).  After a replay, p.grad is the gradient buffer of the last graph captured, not
+        necessarily of the one replayed: read gradients through grad_probe (eager update)."""
         b = self._bufs
         T = self.batch_size
         t0 = self._start()
@@ -1241,6 +1245,7 @@ class VecMultiAgentA2C:
         gr = RowGroups(group_keys(f3))
         ga, gc = gr.rows(0, NA), gr.rows(NA, NA + 1)
         if not group_verify(f3, ga, gc):
+            self._fallback_ret_adv = (ret, adv)                     # the eager update reuses them
             return None                                             # a hash collision: dense, eager
         U = gr.U
         big = max(range(NA), key=lambda a: U[a])
@@ -1268,8 +1273,7 @@ class VecMultiAgentA2C:
         from . import distributed as D
         T = self.batch_size
         b = self._bufs
-        if self._upool is None:
-            self._upool = torch.cuda.graph_pool_handle()
+        if self._st_ret is None:
             self._st_ret = torch.empty_like(ret)
             self._st_adv = torch.empty_like(adv)
             warm_index_tensors(self.device)
@@ -1285,7 +1289,9 @@ class VecMultiAgentA2C:
         cl_st = torch.zeros(1, dtype=torch.float32, device=self.device)
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(self.device)
-        with torch.cuda.graph(g, pool=self._upool):
+        # a private memory pool per captured signature: the graphs replay in any order, which a
+        # shared pool only allows for graphs replayed in capture order
+        with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle()):
             al, cl = update_core(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
                                  b["masks"][:T], b["actions"], self._st_ret, self._st_adv, self.gidx, self.midx,
                                  self.entropy_coef, self.max_grad_norm, D.LOCAL, True, None, groups)

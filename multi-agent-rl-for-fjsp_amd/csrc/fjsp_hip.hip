@@ -45,11 +45,6 @@ FJSP_DIAG(__device__ unsigned long long g_stamps[8];
 // only every 256 sleeps: nothing of the bound stays live in registers across the step loop (a
 // cap held in an SGPR through the loop pushed the multi-wave kernels into SGPR spills, +6 %).
 __device__ __forceinline__ void spin_until(uint32_t* flag, uint32_t v, uint32_t* abort, const uint32_t* cap) {
-#ifdef FJSP_X_UNBOUNDED   // diagnostic build only: the r02 unbounded wait
-    (void)abort; (void)cap;
-    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
-    return;
-#endif
     for (uint32_t it = 1; __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v; it++) {
         if ((it & 255u) == 0u) {
             if (it >= *cap || __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
@@ -57,9 +52,7 @@ __device__ __forceinline__ void spin_until(uint32_t* flag, uint32_t v, uint32_t*
                 break;
             }
         }
-#ifndef FJSP_X_SPIN_NOSLEEP   // diagnostic build: poll without sleeping
         __builtin_amdgcn_s_sleep(1);
-#endif
     }
 }
 
@@ -1157,11 +1150,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     C.lut = s_lut;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / BLOCK);
     const int lane = threadIdx.x % BLOCK;
-#ifdef FJSP_X_NOXCD   // diagnostic build only: workgroup b holds env block b
-    const int blk = (int)blockIdx.x;
-#else
     const int blk = xcd_block((int)blockIdx.x, (int)gridDim.x);
-#endif
     const int e = blk * EPW + lane;
     const bool valid = lane < EPW && e < S.n;
     const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
@@ -1567,9 +1556,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 const uint32_t t = (uint32_t)(k - 1);
                 uint32_t v[SNAP_N];
                 snap_get(snap[(k - 1) & 1], lane, v);
-#ifndef FJSP_X_NOABORTST
                 if (part == 2 && s_abort) v[SA_ST] |= ST_SPIN_TIMEOUT | ST_DIVERGED;
-#endif
                 FJSP_DIAG(
                 __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the snapshot arrived
                 )
