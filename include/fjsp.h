@@ -18,6 +18,9 @@
  *                       (agents/ execute_action, SimPy run, RewardModel, get_observations)
  *   fjsp_step_many   <- K x FJSPSimulation.step with random actions (train.py:268 sample())
  *   fjsp_gae         <- MultiAgentTransitionMemory.finish_trajectory transition_memory.py:45-105
+ *   fjsp_gae_shared  <- the same over the batched A2C's memories (one critic value per env)
+ *   fjsp_a2c_policy_step <- MultiAgentA2C.learn's collect step: predict -> env.step -> memory.put
+ *                       a2c.py:284-309 (one launch per vector step)
  *   fjsp_pack_a2c    <- MultiAgentA2C._get_global_state / _flatten_obs  a2c.py:118-166
  *   FJSP_ACTIONS_HEURISTIC <- MultiAgentA2C._get_heuristic_actions     a2c.py:390-537
  *   fjsp_read_env    <- FJSPSimulation.get_order_progress   FJSPSimulation.py:260-284
