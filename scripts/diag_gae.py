@@ -42,6 +42,8 @@ def run(T, N, A=8, reps=20):
     for u in (4, 8, 16, 24, 32):
         cases.append((f"u{u}", fn(AB, f"gae_u{u}", GEN), False))
         cases.append((f"shared_u{u}", fn(AB, f"gae_shared_u{u}", SH), True))
+    for u, l in ((16, 2), (16, 3), (16, 4), (32, 2)):
+        cases.append((f"shared_lw_u{u}_l{l}", fn(AB, f"gae_shared_lw_u{u}_l{l}", SH), True))
     cases.append(("lib_gae", L.fjsp_gae, False))
     cases.append(("lib_gae_shared", L.fjsp_gae_shared, True))
     for name, f, shared in cases:
