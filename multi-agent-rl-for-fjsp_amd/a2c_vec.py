@@ -996,6 +996,7 @@ class VecMultiAgentA2C:
         self.graph_update = False
         self._ugraphs = {}
         self._st_ret = None
+        self._upool = None
         self._fallback_ret_adv = None      # GAE of a graphed update that fell back to the eager one
         self._eager_updates = 0
         self.grad_probe = None             # grad_probe(flat reduced grads) before clip / Adam (tests)
@@ -1289,9 +1290,13 @@ class VecMultiAgentA2C:
         cl_st = torch.zeros(1, dtype=torch.float32, device=self.device)
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(self.device)
-        # a private memory pool per captured signature: the graphs replay in any order, which a
-        # shared pool only allows for graphs replayed in capture order
-        with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle()):
+        # one memory pool shared by the signatures' graphs (measured: a private pool per graph made
+        # replays diverge from the eager update, test_graphed_update_equals_eager_update); the
+        # graphs replay in any order, which PyTorch only guarantees for capture order — the
+        # bit-for-bit test against the eager update is what vouches for it (opt-in path)
+        if self._upool is None:
+            self._upool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(g, pool=self._upool):
             al, cl = update_core(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
                                  b["masks"][:T], b["actions"], self._st_ret, self._st_adv, self.gidx, self.midx,
                                  self.entropy_coef, self.max_grad_norm, D.LOCAL, True, None, groups)

@@ -1704,6 +1704,95 @@ __global__ void __launch_bounds__(64) k_gae(const double* __restrict__ r, const 
     }
 }
 
+// The shared-value scan (fjsp_gae_shared, N % 64 == 0) with its loads on a loader wave: per
+// workgroup 64 columns (one agent, 64 consecutive envs), a scan wave and a loader wave that keeps
+// L chunks of U timesteps in flight into an LDS ring by 16-byte LDS DMAs (r: two timesteps per
+// instruction, values four, done flags sixteen: 13 instructions per 16-timestep chunk, waited for
+// by a counted vmcnt), so the scan wave issues only its stores and LDS reads.  Same arithmetic
+// sequence per column as k_gae.  Measured at 256 x 8 x 4 096: 37.4 us against 42.4 us for
+// k_gae<float, true> (scripts/diag_gae.py, profiles/r04/gae_ab.json).
+constexpr int GLW_U = 16, GLW_L = 2;
+struct GaeSlot {
+    double r[GLW_U][64];
+    float v[GLW_U][64];
+    uint8_t d[GLW_U][64];
+};
+__device__ __forceinline__ void dma16(const void* g, void* s) {
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g, (__attribute__((address_space(3))) void*)s,
+                                     16, 0, 0);
+}
+__global__ void __launch_bounds__(128) k_gae_lw(const double* __restrict__ r, const float* __restrict__ v,
+                                               const uint8_t* __restrict__ done, int T, int N, int M, double gamma,
+                                               double lamb, double* __restrict__ ret, double* __restrict__ adv) {
+    constexpr int U = GLW_U, L = GLW_L, S = L + 1, PER = U / 2 + U / 4 + U / 16;
+    static_assert(U % 16 == 0 && PER * (L - 1) <= 63, "chunk shape / vmcnt");
+    __shared__ GaeSlot slot[S];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int m0 = blockIdx.x * 64, e0 = m0 % N;
+    const int nch = (T + U - 1) / U;
+    auto issue = [&](int c) __attribute__((always_inline)) {   // chunk c: timesteps T-1-cU down (rows < 0: row 0)
+        GaeSlot& s = slot[c % S];
+        const int t0 = T - 1 - c * U;
+#pragma unroll
+        for (int i = 0; i < U / 2; i++) {
+            const int t = max(t0 - 2 * i - (lane >> 5), 0);
+            dma16(r + (size_t)t * M + m0 + 2 * (lane & 31), &s.r[2 * i][0]);
+        }
+#pragma unroll
+        for (int i = 0; i < U / 4; i++) {
+            const int t = max(t0 - 4 * i - (lane >> 4), 0);
+            dma16(v + (size_t)t * N + e0 + 4 * (lane & 15), &s.v[4 * i][0]);
+        }
+#pragma unroll
+        for (int i = 0; i < U / 16; i++) {
+            const int t = max(t0 - 16 * i - (lane >> 2), 0);
+            dma16(done + (size_t)t * N + e0 + 16 * (lane & 3), &s.d[16 * i][0]);
+        }
+    };
+    constexpr int VM = PER * (L - 1);   // vmcnt <= VM: every chunk but the last L - 1 issued has landed
+    constexpr int WAIT = (VM & 15) | ((VM >> 4) << 14) | (7 << 4) | (15 << 8);
+    if (wave == 1) {
+        for (int c = 0; c < L; c++) issue(c);
+        __builtin_amdgcn_s_waitcnt(WAIT);
+    }
+    __syncthreads();
+    const int m = m0 + lane;
+    const double gl = gamma * lamb;
+    const double bootv = (double)v[(size_t)T * N + e0 + lane];
+    double nv = 0.0, rr = 0.0, gae = 0.0;
+    for (int p = 0; p < nch; p++) {
+        if (wave == 1) {
+            issue(p + L);                          // into the slot chunk p - 1 held (scanned)
+            __builtin_amdgcn_s_waitcnt(WAIT);      // chunk p + 1 has landed
+        } else {
+            const GaeSlot& s = slot[p % S];
+            const int t0 = T - 1 - p * U;
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const int t = t0 - j;
+                if (t < 0) continue;
+                const uint8_t dj = s.d[j][lane];
+                if (t == T - 1 || dj) {   // a trajectory ends at t
+                    nv = (t == T - 1 && !dj) ? bootv : 0.0;
+                    rr = nv;
+                    gae = 0.0;
+                }
+                const size_t i = (size_t)t * M + m;
+                const double rt = s.r[j][lane];
+                const double vt = (double)s.v[j][lane];
+                rr = rt + gamma * rr;
+                __builtin_nontemporal_store(rr, ret + i);
+                const double td = rt + gamma * nv - vt;
+                gae = td + gl * gae;
+                __builtin_nontemporal_store(gae, adv + i);
+                nv = vt;
+            }
+        }
+        __syncthreads();
+    }
+    if (wave == 1) __builtin_amdgcn_s_waitcnt(0x0F70);   // no LDS DMA outlives the workgroup
+}
+
 }  // namespace
 
 // ================================================================ C-ABI
@@ -2172,8 +2261,12 @@ int fjsp_gae_shared(const double* rewards, const float* values, const uint8_t* d
         return fail("bad GAE shape (T > 0, N > 0, agents > 0)");
     if (!rewards || !values || !done || !ret || !adv) return fail("null GAE buffer");
     const int M = agents * N;
-    hipLaunchKernelGGL((k_gae<float, true>), dim3((M + 63) / 64), dim3(64), 0, (hipStream_t)stream, rewards, values,
-                       done, nullptr, T, N, M, gamma, lamb, ret, adv);
+    if (N % 64 == 0)   // 64-column workgroups never straddle two agents: the loader-wave scan
+        hipLaunchKernelGGL(k_gae_lw, dim3(M / 64), dim3(128), 0, (hipStream_t)stream, rewards, values, done, T, N, M,
+                           gamma, lamb, ret, adv);
+    else
+        hipLaunchKernelGGL((k_gae<float, true>), dim3((M + 63) / 64), dim3(64), 0, (hipStream_t)stream, rewards,
+                           values, done, nullptr, T, N, M, gamma, lamb, ret, adv);
     HIPCHK(hipGetLastError());
     return 0;
 }

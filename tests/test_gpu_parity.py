@@ -182,7 +182,8 @@ def test_gae_vs_oracle_large(G):
         assert P.bits_equal(adv[:, m], aa[:, 0]), m
 
 
-@pytest.mark.parametrize("T,N", [(256, 4096), (1, 70), (15, 64), (16, 130), (17, 1), (33, 257), (200, 1000)])
+@pytest.mark.parametrize("T,N", [(256, 4096), (1, 70), (15, 64), (16, 130), (17, 1), (33, 257), (200, 1000),
+                                 (33, 128), (1, 64), (48, 192), (256, 32768)])
 def test_gae_shared_equals_gae(G, T, N):
     """fjsp_gae_shared (one value per env shared by its 8 agents, bootstrap = row T; the A2C's
     call) == fjsp_gae over the expanded values, bit for bit, for batch lengths around the
