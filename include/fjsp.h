@@ -283,12 +283,15 @@ int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t n, const fl
  * [n] as fjsp_a2c_policy writes them (probabilities are not available here).  out: the step's
  * outputs of this one step, limited to rewards, term, trunc, status, next_masks and feats (each
  * [F][n], any may be NULL; the other fields must be NULL).  Results equal fjsp_a2c_policy
- * followed by fjsp_step with the same arguments, byte for byte.  Stream-ordered on the handle's
- * stream; replaces fjsp_a2c_policy + fjsp_step per vector step (one launch instead of two). */
+ * followed by fjsp_step with the same arguments, byte for byte.  Replaces fjsp_a2c_policy +
+ * fjsp_step per vector step (one launch instead of two).  Only the envs [env_begin, env_begin +
+ * env_count) are processed (whole 64-env tiles: env_begin a multiple of 64, env_count a multiple
+ * of 64 or reaching n; pointers stay those of all n envs), so that launches over disjoint env
+ * ranges can run concurrently on different streams; stream NULL = the handle's stream. */
 int fjsp_a2c_policy_step(fjsp_handle* h, const float* feats, const int8_t* masks, const float* actor_w,
                          const float* critic_w, const uint64_t* seed, uint32_t env_gid0, uint32_t step,
                          int32_t deterministic, uint8_t* actions, float* values, int32_t autoreset,
-                         const fjsp_out* out);
+                         const fjsp_out* out, int32_t env_begin, int32_t env_count, void* hip_stream);
 /* The critic's forward over n samples for the A2C update (a2c.py:692-699 critic(global_states)
  * over the batch; a2c_vec._CriticGrouped): x f32 [38][n] (feature rows, as fjsp_a2c_policy's
  * feats), critic_w packed as for fjsp_a2c_policy -> values f32 [n] and the post-ReLU hidden

@@ -147,7 +147,7 @@ def lib():
         "fjsp_a2c_critic_forward": (I, [P, I, P, P, P, P, P, P]),
         "fjsp_a2c_critic_backward": (I, [P, P, P, I, P, P, P, P, P, P, P]),
         "fjsp_gae_shared": (I, [P, P, P, I, I, I, D, D, P, P, P]),
-        "fjsp_a2c_policy_step": (I, [P, P, P, P, P, P, U32, U32, I, P, P, I, ctypes.POINTER(fjsp_out)]),
+        "fjsp_a2c_policy_step": (I, [P, P, P, P, P, P, U32, U32, I, P, P, I, ctypes.POINTER(fjsp_out), I, I, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -499,11 +499,9 @@ def group_keys(feats):
 
 def bucket(u):
     """A group count rounded up to a coarse bucket (1/16 to 1/8 of the count: ≤ 12.5 % more
-    columns, ~6 % on average), so that the update's shapes repeat from batch to batch and its
-    captured graph (VecMultiAgentA2C._update_graphed, one per shape signature) is replayed
-    instead of recaptured.  Padding groups own no samples: computed, never gathered, zero
-    gradient.  Eager and captured updates use the same buckets, so they agree bit for bit.
-    FJSP_GROUP_BUCKETS=0: exact counts."""
+    columns, ~6 % on average), so that the update's shapes (and the library kernels chosen for
+    them) repeat from batch to batch.  Padding groups own no samples: computed, never gathered,
+    zero gradient.  FJSP_GROUP_BUCKETS=0: exact counts."""
     import os
     u = int(u)
     if os.environ.get("FJSP_GROUP_BUCKETS", "1") == "0" or u <= 64:
@@ -551,7 +549,7 @@ class RowGroups:
         um = bucket(max(g.U))
         g.first, g.ends = self.first[lo:hi, :um], self.ends[lo:hi, :um]
         g.inv, g.perm = self.inv[lo:hi], self.perm[lo:hi]
-        g.rep = None if self.rep is None else self.rep[lo:hi]   # (the captured update keeps none)
+        g.rep = None if self.rep is None else self.rep[lo:hi]
         return g
 
     def gather(self, y):
@@ -738,8 +736,8 @@ class A2CLosses:
     @staticmethod
     def compute(actors, critic, feats, masks, actions, returns, adv, gidx, midx, entropy_coef,
                 adv_mean, adv_std, count, dedup=False, groups=None):
-        """groups = (ga, gc): a verified grouping computed by the caller (the captured update);
-        else dedup groups here (keys, sort, check: two host synchronisations)."""
+        """groups = (ga, gc): a verified grouping computed by the caller; else dedup groups here
+        (keys, sort, check: two host synchronisations)."""
         f3 = feats if feats.dim() == 3 else feats[None]
         T, _, n = f3.shape
         S = T * n
@@ -975,6 +973,9 @@ class VecMultiAgentA2C:
         # ... with the env step inside the same launch (fjsp_a2c_policy_step; False: the policy
         # kernel, then fjsp_step, two launches per vector step, the same bytes)
         self.fused_step = self.fused_policy
+        # env groups of the fused collect, each on a stream of its own (_collect_groups)
+        self.collect_groups = 2
+        self._streams = None
         # sampling key: (seed, batch) -> counter hash per (global env id, step, agent); the same
         # on every rank, the env's global id separates the shards
         self._rng_host = int.from_bytes(__import__("os").urandom(7), "little") if seed is None else int(seed)
@@ -989,16 +990,6 @@ class VecMultiAgentA2C:
         self._graph_det = None
         self._eager_batches = 0
         self.gae_fn = batch_advantages     # finish_trajectory over a batch (tests may inject a CPU stand-in)
-        # the update after the grouping as hipGraphs, one per shape signature (_update_graphed):
-        # bit-identical to the eager update, but measured no faster at 4 096 envs (the update is
-        # GPU-bound: 9.7 ms replayed against 9.0-9.6 eager; every new signature costs a capture,
-        # scripts/ab_update.py), so opt-in
-        self.graph_update = False
-        self._ugraphs = {}
-        self._st_ret = None
-        self._upool = None
-        self._fallback_ret_adv = None      # GAE of a graphed update that fell back to the eager one
-        self._eager_updates = 0
         self.grad_probe = None             # grad_probe(flat reduced grads) before clip / Adam (tests)
         self.exchange_timing = None        # dict of synchronised stage times (ms) when not None (bench)
 
@@ -1061,17 +1052,36 @@ class VecMultiAgentA2C:
                                        P(act_out), P(val_out), P(probs_out), ctypes.c_void_p(stream))
         nat.check(rc)
 
-    def policy_step(self, t, deterministic):
+    def policy_step(self, t, deterministic, env_begin=0, env_count=None, stream=None):
         """Vector step t of the collect in one launch (fjsp_a2c_policy_step): the fused policy's
         actions and values, then the env step of each 64-env tile by its last actor workgroup,
         writing rewards / term / trunc / status and the next observation's masks and features into
-        the rollout slab (bytes equal to policy_fused + fjsp_step)."""
+        the rollout slab (bytes equal to policy_fused + fjsp_step).  env_begin / env_count: the
+        envs of this launch (whole 64-env tiles), on `stream` (default: the current stream)."""
         b = self._bufs
         P = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+        st = (stream or torch.cuda.current_stream(self.device)).cuda_stream
         nat.check(nat.lib().fjsp_a2c_policy_step(self.env.handle, P(b["feats"][t]), P(b["masks"][t]), P(self._pw_actor),
                                                  P(self._pw_critic), P(self._rng), int(self.env.env_id_base), int(t),
                                                  int(bool(deterministic)), P(b["actions"][t]), P(b["values"][t]), 1,
-                                                 ctypes.byref(b["outs"][t])))
+                                                 ctypes.byref(b["outs"][t]), int(env_begin),
+                                                 int(self.N - env_begin if env_count is None else env_count),
+                                                 ctypes.c_void_p(st)))
+
+    def _collect_groups(self):
+        """The collect's env groups: (env_begin, env_count) of whole 64-env tiles, collect_groups of
+        them (fewer when N has fewer tiles).  Each group's chain of vector steps runs on a stream of
+        its own: the groups' launches overlap, so one group's env-step tail runs beside another's
+        network layers (the step's chain needs only its own tiles)."""
+        tiles = -(-self.N // 64)
+        g = max(1, min(int(self.collect_groups), tiles))
+        out, t0 = [], 0
+        for i in range(g):
+            nt = tiles // g + (1 if i < tiles % g else 0)
+            e0, e1 = 64 * t0, min(self.N, 64 * (t0 + nt))
+            out.append((e0, e1 - e0))
+            t0 += nt
+        return out
 
     def repack(self):
         """Refresh the fused kernel's packed weights (after an update / load)."""
@@ -1139,10 +1149,23 @@ class VecMultiAgentA2C:
         h = self.env.handle
         self.env._sync_stream()
         T = self.batch_size
-        for t in range(T):
-            if self.fused_step and action_fn is None:
-                self.policy_step(t, deterministic)
-                continue
+        if self.fused_step and action_fn is None:
+            groups = self._collect_groups()
+            if len(groups) == 1:
+                for t in range(T):
+                    self.policy_step(t, deterministic)
+            else:
+                cur = torch.cuda.current_stream(self.device)
+                if self._streams is None or len(self._streams) != len(groups):
+                    self._streams = [torch.cuda.Stream(self.device) for _ in groups]
+                for s in self._streams:
+                    s.wait_stream(cur)
+                for t in range(T):
+                    for (e0, cnt), s in zip(groups, self._streams):
+                        self.policy_step(t, deterministic, e0, cnt, s)
+                for s in self._streams:
+                    cur.wait_stream(s)
+        for t in range(0 if self.fused_step and action_fn is None else T):
             if self.fused_policy and action_fn is None:
                 self.policy_fused(b["feats"][t], b["masks"][t], t, deterministic, b["actions"][t], b["values"][t])
             else:
@@ -1200,110 +1223,23 @@ class VecMultiAgentA2C:
         if fw:
             raise RuntimeError(f"fjsp step kernels reported fault word {fw:#x} (a hand-off wait gave up): "
                                "the batch's transitions are invalid")
-        res = None
         if self.exchange == "gather" and D.active(self.group):
             al, cl = self._update_gathered()
-        elif (ret is None and self.graph_update and self.grad_probe is None and not D.active(self.group)
-              and self._eager_updates >= 1 and (res := self._update_graphed()) is not None):
-            al, cl = res
         else:
             t0 = self._start()
             if ret is None:
-                fb, self._fallback_ret_adv = self._fallback_ret_adv, None
-                ret, adv = fb if fb is not None else self.advantages()
+                ret, adv = self.advantages()
             b = self._bufs
             T = self.batch_size
             al, cl = update_step(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
                                  b["masks"][:T], b["actions"], ret, adv, self.gidx, self.midx, self.entropy_coef,
                                  self.max_grad_norm, self.group, self.dedup, self.grad_probe)
-            self._eager_updates += 1
             self._mark("learn", t0)
         for a, x in zip(AGENTS, al):
             self.actor_loss_history[a].append(x)
         self.critic_loss_history.append(cl)
-        if res is None:
-            self.repack()                  # the captured update repacks inside its graph
+        self.repack()
         return al, cl
-
-    def _update_graphed(self):
-        """The update with everything after the grouping replayed from a hipGraph.
-
-        Eager: GAE, the grouping keys, the sort and the collision check (two host
-        synchronisations: the group counts set the shapes, a collision falls back to the dense
-        update).  The rest — advantage statistics, the networks on their distinct inputs, the
-        loss head, backward, per-agent clipping, Adam, the policy kernel's weight repack — has
-        fixed shapes for a given signature of (bucketed) group counts, so it is captured once per
-        signature and replayed on static copies of the batch's grouping (~430 launches become
-        one; the host-side gaps between them were ~2 ms per update).  Returns (actor losses,
-        critic loss) or None when the caller must run the eager update (the batch's GAE is kept
-        for it).  After a replay, p.grad is the gradient buffer of the last graph captured, not
-        necessarily of the one replayed: read gradients through grad_probe (eager update)."""
-        b = self._bufs
-        T = self.batch_size
-        t0 = self._start()
-        ret, adv = self.advantages()
-        f3 = b["feats"][:T]
-        gr = RowGroups(group_keys(f3))
-        ga, gc = gr.rows(0, NA), gr.rows(NA, NA + 1)
-        if not group_verify(f3, ga, gc):
-            self._fallback_ret_adv = (ret, adv)                     # the eager update reuses them
-            return None                                             # a hash collision: dense, eager
-        U = gr.U
-        big = max(range(NA), key=lambda a: U[a])
-        sig = (gr.first.shape[1], ga.first.shape[1], gc.first.shape[1], big, bucket(U[big]),
-               bucket(max(U[a] for a in range(NA) if a != big)))
-        e = self._ugraphs.pop(sig, None)
-        if e is None:
-            e = self._capture_update(gr, ret, adv)
-            while len(self._ugraphs) >= 6:                          # least recently used out
-                self._ugraphs.pop(next(iter(self._ugraphs)))
-        self._ugraphs[sig] = e                                      # most recently used last
-        if e.get("fresh"):
-            e["fresh"] = False
-        else:
-            for k in ("first", "ends", "inv", "perm"):
-                getattr(e["gr"], k).copy_(getattr(gr, k))
-            self._st_ret.copy_(ret)
-            self._st_adv.copy_(adv)
-        e["graph"].replay()
-        self._mark("learn", t0)
-        return e["al"].cpu().tolist(), float(e["cl"].cpu()[0])
-
-    def _capture_update(self, gr, ret, adv):
-        """Capture the update after the grouping for the shapes of grouping gr (update_graph)."""
-        from . import distributed as D
-        T = self.batch_size
-        b = self._bufs
-        if self._st_ret is None:
-            self._st_ret = torch.empty_like(ret)
-            self._st_adv = torch.empty_like(adv)
-            warm_index_tensors(self.device)
-        self._st_ret.copy_(ret)
-        self._st_adv.copy_(adv)
-        sgr = RowGroups.__new__(RowGroups)
-        sgr.U = list(gr.U)
-        for k in ("first", "ends", "inv", "perm"):
-            setattr(sgr, k, getattr(gr, k).clone())
-        sgr.rep = None
-        groups = (sgr.rows(0, NA), sgr.rows(NA, NA + 1))
-        al_st = torch.zeros(NA, dtype=torch.float32, device=self.device)
-        cl_st = torch.zeros(1, dtype=torch.float32, device=self.device)
-        g = torch.cuda.CUDAGraph()
-        torch.cuda.synchronize(self.device)
-        # one memory pool shared by the signatures' graphs (measured: a private pool per graph made
-        # replays diverge from the eager update, test_graphed_update_equals_eager_update); the
-        # graphs replay in any order, which PyTorch only guarantees for capture order — the
-        # bit-for-bit test against the eager update is what vouches for it (opt-in path)
-        if self._upool is None:
-            self._upool = torch.cuda.graph_pool_handle()
-        with torch.cuda.graph(g, pool=self._upool):
-            al, cl = update_core(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
-                                 b["masks"][:T], b["actions"], self._st_ret, self._st_adv, self.gidx, self.midx,
-                                 self.entropy_coef, self.max_grad_norm, D.LOCAL, True, None, groups)
-            al_st.copy_(al)
-            cl_st.copy_(cl)
-            self.repack()
-        return {"graph": g, "gr": sgr, "al": al_st, "cl": cl_st, "fresh": True}
 
     def _update_gathered(self):
         """Experience gather into the learner (rank 0 of the group): the reference's

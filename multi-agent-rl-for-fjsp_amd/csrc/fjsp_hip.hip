@@ -2131,21 +2131,26 @@ int fjsp_step(fjsp_handle* h, const uint8_t* actions, const uint8_t* agent_order
 
 int fjsp_a2c_policy_step(fjsp_handle* h, const float* feats, const int8_t* masks, const float* actor_w,
                          const float* critic_w, const uint64_t* seed, uint32_t env_gid0, uint32_t step,
-                         int32_t deterministic, uint8_t* actions, float* values, int32_t autoreset, const fjsp_out* out) {
+                         int32_t deterministic, uint8_t* actions, float* values, int32_t autoreset, const fjsp_out* out,
+                         int32_t env_begin, int32_t env_count, void* stream) {
     if (!h) return fail("null handle");
     if (!h->has_reset) return fail("fjsp_a2c_policy_step before fjsp_reset");
     if (!feats || !masks || !actor_w || !seed || !actions || (values && !critic_w))
         return fail("fjsp_a2c_policy_step: null buffer");
+    if (env_begin < 0 || env_count <= 0 || env_begin % 64 || env_begin + env_count > h->n ||
+        (env_count % 64 && env_begin + env_count != h->n))
+        return fail("fjsp_a2c_policy_step: envs [env_begin, env_begin + env_count) must be whole 64-env tiles of the handle");
     DeviceGuard g(h->device);
-    if (h->timing) HIPCHK(hipEventRecord(h->ev0, h->stream));
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    if (h->timing) HIPCHK(hipEventRecord(h->ev0, st));
     h->last_kernel = "k_policy_step";
     const size_t cnt_words = ((size_t)h->ntiles + 63) & ~(size_t)63;
     const int rc = fjsp_internal_policy_step(feats, masks, h->n, actor_w, critic_w, seed, env_gid0, step, deterministic,
                                              actions, values, h->S, h->dcfg, out ? *out : kNoOut, h->tiles,
-                                             h->tiles + cnt_words, autoreset, h->stream);
+                                             h->tiles + cnt_words, autoreset, env_begin, env_count, st);
     if (rc) return rc;
     if (h->timing) {
-        HIPCHK(hipEventRecord(h->ev1, h->stream));
+        HIPCHK(hipEventRecord(h->ev1, st));
         h->timed = 1;
     }
     return 0;

@@ -309,6 +309,7 @@ struct PolicyArgs {
     float* values;
     float* probs_out;
     int nc, na;   // critic / actor workgroups per role
+    int tile0 = 0;   // first 64-env tile of the launch (k_policy_step over an env range)
 };
 
 // The critic on a tile of 32 envs: layers 1 and 2 one 32-row tile per wave, layer 3 (128 rows)
@@ -630,10 +631,10 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.x;
     if (b < A.nc) {
-        critic_tile<false>(A, b, s_mem, tid, lane, wave, CriticSave{});
+        critic_tile<false>(A, 2 * A.tile0 + b, s_mem, tid, lane, wave, CriticSave{});
         return;
     }
-    const int role = (b - A.nc) / A.na, tile = (b - A.nc) % A.na;
+    const int role = (b - A.nc) / A.na, tile = A.tile0 + (b - A.nc) % A.na;
     int act = 0;
     actor_tile(A, role, tile, s_mem, tid, lane, wave, act);
     if (wave == 0) {
@@ -1070,12 +1071,13 @@ int fjsp_internal_policy_step(const float* feats, const int8_t* masks, int32_t n
                               const float* critic_w, const uint64_t* seed, uint32_t env_gid0, uint32_t step,
                               int32_t deterministic, uint8_t* actions, float* values, const fjsp::DevState& S,
                               const fjsp::Cfg& C, const fjsp_out& out, uint32_t* tile_cnt, uint32_t* tile_act,
-                              int32_t autoreset, hipStream_t stream) {
+                              int32_t autoreset, int32_t env_begin, int32_t env_count, hipStream_t stream) {
     if (out.obs_i32 || out.obs_i8 || out.obs_f32 || out.masks || out.results || out.orders_completed || out.packaged ||
         out.sim_time || out.next_i32 || out.next_i8 || out.next_f32)
         return fjsp_internal_fail("fjsp_a2c_policy_step: outputs limited to rewards, term, trunc, status, next_masks, feats");
+    // envs [env_begin, env_begin + env_count): whole 64-env tiles (the caller checks the range)
     PolicyArgs A{feats, masks, n, actor_w, critic_w, seed, env_gid0, step, deterministic, actions, values, nullptr,
-                 values ? (n + TC - 1) / TC : 0, (n + TA - 1) / TA};
+                 values ? (env_count + TC - 1) / TC : 0, (env_count + TA - 1) / TA, env_begin / TA};
     StepArgs St{S, C, out.rewards, out.term, out.trunc, out.status, out.next_masks, out.feats, tile_cnt, tile_act, autoreset};
     hipLaunchKernelGGL(k_policy_step, dim3((unsigned)(A.nc + NAG * A.na)), dim3(NTHR), 0, stream, A, St);
     const hipError_t err = hipGetLastError();

@@ -329,10 +329,11 @@ __device__ __forceinline__ void step_and_emit(Env& E, const Tables& T, const Cfg
 
 }  // namespace fjsp
 
-// fjsp_policy.hip: the launch of the fused policy + step kernel (fjsp_a2c_policy_step); tile_cnt
-// [ceil(n / 64)] arrival counters (zero between launches), tile_act [ceil(n / 64)][8][16] words.
+// fjsp_policy.hip: the launch of the fused policy + step kernel (fjsp_a2c_policy_step) over the
+// envs [env_begin, env_begin + env_count) (env_begin a multiple of 64); tile_cnt [ceil(n / 64)]
+// arrival counters (zero between launches), tile_act [ceil(n / 64)][8][16] words.
 int fjsp_internal_policy_step(const float* feats, const int8_t* masks, int32_t n, const float* actor_w,
                               const float* critic_w, const uint64_t* seed, uint32_t env_gid0, uint32_t step,
                               int32_t deterministic, uint8_t* actions, float* values, const fjsp::DevState& S,
                               const fjsp::Cfg& C, const fjsp_out& out, uint32_t* tile_cnt, uint32_t* tile_act,
-                              int32_t autoreset, hipStream_t stream);
+                              int32_t autoreset, int32_t env_begin, int32_t env_count, hipStream_t stream);
