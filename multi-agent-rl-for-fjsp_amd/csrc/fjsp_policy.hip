@@ -578,15 +578,29 @@ struct StepArgs {
     int autoreset;
 };
 
+// The tile's state words, [NSTATE][64] u32 after the policy's LDS (STATE_BYTES more per
+// workgroup: 2 x 77.5 KB still fit a CU): every actor workgroup of the tile copies them in with
+// LDS DMAs at its start, in the shadow of its network, so the one that runs the step reads them
+// from LDS instead of waiting a memory round trip after the hand-off.
+constexpr int STATE_BYTES = fjsp::NSTATE * 64 * 4;
+static_assert(2 * (LDS_BYTES + STATE_BYTES) <= 160 * 1024, "two workgroups per CU");
+__device__ __forceinline__ void state_prefetch(const StepArgs& St, int tile, uint32_t* s_state, int lane, int wave) {
+    const int e = min(tile * TA + lane, St.S.n - 1);
+    for (int i = wave; i < fjsp::NSTATE; i += NWAVE)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(St.S.words + (size_t)i * St.S.n + e),
+                                         (__attribute__((address_space(3))) void*)(s_state + i * 64), 4, 0, 0);
+}
+
 __device__ __forceinline__ void tile_step(const PolicyArgs& A, const StepArgs& St, int tile, unsigned char* s_mem,
-                                          int lane) {
+                                          const uint32_t* s_state, int lane) {
     double* s_lut = reinterpret_cast<double*>(s_mem);
     const int e = tile * TA + lane;
     const bool valid = e < A.n;
     fjsp::Env E;
     int act[NAG];
     if (valid) {
-        fjsp::env_load(E, St.S.words, St.S.n, e);
+#pragma unroll
+        for (int i = 0; i < fjsp::NSTATE; i++) E.w[i] = s_state[i * 64 + lane];
         const gu32* ta = (const gu32*)(St.tile_act) + (size_t)tile * NAG * 16 + (lane >> 2);
 #pragma unroll
         for (int a = 0; a < NAG; a++)
@@ -626,7 +640,8 @@ __device__ __forceinline__ void tile_step(const PolicyArgs& A, const StepArgs& S
 }
 
 __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) k_policy_step(PolicyArgs A, StepArgs St) {
-    __shared__ __attribute__((aligned(16))) unsigned char s_mem[LDS_BYTES];
+    __shared__ __attribute__((aligned(16))) unsigned char s_mem[LDS_BYTES + STATE_BYTES];
+    uint32_t* s_state = reinterpret_cast<uint32_t*>(s_mem + LDS_BYTES);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.x;
@@ -635,6 +650,7 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
         return;
     }
     const int role = (b - A.nc) / A.na, tile = A.tile0 + (b - A.nc) % A.na;
+    state_prefetch(St, tile, s_state, lane, wave);   // landed by actor_tile's first barrier
     int act = 0;
     actor_tile(A, role, tile, s_mem, tid, lane, wave, act);
     if (wave == 0) {
@@ -645,8 +661,9 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
         if (lane < 16)
             __hip_atomic_store((gu32*)(St.tile_act) + ((size_t)tile * NAG + role) * 16 + lane, w,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    // every wave: its action stores (wave 0) and its state DMAs into LDS have landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();   // every wave is done with s_mem, the action words are drained
     uint32_t* s_last = reinterpret_cast<uint32_t*>(s_mem + LDS_BYTES - 16);
     if (tid == 0) {
@@ -657,7 +674,7 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
     }
     __syncthreads();
     if (wave != 0 || !*s_last) return;
-    tile_step(A, St, tile, s_mem, lane);
+    tile_step(A, St, tile, s_mem, s_state, lane);
 }
 
 // The critic's forward over n samples for the A2C update (values + the saved hidden layers).
