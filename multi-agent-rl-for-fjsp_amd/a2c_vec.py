@@ -976,6 +976,7 @@ class VecMultiAgentA2C:
         # env groups of the fused collect, each on a stream of its own (_collect_groups)
         self.collect_groups = 2
         self._streams = None
+        self._collect_values = True        # diagnostics: False = the collect without the critic
         # sampling key: (seed, batch) -> counter hash per (global env id, step, agent); the same
         # on every rank, the env's global id separates the shards
         self._rng_host = int.from_bytes(__import__("os").urandom(7), "little") if seed is None else int(seed)
@@ -1063,7 +1064,8 @@ class VecMultiAgentA2C:
         st = (stream or torch.cuda.current_stream(self.device)).cuda_stream
         nat.check(nat.lib().fjsp_a2c_policy_step(self.env.handle, P(b["feats"][t]), P(b["masks"][t]), P(self._pw_actor),
                                                  P(self._pw_critic), P(self._rng), int(self.env.env_id_base), int(t),
-                                                 int(bool(deterministic)), P(b["actions"][t]), P(b["values"][t]), 1,
+                                                 int(bool(deterministic)), P(b["actions"][t]),
+                                                 P(b["values"][t]) if self._collect_values else None, 1,
                                                  ctypes.byref(b["outs"][t]), int(env_begin),
                                                  int(self.N - env_begin if env_count is None else env_count),
                                                  ctypes.c_void_p(st)))

@@ -18,7 +18,7 @@ V = importlib.import_module("multi-agent-rl-for-fjsp_amd.vec_env")
 
 def main(n=4096, T=256, reps=8, init="random", groups=(1, 2, 4, 8)):
     learners = {}
-    modes = [("g%d" % g, True, g) for g in groups] + [("two_launch", False, 1)]
+    modes = [("g%d" % g, True, g) for g in groups] + [("two_launch", False, 1), ("g2_no_critic", True, 2)]
     for name, fused, g in modes:
         env = V.FJSPVecEnv(n)
         L = A.VecMultiAgentA2C(env, batch_size=T, seed=3)
@@ -26,6 +26,7 @@ def main(n=4096, T=256, reps=8, init="random", groups=(1, 2, 4, 8)):
             L.load_state_dicts(A.load_npz_weights(os.path.join(REPO, "tests", "golden", "trained_policy.npz")))
         L.fused_step = fused
         L.collect_groups = g
+        L._collect_values = name != "g2_no_critic"   # what the critic's workgroups cost the collect
         L.reset(seeds=torch.arange(n), num_orders=25)
         for _ in range(3):       # eager, capture, replay
             L.collect()
