@@ -176,9 +176,9 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
  * the stream env value + e of one big handle starts from; stream-ordered); "spin_cap"
  * (256..2^31-1, default 2^22: sleep iterations, checked every 256 a wave of a multi-wave step kernel waits for another
  * wave's hand-off before it gives up and flags FJSP_STATUS_SPIN_TIMEOUT / fjsp_faults); "test_stall"
- * (0..2^20, default 0; tests only: in every later multi-wave step launch, workgroup 0's owner
- * wave sleeps value x ~8k cycles before its first step, so that the other waves' bounded waits
- * give up and the give-up path runs).  spin_cap and test_stall are not part of a snapshot. */
+ * (0..2^20, default 0; tests only: later k_step_ag and k_step_pipe<lds,2emit,predraw> launches
+ * run a test build in which workgroup 0's owner wave sleeps value x ~8k cycles before its first
+ * step, so that the other waves' bounded waits give up and the give-up path runs).  spin_cap and test_stall are not part of a snapshot. */
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value);
 int fjsp_num_envs(const fjsp_handle* h);
 /* Bytes of device state per env (HBM footprint of the SoA state). */
@@ -322,14 +322,17 @@ int fjsp_a2c_group_verify(const float* feats, int32_t T, int32_t n, const int64_
 /* The actor loss head of the grouped update (a2c.py:204-220 masked probabilities, :705-731
  * entropy and calc_actor_loss): pu f32 [8][8][umax] = each agent's action probabilities per
  * distinct input, inv int64 [8][T * n] = each sample's distinct input, masks int8 [T][29][n],
- * actions int64 [8][T * n], adv_n f32 [8][T * n] (normalised advantages).  Out: grad f32
+ * actions u8 [T][8][n] and adv f64 [T][8][n] (the rollout slab's and GAE's layouts; sample
+ * s = t * n + e), adv_mean / adv_std f32 [8] (the advantages are used as
+ * (float(adv) - mean) / (std + 1e-8), calc_actor_loss a2c.py:724-731; both NULL: float(adv)
+ * as is).  Out: grad f32
  * [29][T * n] = d(sum_a actor_loss_a) / d(sample probabilities), row mask_off[a] + j for agent
  * a's valid action j (the 29 action-mask columns' order), and sums f64
  * [8][ceil(T * n / 256)][2] = per agent and block of 256 samples (sum adv_n * logp, sum
  * entropy); the caller adds the blocks.  Stream-ordered. */
 int fjsp_a2c_actor_head(const float* pu, int32_t umax, const int64_t* inv, int32_t T, int32_t n, const int8_t* masks,
-                        const int64_t* actions, const float* adv_n, float inv_count, float ent_coef, float* grad,
-                        double* sums, void* stream);
+                        const uint8_t* actions, const double* adv, const float* adv_mean, const float* adv_std,
+                        float inv_count, float ent_coef, float* grad, double* sums, void* stream);
 /* ReLU backward fused with the bias gradient (the critic backward of the A2C update,
  * a2c.py:713-722 calc_critic_loss through the 256-256-128 ReLU layers): gy, y f32 [rows][cols]
  * (y = the layer's ReLU output), cols 128 or 256.  Out: g f32 [rows][cols] = gy where y > 0

@@ -143,7 +143,7 @@ def lib():
         "fjsp_a2c_group_verify": (I, [P, I, I, P, P, P, P]),
         "fjsp_a2c_relu_bias_grad": (I, [P, P, ctypes.c_int64, I, P, P, P]),
         "fjsp_a2c_value_head_grad": (I, [P, P, P, ctypes.c_int64, P, P, P]),
-        "fjsp_a2c_actor_head": (I, [P, I, P, I, I, P, P, P, ctypes.c_float, ctypes.c_float, P, P, P]),
+        "fjsp_a2c_actor_head": (I, [P, I, P, I, I, P, P, P, P, P, ctypes.c_float, ctypes.c_float, P, P, P]),
         "fjsp_a2c_critic_forward": (I, [P, I, P, P, P, P, P, P]),
         "fjsp_a2c_critic_backward": (I, [P, P, P, I, P, P, P, P, P, P, P]),
         "fjsp_gae_shared": (I, [P, P, P, I, I, I, D, D, P, P, P]),

@@ -621,16 +621,18 @@ class _ActorHead(torch.autograd.Function):
     so its gradient is never used (left 0)."""
 
     @staticmethod
-    def forward(ctx, pu, g, masks, actions, adv_n, count, coef):
+    def forward(ctx, pu, g, masks, actions, adv, adv_mean, adv_std, count, coef):
+        """masks int8 [T, 29, n], actions u8 [T, 8, n], adv f64 [T, 8, n] (the slab's layouts),
+        adv_mean / adv_std f32 [8] (None: the advantages as they are)."""
         T, _, n = masks.shape
         S = T * n
         grad = torch.empty(MASK_DIM, S, dtype=torch.float32, device=pu.device)
         part = torch.empty(NA, -(-S // 256), 2, dtype=torch.float64, device=pu.device)
         pu_c = pu.detach().contiguous()
         stream = torch.cuda.current_stream(pu.device).cuda_stream
-        V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        V = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         nat.check(nat.lib().fjsp_a2c_actor_head(V(pu_c), int(pu_c.shape[2]), V(g.inv), T, n, V(masks), V(actions),
-                                                V(adv_n), 1.0 / count, coef, V(grad), V(part),
+                                                V(adv), V(adv_mean), V(adv_std), 1.0 / count, coef, V(grad), V(part),
                                                 ctypes.c_void_p(stream)))
         sums = part.sum(1)
         ctx.g = g
@@ -654,7 +656,7 @@ class _ActorHead(torch.autograd.Function):
         rs = torch.cat([ce[:, :1], ce[:, 1:] - ce[:, :-1]], dim=1).to(grad.dtype)    # [29, Umax]
         out = torch.zeros(NA * 8, umax, dtype=grad.dtype, device=grad.device)
         out[_valid_rows(grad.device)] = rs
-        return out.view(NA, 8, umax), None, None, None, None, None, None
+        return out.view(NA, 8, umax), None, None, None, None, None, None, None, None
 
 
 _VALID_ROWS = {}
@@ -717,6 +719,13 @@ def _prefix_sum(w, block=1024, dtype=None, add=0):
     return c.view(*lead, P)[..., :S]
 
 
+def slab_cols(f3, idx):
+    """Columns idx (samples s = t * N + e) of a [T, C, N] slab as a [C, len(idx)] view: the
+    gathered columns only, no [C, T * N] transposed copy of the slab."""
+    N = f3.shape[2]
+    return f3[idx // N, :, idx % N].t()
+
+
 class A2CLosses:
     """Loss sums for one (possibly sharded) batch; `count` = the GLOBAL sample count.
 
@@ -736,13 +745,19 @@ class A2CLosses:
     @staticmethod
     def compute(actors, critic, feats, masks, actions, returns, adv, gidx, midx, entropy_coef,
                 adv_mean, adv_std, count, dedup=False, groups=None):
-        """groups = (ga, gc): a verified grouping computed by the caller; else dedup groups here
-        (keys, sort, check: two host synchronisations)."""
+        """The rollout slab's layouts: feats f32 [T, 38, N], masks int8 [T, 29, N], actions u8
+        [T, 8, N], returns / adv f64 [T, 8, N] (a single step may drop the T axis).  groups =
+        (ga, gc): a verified grouping computed by the caller; else dedup groups here (keys, sort,
+        check: two host synchronisations).  On the GPU the grouped path reads the slabs in place
+        (columns gathered per group, the loss head reading actions and advantages in their
+        layouts); [8, S] copies are made for the dense / CPU path only."""
         f3 = feats if feats.dim() == 3 else feats[None]
+        m3 = masks if masks.dim() == 3 else masks[None]
+        a3 = actions if actions.dim() == 3 else actions[None]
+        r3 = returns if returns.dim() == 3 else returns[None]
+        d3 = adv if adv.dim() == 3 else adv[None]
         T, _, n = f3.shape
         S = T * n
-        gt = f3.permute(1, 0, 2).reshape(GLOBAL_DIM, S)                # [38, S]
-        x = None if (dedup or groups is not None) and feats.is_cuda else actor_inputs(feats, gidx)   # [8, 13, S]
         ga = gc = None
         if groups is not None:
             ga, gc = groups
@@ -750,42 +765,47 @@ class A2CLosses:
             f3 = f3.contiguous()
             gr = RowGroups(group_keys(f3))                          # 8 actor rows + the critic's
             ga, gc = gr.rows(0, NA), gr.rows(NA, NA + 1)
+            x = gt = None
+            if not feats.is_cuda:
+                x, gt = actor_inputs(feats, gidx), f3.permute(1, 0, 2).reshape(GLOBAL_DIM, S)
             if not group_verify(f3, ga, gc, x, gt):                 # a hash collision: dense
                 ga = gc = None
-                if x is None:
-                    x = actor_inputs(feats, gidx)
 
-        def cols(agents, idx):                                       # [k, 13, u] from gt
+        def cols(agents, idx):                                       # [k, 13, u] from the slab
             k, u = idx.shape
-            c = gt[:, idx.reshape(-1)].view(GLOBAL_DIM, k, u)
+            c = slab_cols(f3, idx.reshape(-1)).reshape(GLOBAL_DIM, k, u)
             c = torch.cat([c, c.new_zeros(1, k, u)])
             return c[gidx[agents], torch.arange(k, device=idx.device)[:, None], :]
         # the critic first: its GEMMs keep the GPU busy while the host issues the actors' many
         # small launches (after the grouping's host synchronisations the queue is empty)
         if gc is not None and feats.is_cuda and gc.first.shape[1] >= 65536 and critic_fused:
-            vu = critic_grouped(critic, gt[:, gc.first[0]]).reshape(1, 1, -1)
+            vu = critic_grouped(critic, slab_cols(f3, gc.first[0]).contiguous()).reshape(1, 1, -1)
             v = gc.gather(vu).reshape(-1)                            # [S]
         elif gc is not None:
-            vu = mlp_forward(critic.net, gt[:, gc.first[0]].t()).reshape(1, 1, -1)
+            vu = mlp_forward(critic.net, slab_cols(f3, gc.first[0]).t()).reshape(1, 1, -1)
             v = gc.gather(vu).reshape(-1)                            # [S]
         else:
-            v = mlp_forward(critic.net, gt.t()).reshape(-1)
-        adv_n = (adv - adv_mean[:, None]) / (adv_std[:, None] + 1e-8) if count > 1 else adv
+            v = mlp_forward(critic.net, f3.permute(0, 2, 1).reshape(S, GLOBAL_DIM)).reshape(-1)
+        norm = count > 1
         if ga is not None and feats.is_cuda:
-            # the loss head and its gradient in one kernel (fjsp_a2c_actor_head)
-            m3 = (masks if masks.dim() == 3 else masks[None]).contiguous()
-            actor_losses = _ActorHead.apply(actors.forward_rows(x, ga, cols), ga, m3, actions.contiguous(),
-                                            adv_n.float().contiguous(), float(count), float(entropy_coef))
+            # the loss head and its gradient in one kernel (fjsp_a2c_actor_head), on the slabs
+            actor_losses = _ActorHead.apply(actors.forward_rows(None, ga, cols), ga, m3.contiguous(), a3.contiguous(),
+                                            d3.contiguous(), adv_mean if norm else None, adv_std if norm else None,
+                                            float(count), float(entropy_coef))
         else:
+            x = actor_inputs(feats, gidx)                            # [8, 13, S]
+            acts = a3.long().permute(1, 0, 2).reshape(NA, S)
+            adv32 = d3.float().permute(1, 0, 2).reshape(NA, S)        # calc_actor_loss: FloatTensor(adv)
+            adv_n = (adv32 - adv_mean[:, None]) / (adv_std[:, None] + 1e-8) if norm else adv32
             if ga is not None:
                 probs = ga.gather(actors.forward_rows(x, ga, cols))  # [8, 8, S]
             else:
                 probs = actors(x)                                    # [8, 8, S]
             ent = entropy_of(probs)                                  # [8, S]
             pm = masked_probs(probs, agent_masks(masks, midx))
-            logp = categorical_log_prob(pm, actions)                 # [8, S]
+            logp = categorical_log_prob(pm, acts)                    # [8, S]
             actor_losses = -(adv_n * logp).sum(dim=1) / count - entropy_coef * ent.sum(dim=1) / count
-        critic_loss = ((v[None, :] - returns) ** 2).sum() / (NA * count)
+        critic_loss = ((v.view(T, 1, n) - r3.float()) ** 2).sum() / (NA * count)
         return actor_losses, critic_loss
 
 
@@ -880,15 +900,10 @@ def update_core(actors, critic, optim_actor, optim_critic, feats, masks, actions
     critic loss [1] as device tensors.  With groups (a verified grouping) and no group / probe it
     issues no host synchronisation, so a graph can capture it."""
     from . import distributed as D
-    T, _, N = feats.shape
-    S = T * N
-    adv32 = adv.float().permute(1, 0, 2).reshape(NA, S)             # calc_actor_loss: FloatTensor(adv)
-    ret32 = ret.float().permute(1, 0, 2).reshape(NA, S)
-    acts = actions.long().permute(1, 0, 2).reshape(NA, S)
-    count, mean, std = D.adv_stats(adv32, group)
+    count, mean, std = D.adv_stats_slab(adv, group)                  # of FloatTensor(adv), a2c.py:724-731
     optim_actor.zero_grad(set_to_none=True)
     optim_critic.zero_grad(set_to_none=True)
-    actor_losses, critic_loss = A2CLosses.compute(actors, critic, feats, masks, acts, ret32, adv32, gidx, midx,
+    actor_losses, critic_loss = A2CLosses.compute(actors, critic, feats, masks, actions, ret, adv, gidx, midx,
                                                   entropy_coef, mean, std, count, dedup, groups)
     (actor_losses.sum() + critic_loss).backward()
     D.allreduce_grads(list(actors.parameters()) + list(critic.parameters()), group)

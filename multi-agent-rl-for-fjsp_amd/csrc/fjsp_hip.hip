@@ -658,7 +658,9 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
     }
 }
 
-template <bool LDS, int NEMIT, bool PG = false>
+// STALL: the test build of the kernel (option "test_stall"): the production instances carry no
+// code of it (any code there shifted k_step_ag's register allocation: +1.2 % per step, measured).
+template <bool LDS, int NEMIT, bool PG = false, bool STALL = false>
 __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2))) k_step_pipe(DevState S, Cfg C, int K, uint64_t seed,
                                                               uint32_t gid0, uint32_t step0, int mode, int autoreset,
                                                               fjsp_out out) {
@@ -723,7 +725,9 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
         }
     }
     __syncthreads();
-    if (wave == 0 && blockIdx.x == 0) stall_for_test(S);
+    if constexpr (STALL) {
+        if (wave == 0 && blockIdx.x == 0) stall_for_test(S);
+    }
     if (wave == 0) {
         __builtin_amdgcn_s_setprio(3);   // the sim wave is the critical path: win shared issue slots
         Env E;
@@ -1115,7 +1119,7 @@ __device__ __forceinline__ void ag_emit(int part, const uint32_t* v, uint32_t t,
 
 // EPW: envs per workgroup (64, 32 or 16; lanes >= EPW idle): fewer envs per CU spread N envs
 // over more CUs (every workgroup keeps its 150 KB of LDS, so one workgroup per CU).
-template <int EPW>
+template <int EPW, bool STALL = false>   // STALL: the test build (option "test_stall"), see k_step_pipe
 __global__ void __launch_bounds__(AG_WAVES * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2)))
 k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0, int autoreset, fjsp_out out) {
     static_assert(EPW == 64 || EPW == 32 || EPW == 16, "envs per workgroup");
@@ -1244,7 +1248,9 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     FJSP_DIAG(
     if (threadIdx.x == 0) atomicAdd(&g_agstamps[56], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_entry));
     )
-    if (wave == AG_AM && blockIdx.x == 0) stall_for_test(S);
+    if constexpr (STALL) {
+        if (wave == AG_AM && blockIdx.x == 0) stall_for_test(S);
+    }
     if (wave == AG_AM) {
         __builtin_amdgcn_s_setprio(3);   // the machines -> AGV chain is the critical path
         Env E;
@@ -1823,6 +1829,7 @@ struct fjsp_handle {
     // then [ntiles][8][16] action words; outside the state block (not part of a snapshot)
     uint32_t* tiles;
     int ntiles;
+    int test_stall;   // option "test_stall" (tests): launch the STALL builds of the multi-wave kernels
 };
 
 static thread_local std::string g_err;
@@ -2058,6 +2065,7 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
         const uint32_t v = (uint32_t)value;
         HIPCHK(hipStreamSynchronize(h->stream));
         HIPCHK(hipMemcpy(h->S.words + (size_t)NWORDS * h->n + AUX_TEST_STALL, &v, 4, hipMemcpyHostToDevice));
+        h->test_stall = value != 0;
         return 0;
     }
     if (!strcmp(name, "env_id_base")) {
@@ -2210,7 +2218,11 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
             hipLaunchKernelGGL(kern, agrid, dim3(AG_WAVES * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed,
                                env_gid0, step0, autoreset, o);
         };
-        if (epw == 16) launch_ag(k_step_ag<16>);
+        if (h->test_stall) {
+            if (epw == 16) launch_ag(k_step_ag<16, true>);
+            else if (epw == 32) launch_ag(k_step_ag<32, true>);
+            else launch_ag(k_step_ag<64, true>);
+        } else if (epw == 16) launch_ag(k_step_ag<16>);
         else if (epw == 32) launch_ag(k_step_ag<32>);
         else launch_ag(k_step_ag<64>);
     } else if (h->use_pipe && !full && !staged) {
@@ -2220,7 +2232,8 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
             hipLaunchKernelGGL(kern, grid, dim3(waves * BLOCK), 0, h->stream, h->S, h->dcfg, K, action_seed, env_gid0,
                                step0, action_mode, autoreset, o);
         };
-        if (lds && two && pg) launch_pipe(k_step_pipe<true, 2, true>, 4);
+        if (lds && two && pg && h->test_stall) launch_pipe(k_step_pipe<true, 2, true, true>, 4);
+        else if (lds && two && pg) launch_pipe(k_step_pipe<true, 2, true>, 4);
         else if (lds) two ? launch_pipe(k_step_pipe<true, 2>, 3) : launch_pipe(k_step_pipe<true, 1>, 2);
         else two ? launch_pipe(k_step_pipe<false, 2>, 3) : launch_pipe(k_step_pipe<false, 1>, 2);
     } else if (lds) {

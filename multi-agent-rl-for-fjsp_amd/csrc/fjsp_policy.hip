@@ -867,8 +867,9 @@ __global__ void __launch_bounds__(256) k_group_keys(const float* __restrict__ fe
 __global__ void __launch_bounds__(256) k_actor_head(const float* __restrict__ pu, int umax,
                                                     const int64_t* __restrict__ inv, int T, int n,
                                                     const int8_t* __restrict__ masks,
-                                                    const int64_t* __restrict__ actions,
-                                                    const float* __restrict__ adv_n, float inv_count, float ent_coef,
+                                                    const uint8_t* __restrict__ actions,
+                                                    const double* __restrict__ advs, const float* __restrict__ adv_mean,
+                                                    const float* __restrict__ adv_std, float inv_count, float ent_coef,
                                                     float* __restrict__ grad, double* __restrict__ sums) {
     const int a = blockIdx.y;
     const size_t S = (size_t)T * n;
@@ -878,8 +879,11 @@ __global__ void __launch_bounds__(256) k_actor_head(const float* __restrict__ pu
         const size_t t = s / (size_t)n, e = s - t * (size_t)n;
         const size_t u = (size_t)inv[(size_t)a * S + s];
         const int na = c_nact[a], mo = c_mask_off[a];
-        const int act = (int)actions[(size_t)a * S + s];
-        const float adv = adv_n[(size_t)a * S + s];
+        // the rollout slab's layout [T][8][n]: actions u8, GAE advantages f64, normalised here as
+        // calc_actor_loss does on FloatTensor(adv) (a2c.py:724-731): (adv - mean) / (std + 1e-8)
+        const size_t ta = (t * NAG + (size_t)a) * (size_t)n + e;
+        const int act = (int)actions[ta];
+        const float adv = adv_std ? ((float)advs[ta] - adv_mean[a]) / (adv_std[a] + 1e-8f) : (float)advs[ta];
         float p[8], m[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
@@ -1106,14 +1110,15 @@ int fjsp_internal_policy_step(const float* feats, const int8_t* masks, int32_t n
 }   // fjsp_hip.hip: sets fjsp_last_error()
 
 extern "C" int fjsp_a2c_actor_head(const float* pu, int32_t umax, const int64_t* inv, int32_t T, int32_t n,
-                                   const int8_t* masks, const int64_t* actions, const float* adv_n, float inv_count,
-                                   float ent_coef, float* grad, double* sums, void* stream) {
+                                   const int8_t* masks, const uint8_t* actions, const double* adv, const float* adv_mean,
+                                   const float* adv_std, float inv_count, float ent_coef, float* grad, double* sums,
+                                   void* stream) {
     if (T <= 0 || n <= 0 || umax <= 0) return fjsp_internal_fail("fjsp_a2c_actor_head: T, n and umax must be > 0");
-    if (!pu || !inv || !masks || !actions || !adv_n || !grad || !sums)
+    if (!pu || !inv || !masks || !actions || !adv || !grad || !sums || (!adv_mean != !adv_std))
         return fjsp_internal_fail("fjsp_a2c_actor_head: null buffer");
     const size_t S = (size_t)T * (size_t)n;
     hipLaunchKernelGGL(k_actor_head, dim3((unsigned)((S + 255) / 256), NAG), dim3(256), 0, (hipStream_t)stream, pu, umax,
-                       inv, T, n, masks, actions, adv_n, inv_count, ent_coef, grad, sums);
+                       inv, T, n, masks, actions, adv, adv_mean, adv_std, inv_count, ent_coef, grad, sums);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

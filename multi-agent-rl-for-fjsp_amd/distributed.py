@@ -97,6 +97,24 @@ def adv_stats(adv, group=None):
     return int(n.item()), mean.float(), var.clamp_min(0).sqrt().float()
 
 
+def adv_stats_slab(adv, group=None):
+    """adv_stats of the rollout slab's advantages adv f64 [T, A, N] (their f32 values, as
+    calc_actor_loss's FloatTensor(adv)) without an [A, T * N] copy of a long batch: f64 sums over
+    the T and N axes (single process, short batches: Tensor.mean / Tensor.std as before)."""
+    T, A, N = adv.shape
+    if not active(group) and (not adv.is_cuda or T * N < 65536):
+        return adv_stats(adv.float().permute(1, 0, 2).reshape(A, T * N), group)
+    x = adv.float().double()
+    s = torch.stack([x.sum(dim=(0, 2)), (x * x).sum(dim=(0, 2)),
+                     torch.full((A,), float(T * N), dtype=torch.float64, device=adv.device)], dim=1)
+    if active(group):
+        dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
+    n = s[0, 2]
+    mean = s[:, 0] / n
+    var = (s[:, 1] - n * mean * mean) / (n - 1)
+    return int(n.item()), mean.float(), var.clamp_min(0).sqrt().float()
+
+
 def allreduce_grads(params, group=None):
     """Sum every parameter's gradient over ranks with ONE flat bucket (one RCCL ring pass)."""
     if not active(group):

@@ -66,8 +66,8 @@ def run(st):
     adv_n = (adv32 - mean[:, None]) / (std[:, None] + 1e-8)
     pu = L.actors.forward_rows(None, ga, cols)
     mark("actor_forward_rows")
-    al = A._ActorHead.apply(pu, ga, masks.contiguous(), acts.contiguous(), adv_n.float().contiguous(), float(count),
-                            L.entropy_coef)
+    al = A._ActorHead.apply(pu, ga, masks.contiguous(), b["actions"].contiguous(), adv.contiguous(), mean, std,
+                            float(count), L.entropy_coef)
     mark("actor_head")
     vu = A.mlp_forward(L.critic.net, gt[:, gc.first[0]].t()).reshape(1, 1, -1)
     v = gc.gather(vu).reshape(-1)
