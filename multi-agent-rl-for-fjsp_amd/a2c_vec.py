@@ -719,13 +719,6 @@ def _prefix_sum(w, block=1024, dtype=None, add=0):
     return c.view(*lead, P)[..., :S]
 
 
-def slab_cols(f3, idx):
-    """Columns idx (samples s = t * N + e) of a [T, C, N] slab as a [C, len(idx)] view: the
-    gathered columns only, no [C, T * N] transposed copy of the slab."""
-    N = f3.shape[2]
-    return f3[idx // N, :, idx % N].t()
-
-
 class A2CLosses:
     """Loss sums for one (possibly sharded) batch; `count` = the GLOBAL sample count.
 
@@ -748,9 +741,8 @@ class A2CLosses:
         """The rollout slab's layouts: feats f32 [T, 38, N], masks int8 [T, 29, N], actions u8
         [T, 8, N], returns / adv f64 [T, 8, N] (a single step may drop the T axis).  groups =
         (ga, gc): a verified grouping computed by the caller; else dedup groups here (keys, sort,
-        check: two host synchronisations).  On the GPU the grouped path reads the slabs in place
-        (columns gathered per group, the loss head reading actions and advantages in their
-        layouts); [8, S] copies are made for the dense / CPU path only."""
+        check: two host synchronisations).  On the GPU the grouped path's loss head reads actions
+        and advantages in the slab layouts; [8, S] copies are made for the dense / CPU path only."""
         f3 = feats if feats.dim() == 3 else feats[None]
         m3 = masks if masks.dim() == 3 else masks[None]
         a3 = actions if actions.dim() == 3 else actions[None]
@@ -765,27 +757,32 @@ class A2CLosses:
             f3 = f3.contiguous()
             gr = RowGroups(group_keys(f3))                          # 8 actor rows + the critic's
             ga, gc = gr.rows(0, NA), gr.rows(NA, NA + 1)
-            x = gt = None
+            x = gv = None
             if not feats.is_cuda:
-                x, gt = actor_inputs(feats, gidx), f3.permute(1, 0, 2).reshape(GLOBAL_DIM, S)
-            if not group_verify(f3, ga, gc, x, gt):                 # a hash collision: dense
+                x, gv = actor_inputs(feats, gidx), f3.permute(1, 0, 2).reshape(GLOBAL_DIM, S)
+            if not group_verify(f3, ga, gc, x, gv):                 # a hash collision: dense
                 ga = gc = None
 
-        def cols(agents, idx):                                       # [k, 13, u] from the slab
+        # the global states as feature rows [38, S]: one copy of the slab, then row-wise gathers
+        # of the groups' representatives (gathering the [T, 38, N] slab's columns directly, 38
+        # strided loads per column plus a transpose, measured slower: profiles/r04/a2c/)
+        gt = f3.permute(1, 0, 2).reshape(GLOBAL_DIM, S)
+
+        def cols(agents, idx):                                       # [k, 13, u] from gt
             k, u = idx.shape
-            c = slab_cols(f3, idx.reshape(-1)).reshape(GLOBAL_DIM, k, u)
+            c = gt[:, idx.reshape(-1)].view(GLOBAL_DIM, k, u)
             c = torch.cat([c, c.new_zeros(1, k, u)])
             return c[gidx[agents], torch.arange(k, device=idx.device)[:, None], :]
         # the critic first: its GEMMs keep the GPU busy while the host issues the actors' many
         # small launches (after the grouping's host synchronisations the queue is empty)
         if gc is not None and feats.is_cuda and gc.first.shape[1] >= 65536 and critic_fused:
-            vu = critic_grouped(critic, slab_cols(f3, gc.first[0]).contiguous()).reshape(1, 1, -1)
+            vu = critic_grouped(critic, gt[:, gc.first[0]]).reshape(1, 1, -1)
             v = gc.gather(vu).reshape(-1)                            # [S]
         elif gc is not None:
-            vu = mlp_forward(critic.net, slab_cols(f3, gc.first[0]).t()).reshape(1, 1, -1)
+            vu = mlp_forward(critic.net, gt[:, gc.first[0]].t()).reshape(1, 1, -1)
             v = gc.gather(vu).reshape(-1)                            # [S]
         else:
-            v = mlp_forward(critic.net, f3.permute(0, 2, 1).reshape(S, GLOBAL_DIM)).reshape(-1)
+            v = mlp_forward(critic.net, gt.t()).reshape(-1)
         norm = count > 1
         if ga is not None and feats.is_cuda:
             # the loss head and its gradient in one kernel (fjsp_a2c_actor_head), on the slabs
