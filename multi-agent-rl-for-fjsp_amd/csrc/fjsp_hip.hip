@@ -1117,11 +1117,45 @@ __device__ __forceinline__ void ag_emit(int part, const uint32_t* v, uint32_t t,
 }
 
 
+__device__ constexpr fjsp_out kNoOutDev = {};
+// k_step_ag's kernel arguments, read per role from the kernarg segment through a pointer the
+// compiler cannot see through (`opaque`): a value read once at the kernel's entry stays in an
+// SGPR through every role's step loop (the state pointers, the config, the output pointers and
+// the action stream: 44 SGPR spills, ~400 v_readlane reloads in r03's build); read inside the
+// role's branch it lives only there.  (volatile reads of the by-value parameters copied them to
+// scratch.)  Same layout as the parameter list.
+struct AgArgs {
+    DevState S;
+    Cfg C;
+    int K;
+    uint64_t seed;
+    uint32_t gid0, step0;
+    int autoreset;
+    fjsp_out out;
+};
+static_assert(sizeof(DevState) == 64 && sizeof(Cfg) == 48 && offsetof(AgArgs, C) == 64 && offsetof(AgArgs, K) == 112 &&
+                  offsetof(AgArgs, seed) == 120 && offsetof(AgArgs, gid0) == 128 && offsetof(AgArgs, autoreset) == 136 &&
+                  offsetof(AgArgs, out) == 144,
+              "AgArgs mirrors k_step_ag's kernel arguments (the kernarg segment's layout)");
+template <class T>
+__device__ __forceinline__ const T* opaque(const T* p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+__device__ __forceinline__ const AgArgs* ag_args() {
+    return opaque(reinterpret_cast<const AgArgs*>(__builtin_amdgcn_kernarg_segment_ptr()));
+}
+__device__ __forceinline__ Cfg cfg_at(const AgArgs* a, const double* lut) {
+    Cfg c = a->C;
+    c.lut = lut;
+    return c;
+}
+
 // EPW: envs per workgroup (64, 32 or 16; lanes >= EPW idle): fewer envs per CU spread N envs
 // over more CUs (every workgroup keeps its 150 KB of LDS, so one workgroup per CU).
 template <int EPW, bool STALL = false>   // STALL: the test build (option "test_stall"), see k_step_pipe
 __global__ void __launch_bounds__(AG_WAVES * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2)))
-k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0, int autoreset, fjsp_out out) {
+k_step_ag(DevState S, Cfg Ck, int K, uint64_t seed, uint32_t gid0, uint32_t step0, int autoreset, fjsp_out out) {
     static_assert(EPW == 64 || EPW == 32 || EPW == 16, "envs per workgroup");
     FJSP_DIAG(
     const uint64_t t_entry = __builtin_amdgcn_s_memtime();
@@ -1150,8 +1184,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
     __shared__ uint4 s_pk[BLOCK];   // E3: W0, W4, W5, W7 after step k+1's pickup
     __shared__ uint2 s_pkr[BLOCK];  // E3: its result word, status bits
     __shared__ double s_lut[RLUT_SIZE];
-    for (int i = threadIdx.x; i < RLUT_SIZE; i += AG_WAVES * BLOCK) s_lut[i] = C.lut[i];
-    C.lut = s_lut;
+    for (int i = threadIdx.x; i < RLUT_SIZE; i += AG_WAVES * BLOCK) s_lut[i] = Ck.lut[i];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / BLOCK);
     const int lane = threadIdx.x % BLOCK;
     const int blk = xcd_block((int)blockIdx.x, (int)gridDim.x);
@@ -1252,6 +1285,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         if (wave == AG_AM && blockIdx.x == 0) stall_for_test(S);
     }
     if (wave == AG_AM) {
+        const Cfg C = cfg_at(ag_args(), s_lut);
         __builtin_amdgcn_s_setprio(3);   // the machines -> AGV chain is the critical path
         Env E;
         if (valid) env_load(E, S.words, S.n, e);
@@ -1367,6 +1401,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 if (!((K_WORDS >> i) & 1u)) S.words[i * n + e] = E.w[i];
         }
     } else if (wave == AG_K) {
+        const Cfg C = cfg_at(ag_args(), s_lut);
         __builtin_amdgcn_s_setprio(2);
         Env E;
 #pragma unroll
@@ -1457,6 +1492,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 if ((K_WORDS >> i) & 1u) S.words[i * n + e] = E.w[i];
         }
     } else if (wave == AG_P) {
+        const Cfg C = cfg_at(ag_args(), s_lut);
         __builtin_amdgcn_s_setprio(3);
         // W6..W12 after this wave's last AGV: the next AGV's own words and the list fronts it
         // prefetches, unless AM reset the env (or the launch starts): then AM's post of the step
@@ -1521,8 +1557,15 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         // int8 fields, term, trunc, status, the AGV's pickup / drop masks; E3: step k+1's pickup
         // station (for P), the other masks (balanced by measured cycles: scripts/diag_ag_stamps.py;
         // E0 shares P's SIMD)
+        const Cfg C = cfg_at(ag_args(), s_lut);
         const int part = wave == AG_E0 ? 0 : wave == AG_E1 ? 1 : wave == AG_E2 ? 2 : 3;
         if (part == 3) __builtin_amdgcn_s_setprio(2);   // E3 runs the pickup station for P first
+        const AgArgs* ea = ag_args();   // the outputs and E0's action stream, read in this branch
+        fjsp_out eo = kNoOutDev;
+        eo.obs_i32 = ea->out.obs_i32; eo.obs_i8 = ea->out.obs_i8; eo.obs_f32 = ea->out.obs_f32; eo.masks = ea->out.masks;
+        eo.rewards = ea->out.rewards; eo.term = ea->out.term; eo.trunc = ea->out.trunc; eo.status = ea->out.status;
+        const uint64_t eseed = ea->seed;
+        const uint32_t egid = ea->gid0 + (uint32_t)e, estep = ea->step0;
         for (int k = 0; k <= K; k++) {
             AG_T0();
             if (part == 3 && k + 1 < K) {   // step k+1's pickup station, from P's AGV result of step k
@@ -1554,7 +1597,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
             AG_MARK(0);
             if (part == 0 && k + 2 < K) {   // E0 draws step k + 2's actions (uniform random)
                 int act[NA];
-                synth_uniform(seed, gid0 + (uint32_t)e, step0 + (uint32_t)(k + 2), act);
+                synth_uniform(eseed, egid, estep + (uint32_t)(k + 2), act);
                 s_act[(k + 2) % 3][0][lane] = pack_actions(act, 0);
                 s_act[(k + 2) % 3][1][lane] = pack_actions(act, 4);
             }
@@ -1567,7 +1610,7 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
                 __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the snapshot arrived
                 )
                 AG_MARK(1);
-                ag_emit(part, v, t, n, ue, C, out);
+                ag_emit(part, v, t, n, ue, C, eo);
             }
             AG_MARK(2);
             AG_ACC(ag_busy);
@@ -1575,17 +1618,20 @@ k_step_ag(DevState S, Cfg C, int K, uint64_t seed, uint32_t gid0, uint32_t step0
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) report_abort(S, s_abort);
+    // the state pointers read again for the copy-out (otherwise live in SGPRs through every
+    // role's step loop)
+    const DevState So = ag_args()->S;
+    if (threadIdx.x == 0) report_abort(So, s_abort);
     FJSP_DIAG(
     const uint64_t t_out = __builtin_amdgcn_s_memtime();
     )
     if (valid) {   // the order table and the used slot prefix back to HBM, rows r = wave (mod 8)
         const uint32_t no = s_act[0][0][lane], ns = s_act[0][1][lane];
-        for (uint32_t o = (uint32_t)wave; o < no; o += AG_WAVES) S.orders[(size_t)o * n + e] = TL.orders[o * BLOCK];
+        for (uint32_t o = (uint32_t)wave; o < no; o += AG_WAVES) So.orders[(size_t)o * n + e] = TL.orders[o * BLOCK];
         for (uint32_t q = (uint32_t)wave; q < ns; q += AG_WAVES) {
-            S.scode[(size_t)q * n + e] = TL.scode[q * BLOCK];
-            S.snext[(size_t)q * n + e] = TL.snext[q * BLOCK];
-            S.scstep[(size_t)q * n + e] = TL.scstep[q * BLOCK];
+            So.scode[(size_t)q * n + e] = TL.scode[q * BLOCK];
+            So.snext[(size_t)q * n + e] = TL.snext[q * BLOCK];
+            So.scstep[(size_t)q * n + e] = TL.scstep[q * BLOCK];
         }
     }
     FJSP_DIAG(
