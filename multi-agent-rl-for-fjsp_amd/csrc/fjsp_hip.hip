@@ -1143,7 +1143,7 @@ __device__ __forceinline__ const T* opaque(const T* p) {
     return p;
 }
 __device__ __forceinline__ const AgArgs* ag_args() {
-    return opaque(reinterpret_cast<const AgArgs*>(__builtin_amdgcn_kernarg_segment_ptr()));
+    return opaque((const AgArgs*)__builtin_amdgcn_kernarg_segment_ptr());
 }
 __device__ __forceinline__ Cfg cfg_at(const AgArgs* a, const double* lut) {
     Cfg c = a->C;
