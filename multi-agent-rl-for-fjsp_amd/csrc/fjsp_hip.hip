@@ -658,10 +658,66 @@ __device__ __forceinline__ void predraw_wave(const DevState& S, int K, int lane,
     }
 }
 
+__device__ constexpr fjsp_out kNoOutDev = {};
+// The multi-wave kernels' arguments (k_step_pipe, k_step_ag), read per role from the kernarg
+// segment through a pointer the compiler cannot see through (`opaque`): a value read once at the
+// kernel's entry stays in an SGPR through every role's step loop (the state pointers, the config,
+// the output pointers and the action stream: 44 SGPR spills, ~400 v_readlane reloads in r03's
+// k_step_ag); read inside the role's branch it lives only there.  (volatile reads of the by-value
+// parameters copied them to scratch.)  Same layouts as the parameter lists.
+struct PipeArgs {
+    DevState S;
+    Cfg C;
+    int K;
+    uint64_t seed;
+    uint32_t gid0, step0;
+    int mode, autoreset;
+    fjsp_out out;
+};
+struct AgArgs {
+    DevState S;
+    Cfg C;
+    int K;
+    uint64_t seed;
+    uint32_t gid0, step0;
+    int autoreset;
+    fjsp_out out;
+};
+static_assert(sizeof(DevState) == 64 && sizeof(Cfg) == 48 && offsetof(AgArgs, C) == 64 && offsetof(AgArgs, K) == 112 &&
+                  offsetof(AgArgs, seed) == 120 && offsetof(AgArgs, gid0) == 128 && offsetof(AgArgs, autoreset) == 136 &&
+                  offsetof(AgArgs, out) == 144,
+              "AgArgs mirrors k_step_ag's kernel arguments (the kernarg segment's layout)");
+static_assert(offsetof(PipeArgs, K) == 112 && offsetof(PipeArgs, seed) == 120 && offsetof(PipeArgs, step0) == 132 &&
+                  offsetof(PipeArgs, mode) == 136 && offsetof(PipeArgs, autoreset) == 140 && offsetof(PipeArgs, out) == 144,
+              "PipeArgs mirrors k_step_pipe's kernel arguments");
+template <class T>
+__device__ __forceinline__ const T* opaque(const T* p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+template <class A>
+__device__ __forceinline__ const A* kargs() {
+    return opaque((const A*)__builtin_amdgcn_kernarg_segment_ptr());
+}
+__device__ __forceinline__ const AgArgs* ag_args() { return kargs<AgArgs>(); }
+template <class A>
+__device__ __forceinline__ Cfg cfg_at(const A* a, const double* lut) {
+    Cfg c = a->C;
+    c.lut = lut;
+    return c;
+}
+// the outputs a role writes, read in its branch
+__device__ __forceinline__ fjsp_out out_at(const fjsp_out& o) {
+    fjsp_out r = kNoOutDev;
+    r.obs_i32 = o.obs_i32; r.obs_i8 = o.obs_i8; r.obs_f32 = o.obs_f32; r.masks = o.masks;
+    r.rewards = o.rewards; r.term = o.term; r.trunc = o.trunc; r.status = o.status;
+    return r;
+}
+
 // STALL: the test build of the kernel (option "test_stall"): the production instances carry no
 // code of it (any code there shifted k_step_ag's register allocation: +1.2 % per step, measured).
 template <bool LDS, int NEMIT, bool PG = false, bool STALL = false>
-__global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2))) k_step_pipe(DevState S, Cfg C, int K, uint64_t seed,
+__global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgpu_waves_per_eu(1, 2))) k_step_pipe(DevState S, Cfg Ck, int K, uint64_t seed,
                                                               uint32_t gid0, uint32_t step0, int mode, int autoreset,
                                                               fjsp_out out) {
     static_assert(!PG || LDS, "the pre-drawn tables live in LDS");
@@ -690,8 +746,7 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
     __shared__ PipeSnap snap[2];
     __shared__ uint32_t s_act[2][2][BLOCK];
     __shared__ double s_lut[RLUT_SIZE];
-    for (int i = threadIdx.x; i < RLUT_SIZE; i += (1 + NEMIT + PG) * BLOCK) s_lut[i] = C.lut[i];
-    C.lut = s_lut;
+    for (int i = threadIdx.x; i < RLUT_SIZE; i += (1 + NEMIT + PG) * BLOCK) s_lut[i] = Ck.lut[i];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / BLOCK);
     const int lane = threadIdx.x % BLOCK;
     const int e = blockIdx.x * BLOCK + lane;
@@ -729,6 +784,13 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
         if (wave == 0 && blockIdx.x == 0) stall_for_test(S);
     }
     if (wave == 0) {
+        // the config and the action stream read in this branch (kargs)
+        const PipeArgs* pa = kargs<PipeArgs>();
+        const DevState S = pa->S;
+        const Cfg C = cfg_at(pa, s_lut);
+        const uint64_t seed = pa->seed;
+        const uint32_t gid0 = pa->gid0, step0 = pa->step0;
+        const int mode = pa->mode;
         __builtin_amdgcn_s_setprio(3);   // the sim wave is the critical path: win shared issue slots
         Env E;
         if (valid) env_load(E, S.words, S.n, e);
@@ -856,6 +918,12 @@ __global__ void __launch_bounds__((1 + NEMIT + PG) * BLOCK) __attribute__((amdgp
         // observation fields (+ the next step's uniform actions), wave 2 int8 fields, masks,
         // term, trunc, status.  NEMIT == 1 (many envs: the CUs are already full): one wave.
         const int part = wave - 1;
+        // the config, the outputs and the action stream read in this branch (kargs)
+        const PipeArgs* pa = kargs<PipeArgs>();
+        const Cfg C = cfg_at(pa, s_lut);
+        const fjsp_out out = out_at(pa->out);
+        const uint64_t seed = pa->seed;
+        const uint32_t gid0 = pa->gid0, step0 = pa->step0;
         FJSP_DIAG(
         uint64_t em_busy = 0;
         )
@@ -1116,40 +1184,6 @@ __device__ __forceinline__ void ag_emit(int part, const uint32_t* v, uint32_t t,
     }
 }
 
-
-__device__ constexpr fjsp_out kNoOutDev = {};
-// k_step_ag's kernel arguments, read per role from the kernarg segment through a pointer the
-// compiler cannot see through (`opaque`): a value read once at the kernel's entry stays in an
-// SGPR through every role's step loop (the state pointers, the config, the output pointers and
-// the action stream: 44 SGPR spills, ~400 v_readlane reloads in r03's build); read inside the
-// role's branch it lives only there.  (volatile reads of the by-value parameters copied them to
-// scratch.)  Same layout as the parameter list.
-struct AgArgs {
-    DevState S;
-    Cfg C;
-    int K;
-    uint64_t seed;
-    uint32_t gid0, step0;
-    int autoreset;
-    fjsp_out out;
-};
-static_assert(sizeof(DevState) == 64 && sizeof(Cfg) == 48 && offsetof(AgArgs, C) == 64 && offsetof(AgArgs, K) == 112 &&
-                  offsetof(AgArgs, seed) == 120 && offsetof(AgArgs, gid0) == 128 && offsetof(AgArgs, autoreset) == 136 &&
-                  offsetof(AgArgs, out) == 144,
-              "AgArgs mirrors k_step_ag's kernel arguments (the kernarg segment's layout)");
-template <class T>
-__device__ __forceinline__ const T* opaque(const T* p) {
-    asm volatile("" : "+s"(p));
-    return p;
-}
-__device__ __forceinline__ const AgArgs* ag_args() {
-    return opaque((const AgArgs*)__builtin_amdgcn_kernarg_segment_ptr());
-}
-__device__ __forceinline__ Cfg cfg_at(const AgArgs* a, const double* lut) {
-    Cfg c = a->C;
-    c.lut = lut;
-    return c;
-}
 
 // EPW: envs per workgroup (64, 32 or 16; lanes >= EPW idle): fewer envs per CU spread N envs
 // over more CUs (every workgroup keeps its 150 KB of LDS, so one workgroup per CU).
