@@ -7,6 +7,7 @@ current one.
 
 usage: python scripts/ab_step.py [N] [reps] [lib[:option=value]] ...
   e.g. ab_step.py 4096 8 multi-agent-rl-for-fjsp_amd/libfjsp.so:xcd_map=0 multi-agent-rl-for-fjsp_amd/libfjsp.so:xcd_map=1
+  (option nostatus=1: the launch without the status output)
 """
 import ctypes
 import json
@@ -53,12 +54,18 @@ for sp in specs:
     h = P()
     cfg = nat.default_config()
     chk(L, L.fjsp_create(ctypes.byref(cfg), N, 0, P(stream.cuda_stream), ctypes.byref(h)))
+    nostatus = False
     for kv in filter(None, opt.split(",")):
         k, v = kv.split("=")
+        if k == "nostatus":   # the launch without the status output stream
+            nostatus = bool(int(v))
+            continue
         chk(L, L.fjsp_set_option(h, k.encode(), int(v)))
     seeds = torch.arange(N, dtype=torch.int32, device="cuda")
     chk(L, L.fjsp_reset(h, P(seeds.data_ptr()), None, 30, None))
     buf = V.Buffers(K, N, torch.device("cuda"), infos=False)
+    if nostatus:
+        buf.status = None
     variants.append({"spec": sp, "L": L, "h": h, "buf": buf, "t": 0, "ms": []})
 
 first = []
@@ -78,7 +85,7 @@ for r in range(REPS):
         v["ms"].append(e0.elapsed_time(e1))
 out = {"N": N, "K": K, "reps": REPS, "variants": []}
 for i, v in enumerate(variants):
-    same = all(first[i][k].tobytes() == first[0][k].tobytes() for k in first[0])
+    same = all(first[i][k].tobytes() == first[0][k].tobytes() for k in first[0] if k in first[i])
     out["variants"].append({"spec": v["spec"], "median_ms": float(np.median(v["ms"])), "mean_ms": float(np.mean(v["ms"])),
                             "min_ms": float(np.min(v["ms"])), "us_per_step_median": float(np.median(v["ms"])) * 1e3 / K,
                             "bytes_equal_to_first": same})
