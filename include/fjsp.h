@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define FJSP_ABI_VERSION 7
+#define FJSP_ABI_VERSION 8
 
 #define FJSP_NUM_AGENTS 8      /* pickup, agv, small, big, pkg_blue_1, pkg_blue_2, pkg_red, pkg_green */
 #define FJSP_OBS_I32 20        /* pickup 7 + agv 13 (position = 2) int32 observation fields */
@@ -312,12 +312,17 @@ int fjsp_a2c_critic_backward(const float* g3, const float* h1, const float* h2, 
  * a hash of actor a's padded input (its a2c.py:118-134 observation block, zero-padded to 13
  * columns), row 8 of the critic's 38-column global state (a2c.py:153-166); equal inputs get
  * equal keys (the caller verifies the grouping).  Stream-ordered on `stream`. */
-int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uint64_t* keys, void* stream);
-/* The check of that grouping: rep_a int64 [8][T * n] / rep_c int64 [T * n] = the representative
- * sample of each sample's actor-input / global-state group.  bad int32 [ceil(T * n / 256)] = 1
- * for a block of 256 samples holding one whose inputs differ bitwise from its representative's
- * (a hash collision: the caller falls back to the dense update), else 0.  Stream-ordered. */
-int fjsp_a2c_group_verify(const float* feats, int32_t T, int32_t n, const int64_t* rep_a, const int64_t* rep_c,
+int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uint64_t* keys, float* rows, void* stream);
+/* rows (ABI 8; may be NULL, else 16-byte aligned): f32 [T * n][40], each sample's 38 features as
+ * a sample-major row (2 zero words of padding), written by the same pass: the input of
+ * fjsp_a2c_group_verify.
+ * The check of that grouping: rep_a int64 [8][T * n] / rep_c int64 [T * n] = the representative
+ * sample of each sample's actor-input / global-state group, rows = fjsp_a2c_group_keys' rows
+ * (ABI 8; ABI 7 read the feature-major slab: 38 scattered words per representative).  bad int32
+ * [ceil(T * n / 256)] = 1 for a block of 256 samples holding one whose inputs differ bitwise from
+ * its representative's (a hash collision: the caller falls back to the dense update), else 0.
+ * Stream-ordered. */
+int fjsp_a2c_group_verify(const float* rows, int32_t T, int32_t n, const int64_t* rep_a, const int64_t* rep_c,
                           int32_t* bad, void* stream);
 /* The actor loss head of the grouped update (a2c.py:204-220 masked probabilities, :705-731
  * entropy and calc_actor_loss): pu f32 [8][8][umax] = each agent's action probabilities per

@@ -72,7 +72,7 @@ EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_c
 POLICY_ACTOR_DPAD, POLICY_CRITIC_DPAD = 16, 48
 POLICY_ACTOR_FLOATS = 3 * 256 * 16 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 8 * 256 + 16
 POLICY_CRITIC_FLOATS = 3 * 256 * 48 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 3 * 128 * 256 // 2 + 128 + 128 + 16
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _lib = None
 
@@ -139,7 +139,7 @@ def lib():
         "fjsp_last_kernel": (ctypes.c_char_p, [P]),
         "fjsp_faults": (I, [P, ctypes.POINTER(U32), I]),
         "fjsp_a2c_policy": (I, [P, P, I, P, P, P, U32, U32, I, P, P, P, P]),
-        "fjsp_a2c_group_keys": (I, [P, I, I, P, P]),
+        "fjsp_a2c_group_keys": (I, [P, I, I, P, P, P]),
         "fjsp_a2c_group_verify": (I, [P, I, I, P, P, P, P]),
         "fjsp_a2c_relu_bias_grad": (I, [P, P, ctypes.c_int64, I, P, P, P]),
         "fjsp_a2c_value_head_grad": (I, [P, P, P, ctypes.c_int64, P, P, P]),

@@ -480,16 +480,23 @@ def row_keys(x):
     return k
 
 
-def group_keys(feats):
+GROUP_ROW = 40   # floats per sample-major feature row (38 + 2 zeros), fjsp_a2c_group_keys' rows
+
+
+def group_keys(feats, rows=None):
     """feats f32 [T, 38, N] -> int64 [9, T*N]: row a < 8 = row_keys of actor a's padded inputs
     (actor_inputs), row 8 = row_keys of the critic's global state; on the GPU one pass of the
-    fjsp_a2c_group_keys kernel (the same hash)."""
+    fjsp_a2c_group_keys kernel (the same hash), which also writes each sample's features to rows
+    f32 [T*N, 40] (sample-major, zero-padded: group_verify's input) when rows is given."""
     T, _, N = feats.shape
     if feats.is_cuda:
         f = feats.contiguous()
         keys = torch.empty(NA + 1, T * N, dtype=torch.int64, device=feats.device)
+        if rows is not None:
+            assert rows.is_contiguous() and rows.shape == (T * N, GROUP_ROW) and rows.dtype == torch.float32
         stream = torch.cuda.current_stream(feats.device).cuda_stream
         nat.check(nat.lib().fjsp_a2c_group_keys(ctypes.c_void_p(f.data_ptr()), T, N, ctypes.c_void_p(keys.data_ptr()),
+                                                None if rows is None else ctypes.c_void_p(rows.data_ptr()),
                                                 ctypes.c_void_p(stream)))
         return keys
     gidx = gather_index(feats.device)
@@ -565,17 +572,21 @@ def group_columns(x, key=None):
     return g if bool((x[:, g.rep[0]] == x).all()) else None
 
 
-def group_verify(feats, ga, gc, x=None, gt=None):
+def group_verify(feats, ga, gc, x=None, gt=None, rows=None):
     """True when no hash collision merged different inputs in the groupings ga (actor inputs,
     RowGroups of group_keys rows 0..7) and gc (global states, row 8) of feats f32 [T, 38, N]:
     every sample's inputs equal those of its group's representative.  On the GPU one pass of the
-    fjsp_a2c_group_verify kernel (bitwise); else x [8, 13, S] / gt [38, S] compared in torch."""
+    fjsp_a2c_group_verify kernel (bitwise) over rows, the sample-major rows group_keys wrote
+    (made here when not given); else x [8, 13, S] / gt [38, S] compared in torch."""
     if feats.is_cuda:
         T, _, n = feats.shape
+        if rows is None:
+            rows = torch.nn.functional.pad(feats.permute(0, 2, 1).reshape(T * n, GLOBAL_DIM),
+                                           (0, GROUP_ROW - GLOBAL_DIM)).contiguous()
         bad = torch.empty(-(-(T * n) // 256), dtype=torch.int32, device=feats.device)
         stream = torch.cuda.current_stream(feats.device).cuda_stream
         V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-        nat.check(nat.lib().fjsp_a2c_group_verify(V(feats), T, n, V(ga.rep), V(gc.rep), V(bad),
+        nat.check(nat.lib().fjsp_a2c_group_verify(V(rows), T, n, V(ga.rep), V(gc.rep), V(bad),
                                                   ctypes.c_void_p(stream)))
         return not bool(bad.any())
     ok = torch.stack([(torch.gather(x, 2, ga.rep[:, None, :].expand_as(x)) == x).all(),
@@ -755,13 +766,15 @@ class A2CLosses:
             ga, gc = groups
         elif dedup:
             f3 = f3.contiguous()
-            gr = RowGroups(group_keys(f3))                          # 8 actor rows + the critic's
+            rows = torch.empty(S, GROUP_ROW, dtype=torch.float32, device=f3.device) if f3.is_cuda else None
+            gr = RowGroups(group_keys(f3, rows))                    # 8 actor rows + the critic's
             ga, gc = gr.rows(0, NA), gr.rows(NA, NA + 1)
             x = gv = None
             if not feats.is_cuda:
                 x, gv = actor_inputs(feats, gidx), f3.permute(1, 0, 2).reshape(GLOBAL_DIM, S)
-            if not group_verify(f3, ga, gc, x, gv):                 # a hash collision: dense
+            if not group_verify(f3, ga, gc, x, gv, rows):           # a hash collision: dense
                 ga = gc = None
+            del rows
 
         # the global states as feature rows [38, S]: one copy of the slab, then row-wise gathers
         # of the groups' representatives (gathering the [T, 38, N] slab's columns directly, 38

@@ -820,7 +820,10 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
 // Keys of the A2C update's grouping of repeated inputs (a2c_vec.row_keys, the same hash): per
 // sample s = t * n + e of feats f32 [T][38][n], key a < 8 over actor a's 13 padded input columns
 // (its OBS_DIMS[a] a2c features, then zeros), key 8 over all 38; k = fmix64(k * MUL + bits(x_c)
-// + c + 1) from k = 0.  One lane per sample, each column a coalesced load.
+// + c + 1) from k = 0.  One lane per sample, each column a coalesced load.  rows (may be null):
+// the sample's 38 features also as a sample-major row [S][GROW] (zero-padded), what the grouping
+// check compares.
+constexpr int GROW = 40;
 constexpr uint64_t GK_MUL = 0x100000001B3ull * 0x9E37ull + 1ull;
 __device__ __forceinline__ uint64_t gk_fmix(uint64_t z) {
     z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
@@ -828,7 +831,7 @@ __device__ __forceinline__ uint64_t gk_fmix(uint64_t z) {
     return z ^ (z >> 31);
 }
 __global__ void __launch_bounds__(256) k_group_keys(const float* __restrict__ feats, int T, int n,
-                                                    uint64_t* __restrict__ keys) {
+                                                    uint64_t* __restrict__ keys, float* __restrict__ rows) {
     const size_t S = (size_t)T * n;
     const size_t s = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (s >= S) return;
@@ -839,9 +842,12 @@ __global__ void __launch_bounds__(256) k_group_keys(const float* __restrict__ fe
     uint64_t ka[NAG];
 #pragma unroll
     for (int a = 0; a < NAG; a++) ka[a] = 0;
+    float xv[GROW];
+#pragma unroll
+    for (int c = 0; c < GROW; c++) xv[c] = c < 38 ? x[(size_t)c * n] : 0.0f;
 #pragma unroll
     for (int c = 0; c < 38; c++) {
-        const uint64_t b = (uint64_t)__float_as_uint(x[(size_t)c * n]);
+        const uint64_t b = (uint64_t)__float_as_uint(xv[c]);
         kc = gk_fmix(kc * GK_MUL + b + (uint64_t)(c + 1));
 #pragma unroll
         for (int a = 0; a < NAG; a++)
@@ -854,6 +860,11 @@ __global__ void __launch_bounds__(256) k_group_keys(const float* __restrict__ fe
         keys[(size_t)a * S + s] = ka[a];
     }
     keys[(size_t)NAG * S + s] = kc;
+    if (rows) {
+        float4* r = reinterpret_cast<float4*>(rows + s * GROW);
+#pragma unroll
+        for (int q = 0; q < GROW / 4; q++) r[q] = make_float4(xv[4 * q], xv[4 * q + 1], xv[4 * q + 2], xv[4 * q + 3]);
+    }
 }
 
 // The actor loss head of the grouped A2C update for one (agent, sample): the reference's
@@ -952,8 +963,10 @@ __global__ void __launch_bounds__(256) k_actor_head(const float* __restrict__ pu
 // of every input with its group's representative): sample s is bad when any of actor a's input
 // columns differs bitwise from those of rep_a[a][s], or any of its 38 global-state columns from
 // those of rep_c[s] (a hash collision merged two different inputs).  Samples that represent
-// their own group are skipped.  bad[block] = 1 if any sample of the workgroup is bad, else 0.
-__global__ void __launch_bounds__(256) k_group_verify(const float* __restrict__ feats, int T, int n,
+// their own group are skipped.  The inputs are read from the sample-major rows k_group_keys
+// wrote (a representative's features are one 160-byte row, not 38 scattered words of the
+// feature-major slab).  bad[block] = 1 if any sample of the workgroup is bad, else 0.
+__global__ void __launch_bounds__(256) k_group_verify(const float* __restrict__ rows, int T, int n,
                                                       const int64_t* __restrict__ rep_a,
                                                       const int64_t* __restrict__ rep_c, int32_t* __restrict__ bad) {
     const size_t S = (size_t)T * n;
@@ -961,28 +974,34 @@ __global__ void __launch_bounds__(256) k_group_verify(const float* __restrict__ 
     int diff = 0;
     if (s < S) {
         constexpr int offs[NAG + 1] = {0, 7, 20, 23, 26, 29, 32, 35, 38};
-        const size_t t = s / (size_t)n, e = s - t * (size_t)n;
-        const uint32_t* x = reinterpret_cast<const uint32_t*>(feats) + t * 38 * (size_t)n + e;
-        uint32_t v[38];
+        const uint4* x = reinterpret_cast<const uint4*>(rows) + s * (GROW / 4);
+        uint4 v[GROW / 4];
 #pragma unroll
-        for (int c = 0; c < 38; c++) v[c] = x[(size_t)c * n];
-        auto col = [&](size_t r) {
-            const size_t tr = r / (size_t)n, er = r - tr * (size_t)n;
-            return reinterpret_cast<const uint32_t*>(feats) + tr * 38 * (size_t)n + er;
-        };
+        for (int q = 0; q < GROW / 4; q++) v[q] = x[q];
+        auto word = [](const uint4& u, int i) { return i == 0 ? u.x : i == 1 ? u.y : i == 2 ? u.z : u.w; };
         const size_t rc = (size_t)rep_c[s];
         if (rc != s) {
-            const uint32_t* y = col(rc);
+            const uint4* y = reinterpret_cast<const uint4*>(rows) + rc * (GROW / 4);
 #pragma unroll
-            for (int c = 0; c < 38; c++) diff |= (int)(y[(size_t)c * n] != v[c]);
+            for (int q = 0; q < GROW / 4; q++) {
+                const uint4 w = y[q];
+                diff |= (int)((w.x ^ v[q].x) | (w.y ^ v[q].y) | (w.z ^ v[q].z) | (w.w ^ v[q].w)) != 0;
+            }
         }
 #pragma unroll
         for (int a = 0; a < NAG; a++) {
             const size_t ra = (size_t)rep_a[(size_t)a * S + s];
             if (ra != s) {
-                const uint32_t* y = col(ra);
+                const uint4* y = reinterpret_cast<const uint4*>(rows) + ra * (GROW / 4);
 #pragma unroll
-                for (int c = offs[a]; c < offs[a + 1]; c++) diff |= (int)(y[(size_t)c * n] != v[c]);
+                for (int q = offs[a] / 4; q <= (offs[a + 1] - 1) / 4; q++) {
+                    const uint4 w = y[q];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int c = 4 * q + i;
+                        if (c >= offs[a] && c < offs[a + 1]) diff |= (int)(word(w, i) != word(v[q], i));
+                    }
+                }
             }
         }
     }
@@ -1127,12 +1146,14 @@ extern "C" int fjsp_a2c_actor_head(const float* pu, int32_t umax, const int64_t*
     return 0;
 }
 
-extern "C" int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uint64_t* keys, void* stream) {
+extern "C" int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uint64_t* keys, float* rows,
+                                   void* stream) {
     if (T <= 0 || n <= 0) return fjsp_internal_fail("fjsp_a2c_group_keys: T and n must be > 0");
     if (!feats || !keys) return fjsp_internal_fail("fjsp_a2c_group_keys: null buffer");
     const size_t S = (size_t)T * (size_t)n;
+    if (rows && ((uintptr_t)rows & 15u)) return fjsp_internal_fail("fjsp_a2c_group_keys: rows must be 16-byte aligned");
     hipLaunchKernelGGL(k_group_keys, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, feats, T, n,
-                       keys);
+                       keys, rows);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));
@@ -1141,12 +1162,13 @@ extern "C" int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uin
     return 0;
 }
 
-extern "C" int fjsp_a2c_group_verify(const float* feats, int32_t T, int32_t n, const int64_t* rep_a,
+extern "C" int fjsp_a2c_group_verify(const float* rows, int32_t T, int32_t n, const int64_t* rep_a,
                                      const int64_t* rep_c, int32_t* bad, void* stream) {
     if (T <= 0 || n <= 0) return fjsp_internal_fail("fjsp_a2c_group_verify: T and n must be > 0");
-    if (!feats || !rep_a || !rep_c || !bad) return fjsp_internal_fail("fjsp_a2c_group_verify: null buffer");
+    if (!rows || !rep_a || !rep_c || !bad) return fjsp_internal_fail("fjsp_a2c_group_verify: null buffer");
+    if ((uintptr_t)rows & 15u) return fjsp_internal_fail("fjsp_a2c_group_verify: rows must be 16-byte aligned");
     const size_t S = (size_t)T * (size_t)n;
-    hipLaunchKernelGGL(k_group_verify, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, feats, T,
+    hipLaunchKernelGGL(k_group_verify, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, rows, T,
                        n, rep_a, rep_c, bad);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
