@@ -293,8 +293,9 @@ int fjsp_a2c_policy_step(fjsp_handle* h, const float* feats, const int8_t* masks
                          int32_t deterministic, uint8_t* actions, float* values, int32_t autoreset,
                          const fjsp_out* out, int32_t env_begin, int32_t env_count, void* hip_stream);
 /* The critic's forward over n samples for the A2C update (a2c.py:692-699 critic(global_states)
- * over the batch; a2c_vec._CriticGrouped): x f32 [38][n] (feature rows, as fjsp_a2c_policy's
- * feats), critic_w packed as for fjsp_a2c_policy -> values f32 [n] and the post-ReLU hidden
+ * over the batch; a2c_vec._CriticGrouped): x f32 [n][40] (ABI 8: sample-major rows, 38
+ * features + 2 ignored words, the layout of fjsp_a2c_group_keys' rows; ABI 7 took [38][n]
+ * feature rows), critic_w packed as for fjsp_a2c_policy -> values f32 [n] and the post-ReLU hidden
  * layers the backward reads, h1 / h2 f32 [n][256], h3 f32 [n][128] (sample-major).  Same
  * arithmetic as fjsp_a2c_policy's values.  Stream-ordered. */
 int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* critic_w, float* h1, float* h2, float* h3,

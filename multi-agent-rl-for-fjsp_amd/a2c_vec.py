@@ -162,12 +162,12 @@ class _CriticGrouped(torch.autograd.Function):
     layers; the backward: the value-head kernel, both 256-wide ReLU layers' input gradients in one
     kernel (fjsp_a2c_critic_backward, the same split arithmetic), split-K weight gradients
     (hipBLASLt; a matrix-core kernel for them measured slower).
-    xT f32 [38, U] -> v [U]."""
+    x f32 [U, 40] (sample-major rows: 38 features, 2 zeros) -> v [U]."""
 
     @staticmethod
-    def forward(ctx, xT, W1, b1, W2, b2, W3, b3, W4, b4):
-        U = xT.shape[1]
-        dev = xT.device
+    def forward(ctx, x, W1, b1, W2, b2, W3, b3, W4, b4):
+        U = x.shape[0]
+        dev = x.device
         cw = pack_critic_weights(W1, b1, W2, b2, W3, b3, W4, b4)
         h1 = torch.empty(U, W2.shape[1], dtype=torch.float32, device=dev)
         h2 = torch.empty(U, W2.shape[0], dtype=torch.float32, device=dev)
@@ -175,13 +175,13 @@ class _CriticGrouped(torch.autograd.Function):
         v = torch.empty(U, dtype=torch.float32, device=dev)
         V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         stream = torch.cuda.current_stream(dev).cuda_stream
-        nat.check(nat.lib().fjsp_a2c_critic_forward(V(xT), U, V(cw), V(h1), V(h2), V(h3), V(v), ctypes.c_void_p(stream)))
-        ctx.save_for_backward(xT, W2, W3, W4, h1, h2, h3)
+        nat.check(nat.lib().fjsp_a2c_critic_forward(V(x), U, V(cw), V(h1), V(h2), V(h3), V(v), ctypes.c_void_p(stream)))
+        ctx.save_for_backward(x, W2, W3, W4, h1, h2, h3)
         return v
 
     @staticmethod
     def backward(ctx, gv):
-        xT, W2, W3, W4, h1, h2, h3 = ctx.saved_tensors
+        x, W2, W3, W4, h1, h2, h3 = ctx.saved_tensors
         B, C = h3.shape
         gvc = gv.reshape(-1).contiguous()
         w4 = W4.reshape(-1).contiguous()
@@ -206,7 +206,7 @@ class _CriticGrouped(torch.autograd.Function):
             g2, gb2 = _relu_bias_grad((g3 @ W3).contiguous(), h2)
             g1, gb1 = _relu_bias_grad((g2 @ W2).contiguous(), h1)
         gW2 = _splitk_wgrad(g2, h1)
-        gW1 = _splitk_wgrad(g1, xT.t())
+        gW1 = _splitk_wgrad(g1, x[:, :GLOBAL_DIM])
         return (None, gW1, gb1, gW2, gb2, gW3, ps[:C], ps[C:2 * C].view(1, C), ps[2 * C:2 * C + 1])
 
 
@@ -217,10 +217,20 @@ critic_fused = os.environ.get("FJSP_CRITIC_FUSED", "1") != "0"
 critic_bwd_fused = os.environ.get("FJSP_CRITIC_BWD", "1") != "0"
 
 
-def critic_grouped(critic, xT):
-    """v [U] of the critic over the columns of xT f32 [38, U] (distinct global states)."""
+def feature_rows(f3):
+    """feats f32 [T, 38, N] -> the sample-major rows f32 [T*N, 40] (zero-padded) that
+    group_keys writes on the GPU (for callers without them)."""
+    T, _, N = f3.shape
+    return torch.nn.functional.pad(f3.permute(0, 2, 1).reshape(T * N, GLOBAL_DIM),
+                                   (0, GROUP_ROW - GLOBAL_DIM)).contiguous()
+
+
+def critic_grouped(critic, x):
+    """v [U] of the critic over the rows of x f32 [U, 40] (distinct global states, sample-major,
+    38 features + 2 zeros: feature_rows / group_keys' rows)."""
     n = critic.net
-    return _CriticGrouped.apply(xT.contiguous(), n[0].weight, n[0].bias, n[2].weight, n[2].bias, n[4].weight,
+    assert x.shape[1] == GROUP_ROW
+    return _CriticGrouped.apply(x.contiguous(), n[0].weight, n[0].bias, n[2].weight, n[2].bias, n[4].weight,
                                 n[4].bias, n[6].weight, n[6].bias)
 
 
@@ -581,8 +591,7 @@ def group_verify(feats, ga, gc, x=None, gt=None, rows=None):
     if feats.is_cuda:
         T, _, n = feats.shape
         if rows is None:
-            rows = torch.nn.functional.pad(feats.permute(0, 2, 1).reshape(T * n, GLOBAL_DIM),
-                                           (0, GROUP_ROW - GLOBAL_DIM)).contiguous()
+            rows = feature_rows(feats)
         bad = torch.empty(-(-(T * n) // 256), dtype=torch.int32, device=feats.device)
         stream = torch.cuda.current_stream(feats.device).cuda_stream
         V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
@@ -762,6 +771,7 @@ class A2CLosses:
         T, _, n = f3.shape
         S = T * n
         ga = gc = None
+        rows = None
         if groups is not None:
             ga, gc = groups
         elif dedup:
@@ -774,22 +784,34 @@ class A2CLosses:
                 x, gv = actor_inputs(feats, gidx), f3.permute(1, 0, 2).reshape(GLOBAL_DIM, S)
             if not group_verify(f3, ga, gc, x, gv, rows):           # a hash collision: dense
                 ga = gc = None
-            del rows
 
-        # the global states as feature rows [38, S]: one copy of the slab, then row-wise gathers
-        # of the groups' representatives (gathering the [T, 38, N] slab's columns directly, 38
-        # strided loads per column plus a transpose, measured slower: profiles/r04/a2c/)
-        gt = f3.permute(1, 0, 2).reshape(GLOBAL_DIM, S)
+        if ga is not None and feats.is_cuda:
+            # the groups' representatives gathered as whole sample-major rows (160 B each) of the
+            # keys pass's rows: no [38, S] copy of the slab, no 38 scattered words per column
+            if rows is None:
+                rows = feature_rows(f3)
 
-        def cols(agents, idx):                                       # [k, 13, u] from gt
-            k, u = idx.shape
-            c = gt[:, idx.reshape(-1)].view(GLOBAL_DIM, k, u)
-            c = torch.cat([c, c.new_zeros(1, k, u)])
-            return c[gidx[agents], torch.arange(k, device=idx.device)[:, None], :]
+            def cols(agents, idx):                                   # [k, 13, u]
+                k, u = idx.shape
+                r = rows.index_select(0, idx.reshape(-1)).view(k, u, GROUP_ROW)
+                return torch.gather(r, 2, gidx[agents][:, None, :].expand(k, u, gidx.shape[1])).transpose(1, 2)
+        else:
+            # the global states as feature rows [38, S]: one copy of the slab, then row-wise
+            # gathers of the groups' representatives
+            gt = f3.permute(1, 0, 2).reshape(GLOBAL_DIM, S)
+
+            def cols(agents, idx):                                   # [k, 13, u] from gt
+                k, u = idx.shape
+                c = gt[:, idx.reshape(-1)].view(GLOBAL_DIM, k, u)
+                c = torch.cat([c, c.new_zeros(1, k, u)])
+                return c[gidx[agents], torch.arange(k, device=idx.device)[:, None], :]
         # the critic first: its GEMMs keep the GPU busy while the host issues the actors' many
         # small launches (after the grouping's host synchronisations the queue is empty)
         if gc is not None and feats.is_cuda and gc.first.shape[1] >= 65536 and critic_fused:
-            vu = critic_grouped(critic, gt[:, gc.first[0]]).reshape(1, 1, -1)
+            vu = critic_grouped(critic, rows.index_select(0, gc.first[0])).reshape(1, 1, -1)
+            v = gc.gather(vu).reshape(-1)                            # [S]
+        elif gc is not None and feats.is_cuda:
+            vu = mlp_forward(critic.net, rows.index_select(0, gc.first[0])[:, :GLOBAL_DIM]).reshape(1, 1, -1)
             v = gc.gather(vu).reshape(-1)                            # [S]
         elif gc is not None:
             vu = mlp_forward(critic.net, gt[:, gc.first[0]].t()).reshape(1, 1, -1)

@@ -269,23 +269,35 @@ __device__ __forceinline__ void logit_partials(const f32x16 acc[2], const Row16&
 
 // The tile's inputs: din feature rows from row off of the [38][n] slab, zero-padded to DPAD, for
 // the tile's T envs -> registers (issued first: they overlap the mask check) -> the bf16 planes
-// [NP][T][DPAD + 8].
+// [NP][T][DPAD + 8].  ROWS: the inputs are sample-major rows [n][GROW] instead (the update's
+// distinct global states, gathered from k_group_keys' rows), read along each row.
 constexpr int XI = cmax(C_DPAD * TC, A_DPAD * TA) / NTHR;
-template <int T, int DPAD>
+constexpr int GROW = 40;   // floats per sample-major feature row (38 + 2 zeros)
+template <int T, int DPAD, bool ROWS>
+__device__ __forceinline__ void input_kc(int i, int& k, int& c) {
+    k = ROWS ? i % DPAD : i / T;
+    c = ROWS ? i / DPAD : i % T;
+}
+template <int T, int DPAD, bool ROWS = false>
 __device__ __forceinline__ void inputs_load(const float* __restrict__ feats, int n, int e0, int off, int din, int tid,
                                             float v[XI]) {
 #pragma unroll
     for (int q = 0; q < XI; q++) {
-        const int i = tid + q * NTHR, k = i / T, c = i % T;
-        v[q] = (i < DPAD * T && k < din && e0 + c < n) ? feats[(size_t)(off + k) * n + e0 + c] : 0.0f;
+        int k, c;
+        const int i = tid + q * NTHR;
+        input_kc<T, DPAD, ROWS>(i, k, c);
+        const size_t at = ROWS ? (size_t)(e0 + c) * GROW + off + k : (size_t)(off + k) * n + e0 + c;
+        v[q] = (i < DPAD * T && k < din && e0 + c < n) ? feats[at] : 0.0f;
     }
 }
-template <int T, int DPAD>
+template <int T, int DPAD, bool ROWS = false>
 __device__ __forceinline__ void inputs_store(const float v[XI], int tid, __bf16* s_x) {
     constexpr int S = DPAD + 8, PL = T * S;
 #pragma unroll
     for (int q = 0; q < XI; q++) {
-        const int i = tid + q * NTHR, k = i / T, c = i % T;
+        int k, c;
+        const int i = tid + q * NTHR;
+        input_kc<T, DPAD, ROWS>(i, k, c);
         if (i < DPAD * T) {
             __bf16 x0, x1, x2;
             split3(v[q], x0, x1, x2);
@@ -321,7 +333,7 @@ struct CriticSave {
     float* h2;
     float* h3;
 };
-template <bool SAVE>
+template <bool SAVE, bool ROWS = false>
 __device__ __forceinline__ void critic_tile(const PolicyArgs& A, int tile, unsigned char* s_mem, int tid, int lane,
                                             int wave, const CriticSave& sv) {
     __bf16* s_x = reinterpret_cast<__bf16*>(s_mem);              // inputs [NP][TC][XSC]
@@ -338,11 +350,11 @@ __device__ __forceinline__ void critic_tile(const PolicyArgs& A, int tile, unsig
     const float* W4 = B3 + 128;                                       // [128]
     const float* B4 = W4 + 128;                                       // [1]
     float xv[XI];
-    inputs_load<TC, C_DPAD>(A.feats, n, e0, 0, 38, tid, xv);
+    inputs_load<TC, C_DPAD, ROWS>(A.feats, n, e0, 0, 38, tid, xv);
     WRing<C_DPAD / 16> r1;
     wring_start(r1, wblocks<C_DPAD / 16, C_DPAD / 16>(W1, wave, 0, lane));
     const Row16 b1 = load_rows(B1, 32 * wave, lane);
-    inputs_store<TC, C_DPAD>(xv, tid, s_x);
+    inputs_store<TC, C_DPAD, ROWS>(xv, tid, s_x);
     __syncthreads();
     PST(3, __builtin_amdgcn_s_memtime());
     f32x16 a[1];
@@ -677,13 +689,14 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
     tile_step(A, St, tile, s_mem, s_state, lane);
 }
 
-// The critic's forward over n samples for the A2C update (values + the saved hidden layers).
+// The critic's forward over n samples for the A2C update (values + the saved hidden layers), on
+// sample-major input rows [n][GROW].
 __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)))
 k_critic_fwd(PolicyArgs A, CriticSave sv) {
     __shared__ __attribute__((aligned(16))) unsigned char s_mem[LDS_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    critic_tile<true>(A, (int)blockIdx.x, s_mem, tid, lane, wave, sv);
+    critic_tile<true, true>(A, (int)blockIdx.x, s_mem, tid, lane, wave, sv);
 }
 
 // The critic's backward through layers 3 and 2 for the A2C update (a2c_vec._CriticGrouped): on a
@@ -822,8 +835,7 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
 // (its OBS_DIMS[a] a2c features, then zeros), key 8 over all 38; k = fmix64(k * MUL + bits(x_c)
 // + c + 1) from k = 0.  One lane per sample, each column a coalesced load.  rows (may be null):
 // the sample's 38 features also as a sample-major row [S][GROW] (zero-padded), what the grouping
-// check compares.
-constexpr int GROW = 40;
+// check compares and the update's critic reads.
 constexpr uint64_t GK_MUL = 0x100000001B3ull * 0x9E37ull + 1ull;
 __device__ __forceinline__ uint64_t gk_fmix(uint64_t z) {
     z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
@@ -1225,6 +1237,7 @@ extern "C" int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* c
                                        float* h3, float* values, void* stream) {
     if (n <= 0) return fjsp_internal_fail("fjsp_a2c_critic_forward: n must be > 0");
     if (!x || !critic_w || !h1 || !h2 || !h3 || !values) return fjsp_internal_fail("fjsp_a2c_critic_forward: null buffer");
+    if ((uintptr_t)x & 15u) return fjsp_internal_fail("fjsp_a2c_critic_forward: x must be 16-byte aligned");
     PolicyArgs A{x, nullptr, n, nullptr, critic_w, nullptr, 0u, 0u, 0, nullptr, values, nullptr, (n + TC - 1) / TC, 0};
     hipLaunchKernelGGL(k_critic_fwd, dim3((unsigned)A.nc), dim3(NTHR), 0, (hipStream_t)stream, A, CriticSave{h1, h2, h3});
     const hipError_t err = hipGetLastError();

@@ -23,7 +23,8 @@ cw = A.pack_critic_weights(*[m for i in (0, 2, 4, 6) for m in (n[i].weight, n[i]
 h = [torch.empty(U, c, device="cuda") for c in (256, 256, 128)]
 v = torch.empty(U, device="cuda")
 V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-nat.check(nat.lib().fjsp_a2c_critic_forward(V(xT), U, V(cw), V(h[0]), V(h[1]), V(h[2]), V(v),
+xr = torch.nn.functional.pad(xT.t(), (0, 2)).contiguous()   # ABI 8: sample-major rows [U][40]
+nat.check(nat.lib().fjsp_a2c_critic_forward(V(xr), U, V(cw), V(h[0]), V(h[1]), V(h[2]), V(v),
                                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
 torch.cuda.synchronize()
 c64 = copy.deepcopy(critic).double()

@@ -507,7 +507,8 @@ def test_fused_critic_forward_backward_matches_torch(M):
     (v64 * w.double()).sum().backward()
     g64 = [p.grad for p in c64.parameters()]
     res = {}
-    for name, fwd in (("fused", lambda: A.critic_grouped(critic, xT)),
+    xr = torch.nn.functional.pad(xT.t(), (0, 2)).contiguous()   # the kernel's sample-major rows
+    for name, fwd in (("fused", lambda: A.critic_grouped(critic, xr)),
                       ("torch", lambda: A.mlp_forward(critic.net, xT.t()).reshape(-1))):
         critic.zero_grad(set_to_none=True)
         v = fwd()
