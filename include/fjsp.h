@@ -325,6 +325,33 @@ int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uint64_t* keys
  * Stream-ordered. */
 int fjsp_a2c_group_verify(const float* rows, int32_t T, int32_t n, const int64_t* rep_a, const int64_t* rep_c,
                           int32_t* bad, void* stream);
+/* The grouping itself (ABI 8; a2c_vec.RowGroups on the GPU): keys uint64 [R][S] (R <= 16,
+ * R * S < 2^31, fjsp_a2c_group_keys' rows) -> per row the distinct keys as groups, numbered in
+ * sorted key order, the samples sorted by group with equal keys in sample order (stable), each
+ * group's first sample and run end.  fjsp_a2c_group_sort: one radix sort of every row's 59 key
+ * bits with the row id above them (flat / sorted uint64 [R * S], pos / spos uint32 [R * S]), the
+ * run starts (runs uint32 [R * S]) and their inclusive scan (scan), and the group count of each
+ * row, counts int64 [R]; temp: fjsp_a2c_group_temp_bytes(R * S) bytes.  After the caller has read
+ * counts and chosen umax >= every count, fjsp_a2c_group_runs: starts (scratch) / first / ends int64
+ * [R][umax] (padding groups: start and end S, first = the row's last sorted sample), perm int64
+ * [R][S] (sample of each sorted position), inv int64 [R][S] (group of each sample), rep int64
+ * [R][S] (first sample of each sample's group).  Stream-ordered. */
+int fjsp_a2c_group_temp_bytes(int64_t count, uint64_t* bytes);
+int fjsp_a2c_group_sort(const uint64_t* keys, int32_t R, int64_t S, void* temp, uint64_t temp_bytes, uint64_t* flat,
+                        uint64_t* sorted, uint32_t* pos, uint32_t* spos, uint32_t* runs, uint32_t* scan, int64_t* counts,
+                        void* stream);
+int fjsp_a2c_group_runs(const uint32_t* spos, const uint32_t* scan, int32_t R, int64_t S, int64_t umax, int64_t* starts,
+                        int64_t* perm, int64_t* inv, int64_t* rep, int64_t* first, int64_t* ends, int32_t* gsorted,
+                        void* stream);
+/* (gsorted int32 [R][S]: the group of each sorted position.)  The backward of a per-group gather
+ * over that grouping (a2c.py:692-699: the gradient of every sample's network output summed into
+ * its distinct input): out f32 [J][umax] = per group g of row rowmap[j], the sum in f64 over its
+ * samples in sorted order of vals[j][sample] (* scale[j] in f32 first; scale may be NULL).  temp:
+ * fjsp_a2c_run_sums_bytes(J, S) bytes.  Deterministic.  Stream-ordered. */
+int fjsp_a2c_run_sums_bytes(int32_t J, int64_t S, uint64_t* bytes);
+int fjsp_a2c_run_sums(const float* vals, int32_t J, const int32_t* rowmap, const float* scale, const int64_t* perm,
+                      const int32_t* gsorted, int64_t S, int64_t umax, void* temp, uint64_t temp_bytes, float* out,
+                      void* stream);
 /* The actor loss head of the grouped update (a2c.py:204-220 masked probabilities, :705-731
  * entropy and calc_actor_loss): pu f32 [8][8][umax] = each agent's action probabilities per
  * distinct input, inv int64 [8][T * n] = each sample's distinct input, masks int8 [T][29][n],

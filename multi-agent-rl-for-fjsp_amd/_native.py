@@ -13,7 +13,7 @@ REPO = os.path.dirname(HERE)
 # FJSP_LIB selects a diagnostic build (e.g. libfjsp_stamps.so); default: the product library
 LIB_PATH = os.environ.get("FJSP_LIB") or os.path.join(HERE, "libfjsp.so")
 SRC = os.path.join(HERE, "csrc", "fjsp_hip.hip")
-SRCS = [SRC, os.path.join(HERE, "csrc", "fjsp_policy.hip")]
+SRCS = [SRC, os.path.join(HERE, "csrc", "fjsp_policy.hip"), os.path.join(HERE, "csrc", "fjsp_group.hip")]
 HEADERS = [os.path.join(HERE, "csrc", h) for h in ("fjsp_env.h", "fjsp_stepdev.h", "fjsp_stamps.h")] + [
     os.path.join(REPO, "include", "fjsp.h")]
 
@@ -68,7 +68,8 @@ EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_c
            "fjsp_a2c_group_keys", "fjsp_a2c_group_verify", "fjsp_a2c_actor_head",
            "fjsp_a2c_relu_bias_grad", "fjsp_a2c_value_head_grad", "fjsp_faults", "fjsp_a2c_critic_forward",
            "fjsp_a2c_critic_backward", "fjsp_gae_shared",
-           "fjsp_a2c_policy_step"]
+           "fjsp_a2c_policy_step", "fjsp_a2c_group_temp_bytes", "fjsp_a2c_group_sort", "fjsp_a2c_group_runs",
+           "fjsp_a2c_run_sums_bytes", "fjsp_a2c_run_sums"]
 POLICY_ACTOR_DPAD, POLICY_CRITIC_DPAD = 16, 48
 POLICY_ACTOR_FLOATS = 3 * 256 * 16 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 8 * 256 + 16
 POLICY_CRITIC_FLOATS = 3 * 256 * 48 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 3 * 128 * 256 // 2 + 128 + 128 + 16
@@ -148,6 +149,11 @@ def lib():
         "fjsp_a2c_critic_backward": (I, [P, P, P, I, P, P, P, P, P, P, P]),
         "fjsp_gae_shared": (I, [P, P, P, I, I, I, D, D, P, P, P]),
         "fjsp_a2c_policy_step": (I, [P, P, P, P, P, P, U32, U32, I, P, P, I, ctypes.POINTER(fjsp_out), I, I, P]),
+        "fjsp_a2c_group_temp_bytes": (I, [ctypes.c_int64, ctypes.POINTER(U64)]),
+        "fjsp_a2c_group_sort": (I, [P, I, ctypes.c_int64, P, U64, P, P, P, P, P, P, P, P]),
+        "fjsp_a2c_group_runs": (I, [P, P, I, ctypes.c_int64, ctypes.c_int64, P, P, P, P, P, P, P, P]),
+        "fjsp_a2c_run_sums_bytes": (I, [I, ctypes.c_int64, ctypes.POINTER(U64)]),
+        "fjsp_a2c_run_sums": (I, [P, I, P, P, P, P, ctypes.c_int64, ctypes.c_int64, P, U64, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -538,6 +538,9 @@ class RowGroups:
         R, S = keys.shape
         assert R <= 16, "the row id lives in bits 59..62 of the sort key"
         dev = keys.device
+        if keys.is_cuda and R * S < 2 ** 31:
+            self._init_device(keys)
+            return
         # one flat sort for all rows: the row in bits 59..62 above 59 bits of the key (the
         # grouping is verified by the caller, so a shorter key only risks a dense fallback)
         flat = (keys & ((1 << 59) - 1)) | (torch.arange(R, device=dev, dtype=torch.int64)[:, None] << 59)
@@ -558,6 +561,38 @@ class RowGroups:
         self.inv = torch.empty_like(perm).scatter_(1, perm, seg)
         self.rep = torch.gather(self.first, 1, self.inv)
         self.perm = perm
+        self.gsorted = None   # the run sums' kernel input (device path only)
+
+    def _init_device(self, keys):
+        """The same grouping by the library's kernels (fjsp_a2c_group_sort / _runs: one radix sort
+        with 32-bit sample positions, one scan, one scatter pass; the torch path below does a 64-bit
+        payload sort, a blocked prefix sum, a binary search per group and three gathers)."""
+        R, S = keys.shape
+        RS = R * S
+        dev = keys.device
+        L = nat.lib()
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        E = lambda n, dt: torch.empty(n, dtype=dt, device=dev)  # noqa: E731
+        k = keys.contiguous()
+        tb = ctypes.c_uint64()
+        nat.check(L.fjsp_a2c_group_temp_bytes(RS, ctypes.byref(tb)))
+        temp = E(max(1, tb.value), torch.uint8)
+        flat, srt = E(RS, torch.int64), E(RS, torch.int64)
+        pos, spos, runs, scan = (E(RS, torch.int32) for _ in range(4))
+        counts = E(R, torch.int64)
+        nat.check(L.fjsp_a2c_group_sort(V(k), R, S, V(temp), tb.value, V(flat), V(srt), V(pos), V(spos), V(runs),
+                                        V(scan), V(counts), st))
+        del temp, flat, srt, pos, runs
+        self.U = counts.tolist()                                  # the one host sync
+        umax = bucket(max(self.U))
+        starts, first, ends = (E((R, umax), torch.int64) for _ in range(3))
+        perm, inv, rep = (E((R, S), torch.int64) for _ in range(3))
+        gsorted = E((R, S), torch.int32)
+        nat.check(L.fjsp_a2c_group_runs(V(spos), V(scan), R, S, umax, V(starts), V(perm), V(inv), V(rep), V(first),
+                                        V(ends), V(gsorted), st))
+        self.first, self.ends, self.inv, self.rep, self.perm = first, ends, inv, rep, perm
+        self.gsorted = gsorted
 
     def rows(self, lo, hi):
         """The groupings of rows lo..hi-1 alone (views; Umax = their own largest count)."""
@@ -567,6 +602,7 @@ class RowGroups:
         g.first, g.ends = self.first[lo:hi, :um], self.ends[lo:hi, :um]
         g.inv, g.perm = self.inv[lo:hi], self.perm[lo:hi]
         g.rep = None if self.rep is None else self.rep[lo:hi]
+        g.gsorted = None if self.gsorted is None else self.gsorted[lo:hi]
         return g
 
     def gather(self, y):
@@ -626,8 +662,12 @@ class _GatherRuns(torch.autograd.Function):
 
 def _run_sums(g, gy):
     """gy [R, C, S] per sample -> [R, C, Umax] per group of the RowGroups g: runs of the sorted
-    order summed (an f64 prefix sum differenced at the run ends)."""
+    order summed (on the GPU: fjsp_a2c_run_sums, f64 sums in sorted order; else an f64 prefix sum
+    differenced at the run ends)."""
     R, C, S = gy.shape
+    if g.gsorted is not None:
+        rowmap = _index_tensor(tuple(r for r in range(R) for _ in range(C)), gy.device).int()
+        return run_sums(gy.reshape(R * C, S), rowmap, None, g).view(R, C, -1)
     ce = _prefix_at(torch.gather(gy, 2, g.perm[:, None, :].expand(R, C, S)),
                     (g.ends - 1)[:, None, :].expand(R, C, g.ends.shape[1]))
     return torch.cat([ce[..., :1], ce[..., 1:] - ce[..., :-1]], dim=-1).to(gy.dtype)
@@ -665,6 +705,12 @@ class _ActorHead(torch.autograd.Function):
         g = ctx.g
         S = grad.shape[1]
         umax = g.ends.shape[1]
+        if g.gsorted is not None:   # the device grouping: one run-sum pass (fjsp_a2c_run_sums)
+            row_agent = _index_tensor(tuple(a for a in range(NA) for _ in range(N_ACTIONS[a])), grad.device)
+            rs = run_sums(grad, row_agent, gl.to(grad.dtype)[row_agent], g)              # [29, Umax]
+            out = torch.zeros(NA * 8, umax, dtype=grad.dtype, device=grad.device)
+            out[_valid_rows(grad.device)] = rs
+            return out.view(NA, 8, umax), None, None, None, None, None, None, None, None
         # each agent's rows in its sorted sample order, scaled by the agent's loss gradient
         srt = torch.empty_like(grad)
         for a in range(NA):
@@ -708,6 +754,26 @@ def _valid_rows(device):
         _VALID_ROWS[device] = torch.tensor([a * 8 + j for a in range(NA) for j in range(N_ACTIONS[a])],
                                            device=device)
     return _VALID_ROWS[device]
+
+
+def run_sums(vals, rowmap, scale, g):
+    """out [J, Umax] f32: per group of row rowmap[j] of the (device) RowGroups g, the f64 sum in
+    sorted order of vals[j] (* scale[j]) over the group's samples (fjsp_a2c_run_sums)."""
+    J, S = vals.shape
+    umax = g.first.shape[1]
+    dev = vals.device
+    v = vals.contiguous()
+    rm = rowmap.to(torch.int32).contiguous()
+    sc = None if scale is None else scale.to(torch.float32).contiguous()
+    tb = ctypes.c_uint64()
+    nat.check(nat.lib().fjsp_a2c_run_sums_bytes(J, S, ctypes.byref(tb)))
+    temp = torch.empty(tb.value, dtype=torch.uint8, device=dev)
+    out = torch.empty(J, umax, dtype=torch.float32, device=dev)
+    perm, gs = g.perm.contiguous(), g.gsorted.contiguous()
+    V = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    nat.check(nat.lib().fjsp_a2c_run_sums(V(v), J, V(rm), V(sc), V(perm), V(gs), S, umax, V(temp), tb.value, V(out),
+                                          ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    return out
 
 
 def _prefix_at(w, idx, block=1024):

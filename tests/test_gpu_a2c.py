@@ -530,3 +530,81 @@ def test_prefix_at_equals_full_prefix_sum_on_gpu(M):
         w = torch.randn(29, S, device="cuda")
         idx = torch.sort(torch.randint(0, S, (29, 4000), device="cuda"), -1).values
         assert torch.equal(torch.gather(A._prefix_sum(w.double()), -1, idx), A._prefix_at(w, idx))
+
+
+def test_row_groups_kernels_equal_stable_sort(M):
+    """RowGroups on the GPU (fjsp_a2c_group_sort / _runs) equals the grouping by a stable sort of
+    each row's 59 key bits computed here in numpy: group counts, the sorted order (equal keys in
+    sample order), each sample's group and representative, each group's first sample and run end
+    (padding groups: end S, first = the row's last sorted sample)."""
+    import numpy as np
+    A = M["A"]
+    R, S = 9, 50001
+    g = torch.Generator().manual_seed(7)
+    card = [3, 28, 1225, 40000, 1, 7, 2, 50001, 600]
+    base = torch.stack([torch.randint(0, c, (S,), generator=g) for c in card])
+    keys = base * -7046029254386353131 + torch.arange(R)[:, None] * 977   # int64 wrap: keys over all 64 bits
+    G = A.RowGroups(keys.cuda())
+    k = keys.numpy()
+    rows = np.arange(R, dtype=np.int64)[:, None]
+    flat = (k & ((1 << 59) - 1)) | (rows << 59)
+    order = np.argsort(flat.reshape(-1), kind="stable")
+    sk = flat.reshape(-1)[order].reshape(R, S)
+    perm = order.reshape(R, S) - rows * S
+    new = np.ones((R, S), dtype=bool)
+    new[:, 1:] = sk[:, 1:] != sk[:, :-1]
+    seg = np.cumsum(new, axis=1) - 1
+    U = (seg[:, -1] + 1).tolist()
+    assert G.U == U
+    umax = G.first.shape[1]
+    assert umax == A.bucket(max(U))
+    starts = np.full((R, umax), S, dtype=np.int64)
+    for r in range(R):
+        j = np.nonzero(new[r])[0]
+        starts[r, seg[r, j]] = j
+    first = perm[rows, np.minimum(starts, S - 1)]
+    ends = np.concatenate([starts[:, 1:], np.full((R, 1), S)], axis=1)
+    inv = np.empty((R, S), dtype=np.int64)
+    inv[rows, perm] = seg
+    rep = first[rows, inv]
+    for name, want in (("perm", perm), ("inv", inv), ("rep", rep), ("first", first), ("ends", ends)):
+        assert np.array_equal(getattr(G, name).cpu().numpy(), want), name
+
+
+@pytest.mark.parametrize("S", [1, 1023, 50001, 300000])
+def test_run_sums_kernel_equals_float64_group_sums(M, S):
+    """fjsp_a2c_run_sums (the per-group gradient sums of the grouped update, one pass over the
+    sorted runs) against float64 group sums of the same f32 products: groups of one sample,
+    groups spanning many 1 024-position chunks, a row that is one group, scaled rows; within one
+    f32 rounding of the f64 sum (+ f64 summation error).  The _GatherRuns backward (_run_sums)
+    takes the same kernel."""
+    A = M["A"]
+    R = 5
+    g = torch.Generator().manual_seed(S)
+    card = [1, 3, 977, max(1, S // 2), S]
+    base = torch.stack([torch.randint(0, c, (S,), generator=g) for c in card])
+    G = A.RowGroups((base * -7046029254386353131 + torch.arange(R)[:, None]).cuda())
+    assert G.gsorted is not None
+    J = 9
+    rowmap = torch.tensor([0, 1, 2, 3, 4, 4, 3, 1, 2], dtype=torch.int32)
+    vals = torch.randn(J, S, generator=g) * torch.logspace(-3, 3, J)[:, None]
+    scale = torch.rand(J, generator=g) + 0.5
+    got = A.run_sums(vals.cuda(), rowmap.cuda(), scale.cuda(), G).cpu().double()
+    umax = G.first.shape[1]
+    assert got.shape == (J, umax)
+    inv = G.inv.cpu()
+    x = (vals * scale[:, None]).double()
+    want = torch.zeros(J, umax, dtype=torch.float64)
+    mag = torch.zeros(J, umax, dtype=torch.float64)
+    for j in range(J):
+        want[j].index_add_(0, inv[int(rowmap[j])], x[j])
+        mag[j].index_add_(0, inv[int(rowmap[j])], x[j].abs())
+    tol = torch.finfo(torch.float32).eps * want.abs() + 1e-12 * mag + 1e-300
+    assert bool(((got - want).abs() <= tol).all()), float(((got - want).abs() / (want.abs() + 1e-30)).max())
+    gy = vals[:3].reshape(1, 3, S).expand(R, 3, S).contiguous().cuda()
+    a = A._run_sums(G, gy).cpu().double()
+    for r in range(R):
+        for c in range(3):
+            w = torch.zeros(umax, dtype=torch.float64).index_add_(0, inv[r], vals[c].double())
+            m = torch.zeros(umax, dtype=torch.float64).index_add_(0, inv[r], vals[c].double().abs())
+            assert bool(((a[r, c] - w).abs() <= torch.finfo(torch.float32).eps * w.abs() + 1e-12 * m + 1e-300).all())
