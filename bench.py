@@ -314,6 +314,11 @@ def main():
             dist.destroy_process_group()
         return
     env.reset(seeds=torch.arange(base, base + N), num_orders=args.num_orders)
+    # the bench times its launches with its own events: the library's per-launch hipEvents
+    # (fjsp_last_kernel_ms) would add two more event packets between launches (0.7 % of wall time
+    # per 1 024-step launch, profiles/r04/ab_launch_gaps_lib_timing.json)
+    nat = importlib.import_module("multi-agent-rl-for-fjsp_amd._native")
+    nat.check(nat.lib().fjsp_set_option(env.handle, b"timing", 0))
     B = args.batch_steps                      # env-steps of every env per bench step
     chunk = max(1, min(args.chunk, args.steps * B))
     buf = vec_env.Buffers(chunk, N, dev, infos=False)
