@@ -96,123 +96,143 @@ __global__ void __launch_bounds__(256) k_group_rep(const int64_t* __restrict__ i
 
 // Run sums: out[j][g] = sum over the sorted positions of group g of row a = rowmap[j] of
 // vals[j][perm[a][pos]] (* scale[j], in f32, as the gradient is scaled before the sum), summed in
-// f64 in sorted order, stored as f32.  The backward of a per-group gather (each group's samples'
-// gradients summed: a2c_vec._GatherRuns, _ActorHead): deterministic, one pass.  Each workgroup
-// takes RS_CH sorted positions of one row: per thread 4 positions reduced by runs (a run wholly
-// inside them is final), then each run start walks the following threads' head partials; a run
-// that crosses the chunk's ends leaves its partial sums to k_run_carry, which adds them chunk by
-// chunk from the chunk where the run starts.
+// f64, stored as f32.  The backward of a per-group gather (each group's samples' gradients
+// summed: a2c_vec._GatherRuns, _ActorHead): deterministic, one pass over the values.
+// k_run_chunks: a workgroup takes RS_CH sorted positions of one row, forms their f64 prefix sums
+// (per thread 4, then a block scan of the thread totals in a fixed order), and each run of one
+// group inside the chunk is the difference of the prefixes at its two ends (the group ids of a
+// row's sorted positions rise by one per run, so run k of the chunk is group g0 + k).  A run that
+// crosses a chunk end leaves its chunk part (cont / first_part, last_part / last_g); k_run_carry
+// adds those over chunks with the same construction one level up (prefix sums and a prefix max
+// of the run-start chunks, one workgroup per row).
 constexpr int RS_CH = 1024, RS_T = 256;
+
+// inclusive scan of v over the RS_T threads of a workgroup (Kogge-Stone, fixed order); sc: LDS
+template <class T, class Op>
+__device__ __forceinline__ T block_scan(T v, T* sc, Op op) {
+    const int t = (int)threadIdx.x;
+    sc[t] = v;
+    __syncthreads();
+#pragma unroll
+    for (int d = 1; d < RS_T; d <<= 1) {
+        const T o = t >= d ? sc[t - d] : v;
+        __syncthreads();
+        if (t >= d) v = op(o, v);
+        sc[t] = v;
+        __syncthreads();
+    }
+    return v;
+}
+
 __global__ void __launch_bounds__(RS_T) k_run_chunks(const float* __restrict__ vals, const int32_t* __restrict__ rowmap,
                                                    const float* __restrict__ scale, const int64_t* __restrict__ perm,
                                                    const int32_t* __restrict__ gsorted, int64_t S, int64_t umax,
                                                    int64_t nch, float* __restrict__ out, double* __restrict__ first_part,
-                                                   uint8_t* __restrict__ whole, double* __restrict__ last_part,
+                                                   uint8_t* __restrict__ cont, double* __restrict__ last_part,
                                                    int32_t* __restrict__ last_g) {
-    __shared__ int32_t s_hg[RS_T], s_tg[RS_T];
-    __shared__ double s_hs[RS_T], s_ts[RS_T];
-    __shared__ uint8_t s_single[RS_T];
+    __shared__ double s_sc[RS_T];
+    __shared__ double s_lo[RS_CH], s_hi[RS_CH];   // per run k: the prefix before its first / at its last position
     const int64_t c = blockIdx.x;
     const int j = (int)blockIdx.y, t = (int)threadIdx.x;
     const int64_t a = rowmap[j];
     const float sc = scale ? scale[j] : 1.0f;
-    const int64_t pos0 = c * RS_CH;
+    const int64_t pos0 = c * RS_CH, pend = pos0 + RS_CH < S ? pos0 + RS_CH : S;   // [pos0, pend)
     const int32_t* gs = gsorted + a * S;
     const int64_t* pm = perm + a * S;
     const float* vr = vals + (int64_t)j * S;
     int32_t g[4];
-    double v[4];
+    double pre[4];
+    double acc = 0.0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int64_t p = pos0 + 4 * t + i;
-        g[i] = p < S ? gs[p] : -1;
-        v[i] = p < S ? (double)(vr[pm[p]] * sc) : 0.0;
+        g[i] = p < pend ? gs[p] : -1;
+        acc += p < pend ? (double)(vr[pm[p]] * sc) : 0.0;
+        pre[i] = acc;
     }
-    // runs of this thread's 4 positions: interior runs are final, head and tail go to LDS
-    int32_t hg = g[0], tg = g[0];
-    double hs = v[0], ts = v[0];
-    bool single = true;
+    const double incl = block_scan(acc, s_sc, [](double x, double y) { return x + y; });
+    const double off = incl - acc;   // the prefix before this thread's positions
+    const int32_t g0 = gs[pos0];
 #pragma unroll
-    for (int i = 1; i < 4; i++) {
-        if (g[i] == tg) {
-            ts += v[i];
-        } else {
-            if (single) {
-                hs = ts;
-                single = false;
-            } else if (tg >= 0) {
-                out[(int64_t)j * umax + tg] = (float)ts;   // an interior run: all of its positions are here
-            }
-            tg = g[i];
-            ts = v[i];
-        }
+    for (int i = 0; i < 4; i++) {
+        const int64_t p = pos0 + 4 * t + i;
+        if (p >= pend) break;
+        const int k = g[i] - g0;
+        if (p == pos0 || gs[p - 1] != g[i]) s_lo[k] = i == 0 ? off : off + pre[i - 1];
+        if (p + 1 == pend || gs[p + 1] != g[i]) s_hi[k] = off + pre[i];
     }
-    if (single) hs = ts;
-    s_hg[t] = hg;
-    s_hs[t] = hs;
-    s_tg[t] = tg;
-    s_ts[t] = ts;
-    s_single[t] = single ? 1 : 0;
     __syncthreads();
+    const int32_t glast = gs[pend - 1];
+    const int m = glast - g0 + 1;
     const int32_t prev_g = pos0 > 0 ? gs[pos0 - 1] : -2;
-    const int32_t next_g = pos0 + RS_CH < S ? gs[pos0 + RS_CH] : -2;
-    // a run starting at (thread t0's head or tail) with group gg and partial s: walk forward
-    auto finish = [&](int t0, int32_t gg, double s, bool at_chunk_start) {
-        int u = t0;
-        bool cont = true;
-        while (cont && u + 1 < RS_T && s_hg[u + 1] == gg) {
-            u++;
-            s += s_hs[u];
-            cont = s_single[u] != 0;
-        }
-        const bool to_end = cont && u + 1 == RS_T;
-        const bool from_prev = at_chunk_start && prev_g == gg;
-        const bool into_next = to_end && next_g == gg;
-        const int64_t k = (int64_t)j * nch + c;
+    const int32_t next_g = pend < S ? gs[pend] : -2;
+    const int64_t jc = (int64_t)j * nch + c;
+    for (int k = t; k < m; k += RS_T) {
+        const double sum = s_hi[k] - s_lo[k];
+        const bool from_prev = k == 0 && prev_g == g0, into_next = k == m - 1 && next_g == glast;
         if (from_prev) {
-            first_part[k] = s;
-            whole[k] = into_next ? 1 : 0;
+            first_part[jc] = sum;
+            cont[jc] = into_next ? 2 : 1;   // 2: the run covers the whole chunk and goes on
         } else if (into_next) {
-            last_part[k] = s;
-            last_g[k] = gg;
+            last_part[jc] = sum;
+            last_g[jc] = g0 + k;
         } else {
-            out[(int64_t)j * umax + gg] = (float)s;
-        }
-    };
-    if (hg >= 0 && (t == 0 || hg != s_tg[t - 1])) {   // the head run starts here
-        if (single) finish(t, hg, hs, t == 0);
-        else {
-            const bool from_prev = t == 0 && prev_g == hg;
-            const int64_t k = (int64_t)j * nch + c;
-            if (from_prev) {
-                first_part[k] = hs;
-                whole[k] = 0;
-            } else {
-                out[(int64_t)j * umax + hg] = (float)hs;   // ends inside this thread
-            }
+            out[(int64_t)j * umax + g0 + k] = (float)sum;
         }
     }
-    if (!single && tg >= 0) finish(t, tg, ts, false);   // the tail run starts inside this thread
 }
 
-// runs that cross chunk ends: from the chunk where one starts, its partial + the first partials
-// of the following chunks while they lie wholly inside the run
-__global__ void __launch_bounds__(256) k_run_carry(int J, int64_t nch, int64_t umax, const double* __restrict__ first_part,
-                                                   const uint8_t* __restrict__ whole, const double* __restrict__ last_part,
-                                                   const int32_t* __restrict__ last_g, float* __restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)J * nch) return;
-    const int32_t gg = last_g[i];
-    if (gg < 0) return;
-    const int64_t j = i / nch;
-    int64_t c = i - j * nch;
-    double s = last_part[i];
-    while (++c < nch) {
-        const int64_t k = j * nch + c;
-        s += first_part[k];
-        if (!whole[k]) break;
+// Per row (one workgroup): over its chunks, Q = inclusive prefix sums of the continuation parts
+// (first_part where cont != 0) and M = the last chunk <= c where a crossing run starts; a chunk e
+// whose first run ends there (cont == 1) completes the run that started in chunk M[e - 1]:
+// last_part[M] + Q[e] - Q[M].  Q is kept in qbuf [J][nch] for the lookups.
+__global__ void __launch_bounds__(RS_T) k_run_carry(int64_t nch, int64_t umax, const double* __restrict__ first_part,
+                                                  const uint8_t* __restrict__ cont, const double* __restrict__ last_part,
+                                                  const int32_t* __restrict__ last_g, double* __restrict__ qbuf,
+                                                  float* __restrict__ out) {
+    __shared__ double s_sc[RS_T];
+    __shared__ int64_t s_mx[RS_T];
+    const int64_t j = blockIdx.x, base = j * nch;
+    const int t = (int)threadIdx.x;
+    double qcarry = 0.0;
+    int64_t mcarry = -1;
+    for (int64_t c0 = 0; c0 < nch; c0 += RS_CH) {
+        double q[4], acc = 0.0;
+        int64_t mx[4], m = -1;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int64_t c = c0 + 4 * t + i;
+            const bool in = c < nch;
+            acc += in && cont[base + c] ? first_part[base + c] : 0.0;
+            q[i] = acc;
+            if (in && last_g[base + c] >= 0) m = c;
+            mx[i] = m;
+        }
+        const double qi = block_scan(acc, s_sc, [](double x, double y) { return x + y; });
+        (void)block_scan(m, s_mx, [](int64_t x, int64_t y) { return x > y ? x : y; });   // s_mx: inclusive maxima
+        const double qoff = qcarry + (qi - acc);
+        // the running max before this thread: the inclusive max of the thread before it
+        const int64_t mprev_t = t > 0 ? s_mx[t - 1] : -1;
+        const int64_t moff = mprev_t > mcarry ? mprev_t : mcarry;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int64_t c = c0 + 4 * t + i;
+            if (c < nch) qbuf[base + c] = qoff + q[i];
+        }
+        __syncthreads();   // this tile's Q is visible to the workgroup
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int64_t c = c0 + 4 * t + i;
+            if (c >= nch || cont[base + c] != 1) continue;
+            int64_t st = i == 0 ? moff : (mx[i - 1] > moff ? mx[i - 1] : moff);   // last start chunk < c
+            if (st < 0) continue;   // cannot happen: a continued run started in an earlier chunk
+            const double s = last_part[base + st] + (qoff + q[i]) - qbuf[base + st];
+            out[j * umax + last_g[base + st]] = (float)s;
+        }
+        qcarry += s_sc[RS_T - 1];
+        mcarry = s_mx[RS_T - 1] > mcarry ? s_mx[RS_T - 1] : mcarry;
+        __syncthreads();
     }
-    out[j * umax + gg] = (float)s;
 }
 
 int launch_error() {
@@ -291,7 +311,7 @@ extern "C" int fjsp_a2c_group_runs(const uint32_t* spos, const uint32_t* scan, i
 extern "C" int fjsp_a2c_run_sums_bytes(int32_t J, int64_t S, uint64_t* bytes) {
     if (J <= 0 || S <= 0 || !bytes) return fjsp_internal_fail("fjsp_a2c_run_sums_bytes: need J > 0, S > 0");
     const int64_t n = (int64_t)J * ((S + RS_CH - 1) / RS_CH);
-    *bytes = (uint64_t)n * (8 + 1 + 8 + 4) + 64;
+    *bytes = (uint64_t)n * (8 + 8 + 8 + 4 + 1) + 64;
     return 0;
 }
 
@@ -305,17 +325,22 @@ extern "C" int fjsp_a2c_run_sums(const float* vals, int32_t J, const int32_t* ro
     if (temp_bytes < need) return fjsp_internal_fail("fjsp_a2c_run_sums: temp buffer too small");
     const hipStream_t st = (hipStream_t)stream;
     const int64_t nch = (S + RS_CH - 1) / RS_CH, n = (int64_t)J * nch;
-    char* p = (char*)temp;
-    double* first_part = (double*)p;
+    double* first_part = (double*)temp;
     double* last_part = first_part + n;
-    int32_t* last_g = (int32_t*)(last_part + n);
-    uint8_t* whole = (uint8_t*)(last_g + n);
+    double* qbuf = last_part + n;
+    int32_t* last_g = (int32_t*)(qbuf + n);
+    uint8_t* cont = (uint8_t*)(last_g + n);
     if (hipMemsetAsync(out, 0, sizeof(float) * (size_t)J * (size_t)umax, st) != hipSuccess ||
-        hipMemsetAsync(last_g, 0xFF, sizeof(int32_t) * (size_t)n, st) != hipSuccess)
+        hipMemsetAsync(last_g, 0xFF, sizeof(int32_t) * (size_t)n, st) != hipSuccess ||
+        hipMemsetAsync(cont, 0, (size_t)n, st) != hipSuccess)
         return fjsp_internal_fail("fjsp_a2c_run_sums: memset failed");
     hipLaunchKernelGGL(k_run_chunks, dim3((unsigned)nch, (unsigned)J), dim3(RS_T), 0, st, vals, rowmap, scale, perm, gsorted, S,
-                       umax, nch, out, first_part, whole, last_part, last_g);
+                       umax, nch, out, first_part, cont, last_part, last_g);
     if (int rc = launch_error()) return rc;
-    hipLaunchKernelGGL(k_run_carry, dim3(blocks(n)), dim3(256), 0, st, J, nch, umax, first_part, whole, last_part, last_g, out);
-    return launch_error();
+    if (nch > 1) {
+        hipLaunchKernelGGL(k_run_carry, dim3((unsigned)J), dim3(RS_T), 0, st, nch, umax, first_part, cont, last_part, last_g,
+                           qbuf, out);
+        if (int rc = launch_error()) return rc;
+    }
+    return 0;
 }
