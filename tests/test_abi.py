@@ -49,3 +49,26 @@ def test_a2c_layout_matches_spec():
     assert G.native.lib().fjsp_a2c_layout(out) == 0
     spec = __import__("importlib").import_module("multi-agent-rl-for-fjsp_amd.spec")
     assert list(out) == spec.a2c_feature_index()
+
+
+def test_grouping_entries_validate_arguments_without_gpu():
+    """The grouping / run-sum entries (ABI 8) reject bad shapes and null buffers before touching
+    the device: too many rows (the row id has 4 key bits), sizes past 32-bit positions, null
+    buffers, an empty run-sum batch."""
+    L = G.native.lib()
+    P = ctypes.c_void_p
+    one = P(1)
+    cnt = ctypes.c_uint64()
+    assert L.fjsp_a2c_group_temp_bytes(0, ctypes.byref(cnt)) != 0
+    assert L.fjsp_a2c_group_temp_bytes(1 << 31, ctypes.byref(cnt)) != 0
+    assert L.fjsp_a2c_group_sort(one, 17, 100, one, 1 << 20, one, one, one, one, one, one, one, None) != 0
+    assert b"R <= 16" in L.fjsp_last_error()
+    assert L.fjsp_a2c_group_sort(one, 9, 1 << 28, one, 1 << 20, one, one, one, one, one, one, one, None) != 0
+    assert L.fjsp_a2c_group_sort(None, 9, 100, one, 1 << 20, one, one, one, one, one, one, one, None) != 0
+    assert b"null" in L.fjsp_last_error()
+    assert L.fjsp_a2c_group_runs(one, one, 9, 100, 0, one, one, one, one, one, one, one, None) != 0
+    assert L.fjsp_a2c_run_sums_bytes(0, 100, ctypes.byref(cnt)) != 0
+    assert L.fjsp_a2c_run_sums_bytes(29, 100, ctypes.byref(cnt)) == 0 and cnt.value > 0
+    assert L.fjsp_a2c_run_sums(one, 29, one, None, one, one, 100, 8, one, 0, one, None) != 0
+    assert b"temp buffer too small" in L.fjsp_last_error()
+    assert L.fjsp_a2c_run_sums(one, 70000, one, None, one, one, 100, 8, one, 1 << 30, one, None) != 0
