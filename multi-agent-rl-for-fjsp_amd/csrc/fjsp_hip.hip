@@ -2276,8 +2276,13 @@ int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env
     const bool two_emit = h->n <= 256 * BLOCK;
     // the pre-draw wave pays while the CUs have a free SIMD (and only with auto-reset)
     const bool pg = h->use_pg && lds && two_emit && autoreset;
-    // the agent-group pipeline: state-independent (uniform-random) actions, LDS tables, pre-draw
-    const bool ag = h->use_ag && h->use_pipe && !full && !staged && pg && action_mode == FJSP_ACTIONS_UNMASKED;
+    // the agent-group pipeline: state-independent (uniform-random) actions, LDS tables, pre-draw;
+    // also for 16 384 < N <= 32 768, where its 64-env workgroups run in two rounds and still beat
+    // k_step_pipe<1emit> (24 576 envs 3.17 against 3.75, 32 768 3.20-3.59 against 3.87 ms per
+    // 1 024-step launch; 49 152: 4.85 against 4.37-4.72; profiles/r04/ag_two_rounds_ab.json)
+    const bool ag_wide = h->n > 256 * BLOCK && h->n <= 512 * BLOCK && h->use_lds != 0 && h->use_pg && autoreset;
+    const bool ag = h->use_ag && h->use_pipe && !full && !staged && (pg || ag_wide) &&
+                    action_mode == FJSP_ACTIONS_UNMASKED;
     h->last_kernel = ag ? "k_step_ag<lds,predraw>"
                    : (h->use_pipe && !full && !staged)
                          ? (lds ? (two_emit ? (pg ? "k_step_pipe<lds,2emit,predraw>" : "k_step_pipe<lds,2emit>")

@@ -86,6 +86,24 @@ def test_agents_matches_other_kernels_and_oracle(G):
     assert np.array_equal(a["term"], rec["term"]) and np.array_equal(a["trunc"], rec["trunc"])
 
 
+def test_agents_two_rounds_of_workgroups(G):
+    """Above 16 384 envs (here 20 000: 313 workgroups of 64 envs, two rounds on 256 CUs, the last
+    one partial) k_step_ag runs as well: bytes equal to k_step_pipe<1emit> over launches with
+    truncation resets every 51 steps, and the env views / MT streams left behind are equal."""
+    n, chunks = 20000, [120, 1, 77]
+    runs = []
+    for agents in (1, 0):
+        env = _env(G, n, agents, 1, max_episode_steps=50)
+        env.reset(seeds=torch.arange(n) * 5 + 3, num_orders=10)
+        a = _chunks(G, env, chunks, seed=33)
+        assert env.last_kernel() == (AG if agents else "k_step_pipe<1emit>")
+        runs.append((a, _views(env, (0, 16383, 16384, 19999))))
+    for k in LEAN:
+        assert P.bits_equal(runs[0][0][k], runs[1][0][k]), k
+    assert (runs[0][0]["trunc"].sum() > n)
+    _same_views(runs[0][1], runs[1][1])
+
+
 def test_agents_all_orders_done_resets(G):
     """One order per episode: random play completes it in ~1 of 4 episodes, so episodes end by
     termination (K's completion count -> AM's reset at the next step) and by truncation, at
