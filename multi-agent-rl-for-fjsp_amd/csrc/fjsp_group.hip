@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(256) k_group_runs(const uint32_t* __restrict__
     perm[i] = p;
     gsorted[i] = (int32_t)g;
     inv[r * S + p] = g;
-    if (j == 0 || G[i] != G[i - 1]) {
+    if ((j == 0 || G[i] != G[i - 1]) && g < umax) {   // g < umax: a caller's umax below a count stays in bounds
         starts[r * umax + g] = j;
         first[r * umax + g] = p;
     }
@@ -90,8 +90,8 @@ __global__ void __launch_bounds__(256) k_group_rep(const int64_t* __restrict__ i
                                                    int64_t S, int64_t RS, int64_t umax, int64_t* __restrict__ rep) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= RS) return;
-    const int64_t r = i / S;
-    rep[i] = first[r * umax + inv[i]];
+    const int64_t r = i / S, g = inv[i];
+    rep[i] = g < umax ? first[r * umax + g] : -1;
 }
 
 // Run sums: out[j][g] = sum over the sorted positions of group g of row a = rowmap[j] of
