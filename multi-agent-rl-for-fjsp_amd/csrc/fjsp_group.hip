@@ -176,7 +176,7 @@ __global__ void __launch_bounds__(RS_T) k_run_chunks(const float* __restrict__ v
         } else if (into_next) {
             last_part[jc] = sum;
             last_g[jc] = g0 + k;
-        } else {
+        } else if (g0 + k < umax) {
             out[(int64_t)j * umax + g0 + k] = (float)sum;
         }
     }
@@ -227,7 +227,7 @@ __global__ void __launch_bounds__(RS_T) k_run_carry(int64_t nch, int64_t umax, c
             int64_t st = i == 0 ? moff : (mx[i - 1] > moff ? mx[i - 1] : moff);   // last start chunk < c
             if (st < 0) continue;   // cannot happen: a continued run started in an earlier chunk
             const double s = last_part[base + st] + (qoff + q[i]) - qbuf[base + st];
-            out[j * umax + last_g[base + st]] = (float)s;
+            if (last_g[base + st] < umax) out[j * umax + last_g[base + st]] = (float)s;
         }
         qcarry += s_sc[RS_T - 1];
         mcarry = s_mx[RS_T - 1] > mcarry ? s_mx[RS_T - 1] : mcarry;
