@@ -86,15 +86,29 @@ def _stale():
 
 
 def build(force=False, verbose=False):
-    """Compile libfjsp.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    """Compile libfjsp.so for gfx950 in-tree (hipcc cross-compiles without a GPU): one hipcc
+    process per source file in parallel (no cross-file device calls), then one link."""
     if not force and not _stale():
         return LIB_PATH
-    cmd = ["hipcc"] + HIPCC_FLAGS + ["-o", LIB_PATH] + SRCS
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise FjspNativeError("hipcc failed:\n" + r.stderr[-4000:])
-    if verbose:
-        print(r.stderr)
+    import tempfile
+    with tempfile.TemporaryDirectory(prefix="fjsp_build_") as tmp:
+        objs = [os.path.join(tmp, os.path.basename(s) + ".o") for s in SRCS]
+        cflags = [f for f in HIPCC_FLAGS if f != "-shared"]
+        procs = [subprocess.Popen(["hipcc"] + cflags + ["-c", "-o", o, s], stdout=subprocess.PIPE,
+                                  stderr=subprocess.PIPE, text=True) for s, o in zip(SRCS, objs)]
+        errs = []
+        for p in procs:
+            _, err = p.communicate()
+            if p.returncode != 0:
+                errs.append(err)
+            elif verbose and err:
+                print(err)
+        if errs:
+            raise FjspNativeError("hipcc failed:\n" + "\n".join(e[-4000:] for e in errs))
+        r = subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB_PATH] + objs,
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise FjspNativeError("hipcc link failed:\n" + r.stderr[-4000:])
     return LIB_PATH
 
 

@@ -1061,8 +1061,8 @@ class VecMultiAgentA2C:
         self.entropy_coef = float(entropy_coef)
         self.max_grad_norm = float(max_grad_norm)
         self.group = group
-        if exchange not in ("allreduce", "gather"):
-            raise ValueError("exchange must be 'allreduce' or 'gather'")
+        if exchange not in ("allreduce", "gather", "shard"):
+            raise ValueError("exchange must be 'allreduce', 'gather' or 'shard'")
         self.exchange = exchange
         self.dedup = bool(dedup)   # networks once per distinct input in the update (A2CLosses)
         self.possible_agents = list(AGENTS)
@@ -1106,6 +1106,7 @@ class VecMultiAgentA2C:
         self.gae_fn = batch_advantages     # finish_trajectory over a batch (tests may inject a CPU stand-in)
         self.grad_probe = None             # grad_probe(flat reduced grads) before clip / Adam (tests)
         self.exchange_timing = None        # dict of synchronised stage times (ms) when not None (bench)
+        self.shard_info = {}               # exchange="shard": the last batch's record counts and bytes
 
     # ------------------------------------------------------------ rollout storage
     def _alloc(self):
@@ -1334,12 +1335,28 @@ class VecMultiAgentA2C:
         optimisers stay at their initial state), so a run that later switches to "allreduce"
         or resumes an optimiser must take it from the learner rank."""
         from . import distributed as D
-        fw = self.env.faults()             # synchronises; the update has host syncs of its own
+        # synchronises; the update has host syncs of its own.  With several ranks the fault words
+        # are max-reduced first, so every rank raises together instead of the healthy ones
+        # waiting in the exchange for one that raised
+        fw = D.max_over_ranks(self.env.faults(), self.group, self.device)
         if fw:
             raise RuntimeError(f"fjsp step kernels reported fault word {fw:#x} (a hand-off wait gave up): "
                                "the batch's transitions are invalid")
         if self.exchange == "gather" and D.active(self.group):
             al, cl = self._update_gathered()
+        elif self.exchange == "shard" and D.active(self.group):
+            from . import shard_learner as SL
+            t0 = self._start()
+            if ret is None:
+                ret, adv = self.advantages()
+            b = self._bufs
+            T = self.batch_size
+            info = {}
+            al, cl = SL.update_sharded(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
+                                       b["masks"][:T], b["actions"], ret, adv, self.gidx, self.midx, self.entropy_coef,
+                                       self.max_grad_norm, self.group, self.dedup, self.grad_probe, info)
+            self.shard_info = info
+            self._mark("learn", t0)
         else:
             t0 = self._start()
             if ret is None:
@@ -1409,7 +1426,10 @@ class VecMultiAgentA2C:
                 "distinct_inputs": dict(zip(AGENTS, g.U[:NA])), "distinct_global_states": g.U[NA]}
 
     def exchange_bytes_per_batch(self):
-        """Bytes one rank sends per batch with exchange="gather" (the transition slab)."""
+        """Bytes one rank sends per batch: exchange="gather" the transition slab; "shard" the
+        records the last batch sent to other ranks (measured: the combiner's output varies)."""
+        if self.exchange == "shard":
+            return self.shard_info.get("bytes_sent_to_other_ranks")
         T, N = self.batch_size, self.N
         per_env_step = GLOBAL_DIM * 4 + 29 + NA + NA * 8 + 4 + 1
         return T * N * per_env_step + N * 4

@@ -5,13 +5,14 @@
 // (a2c.py:647-703 _update over the batch); the grouped update runs it once per distinct input and
 // sums the samples' gradients by runs of this order, so the order must be deterministic.
 //
-// One flat radix sort of all rows (the row id in key bits 59..62 above 59 bits of the hash: rows
+// One flat radix sort of all rows (rocPRIM's device radix sort) (the row id in key bits 59..62 above 59 bits of the hash: rows
 // stay contiguous), 32-bit sample positions as the payload (the grouping needs no more), then one
 // inclusive scan of the run starts, and one pass that scatters each sorted position's sample,
 // group and run start.  Replaces torch.sort (64-bit payload), a blocked prefix sum, a binary
 // search per group and three gathers / scatters over [R][S].
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <stdint.h>
 
 #include "../../include/fjsp.h"
@@ -252,11 +253,11 @@ extern "C" int fjsp_a2c_group_temp_bytes(int64_t count, uint64_t* bytes) {
     if (count <= 0 || count >= (1ll << 31)) return fjsp_internal_fail("fjsp_a2c_group_temp_bytes: count must be in (0, 2^31)");
     if (!bytes) return fjsp_internal_fail("fjsp_a2c_group_temp_bytes: null pointer");
     size_t a = 0, b = 0;
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)count, 0, 63) != hipSuccess ||
-        hipcub::DeviceScan::InclusiveSum(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)count) !=
-            hipSuccess)
-        return fjsp_internal_fail("fjsp_a2c_group_temp_bytes: hipcub size query failed");
+    if (rocprim::radix_sort_pairs(nullptr, a, (const uint64_t*)nullptr, (uint64_t*)nullptr, (const uint32_t*)nullptr,
+                                  (uint32_t*)nullptr, (uint32_t)count, 0u, 63u) != hipSuccess ||
+        rocprim::inclusive_scan(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)count,
+                                rocprim::plus<uint32_t>()) != hipSuccess)
+        return fjsp_internal_fail("fjsp_a2c_group_temp_bytes: rocprim size query failed");
     *bytes = (uint64_t)(a > b ? a : b);
     return 0;
 }
@@ -276,12 +277,13 @@ extern "C" int fjsp_a2c_group_sort(const uint64_t* keys, int32_t R, int64_t S, v
     hipLaunchKernelGGL(k_group_flat, dim3(blocks(RS)), dim3(256), 0, st, keys, S, RS, flat, pos);
     if (int rc = launch_error()) return rc;
     size_t tb = (size_t)temp_bytes;
-    if (hipcub::DeviceRadixSort::SortPairs(temp, tb, flat, sorted, pos, spos, (int)RS, 0, 63, st) != hipSuccess)
+    // stable LSD radix sort over the 63 key bits (row id 59..62 above 59 hash bits)
+    if (rocprim::radix_sort_pairs(temp, tb, flat, sorted, pos, spos, (uint32_t)RS, 0u, 63u, st) != hipSuccess)
         return fjsp_internal_fail("fjsp_a2c_group_sort: radix sort failed");
     hipLaunchKernelGGL(k_group_new, dim3(blocks(RS)), dim3(256), 0, st, sorted, S, RS, runs);
     if (int rc = launch_error()) return rc;
     tb = (size_t)temp_bytes;
-    if (hipcub::DeviceScan::InclusiveSum(temp, tb, runs, scan, (int)RS, st) != hipSuccess)
+    if (rocprim::inclusive_scan(temp, tb, runs, scan, (size_t)RS, rocprim::plus<uint32_t>(), st) != hipSuccess)
         return fjsp_internal_fail("fjsp_a2c_group_sort: scan failed");
     hipLaunchKernelGGL(k_group_counts, dim3(1), dim3(64), 0, st, scan, R, S, counts);
     return launch_error();

@@ -2364,7 +2364,10 @@ int fjsp_gae_shared(const double* rewards, const float* values, const uint8_t* d
         return fail("bad GAE shape (T > 0, N > 0, agents > 0)");
     if (!rewards || !values || !done || !ret || !adv) return fail("null GAE buffer");
     const int M = agents * N;
-    if (N % 64 == 0)   // 64-column workgroups never straddle two agents: the loader-wave scan
+    // the loader-wave scan: 64-column workgroups never straddle two agents, and its 16-byte LDS
+    // DMAs need 16-byte aligned rows (a sub-view at an odd offset takes the register scan)
+    const bool aligned = (((uintptr_t)rewards | (uintptr_t)values | (uintptr_t)done) & 15u) == 0;
+    if (N % 64 == 0 && aligned)
         hipLaunchKernelGGL(k_gae_lw, dim3(M / 64), dim3(128), 0, (hipStream_t)stream, rewards, values, done, T, N, M,
                            gamma, lamb, ret, adv);
     else

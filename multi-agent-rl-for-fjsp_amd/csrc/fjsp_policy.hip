@@ -322,7 +322,31 @@ struct PolicyArgs {
     float* probs_out;
     int nc, na;   // critic / actor workgroups per role
     int tile0 = 0;   // first 64-env tile of the launch (k_policy_step over an env range)
+    int xmap = 0;    // actor workgroup -> (role, tile) order, actor_block
 };
+
+// Actor workgroup j (after the critic's) -> (role, tile).  Workgroups are dealt to the 8 XCDs
+// round-robin (block b -> XCD b mod 8), and each XCD has its own 4 MB L2, while the eight actors'
+// split-bf16 weights are 8 x 428 KB + the critic's 667 KB.  xmap 0: role-major (every XCD sees
+// every role's tiles, so every L2 pulls all nine networks each launch); 1: role = j mod 8 (one
+// actor per XCD; the AGV's tiles all on one XCD); 2: the roles in four pairs, each pair on two
+// XCDs with the tiles alternating between them (two actors + the critic per L2, the AGV's tiles
+// over 64 CUs).
+__device__ __forceinline__ void actor_block(const PolicyArgs& A, int j, int& role, int& tile) {
+    if (A.xmap == 1) {
+        role = j & 7;
+        tile = j >> 3;
+    } else if (A.xmap == 2) {
+        // pairs (AGV, small machine), (pickup, big machine), (blue 1, blue 2), (red, green)
+        constexpr uint32_t PAIR = 0x7654'3021u;   // nibble 2p + s = role s of pair p
+        const int x = j & 7, k = j >> 3, p = x & 3, h = x >> 2;
+        role = (int)((PAIR >> (4 * (2 * p + ((k + h) & 1)))) & 0xFu);
+        tile = k;
+    } else {
+        role = j / A.na;
+        tile = j % A.na;
+    }
+}
 
 // The critic on a tile of 32 envs: layers 1 and 2 one 32-row tile per wave, layer 3 (128 rows)
 // on waves 0..3, the value head from layer 3's accumulators.  SAVE (the A2C update's forward,
@@ -548,7 +572,8 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // (critic first or last, the AGV's workgroups first: within 3 %, profiles/r03/experiments)
     const int b = blockIdx.x;
-    const int role = b < A.nc ? NAG : (b - A.nc) / A.na;
+    int role = NAG, tile = 0;
+    if (b >= A.nc) actor_block(A, b - A.nc, role, tile);
     PST(0, __builtin_amdgcn_s_memrealtime());
     PST(1, __builtin_amdgcn_s_memtime());
     PST(11, __builtin_amdgcn_s_getreg(4 | (31 << 11)));
@@ -556,7 +581,7 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
     PST(13, role);
     int act = 0;
     if (role == NAG) critic_tile<false>(A, b, s_mem, tid, lane, wave, CriticSave{});
-    else actor_tile(A, role, (b - A.nc) % A.na, s_mem, tid, lane, wave, act);
+    else actor_tile(A, role, tile, s_mem, tid, lane, wave, act);
     PST(9, __builtin_amdgcn_s_memtime());
     PST(10, __builtin_amdgcn_s_memrealtime());
 }
@@ -661,7 +686,9 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
         critic_tile<false>(A, 2 * A.tile0 + b, s_mem, tid, lane, wave, CriticSave{});
         return;
     }
-    const int role = (b - A.nc) / A.na, tile = A.tile0 + (b - A.nc) % A.na;
+    int role, tile;
+    actor_block(A, b - A.nc, role, tile);
+    tile += A.tile0;
     state_prefetch(St, tile, s_state, lane, wave);   // landed by actor_tile's first barrier
     int act = 0;
     actor_tile(A, role, tile, s_mem, tid, lane, wave, act);
@@ -1117,6 +1144,13 @@ __global__ void __launch_bounds__(256) k_value_head_grad(const float* __restrict
 
 int fjsp_internal_fail(const char* msg);
 
+// actor_block's order for the policy launches: FJSP_POLICY_XMAP=0|1|2 (A/B runs; read per launch,
+// so a captured graph keeps the order it was captured with), default 2
+static int policy_xmap() {
+    const char* e = getenv("FJSP_POLICY_XMAP");
+    return (e && e[0] >= '0' && e[0] <= '2' && !e[1]) ? e[0] - '0' : 2;
+}
+
 // fjsp_a2c_policy_step's launch (fjsp_hip.hip holds the handle): k_policy_step on the policy's
 // grid, the step's state / config / outputs and the tile hand-off buffers from the handle.
 int fjsp_internal_policy_step(const float* feats, const int8_t* masks, int32_t n, const float* actor_w,
@@ -1129,7 +1163,7 @@ int fjsp_internal_policy_step(const float* feats, const int8_t* masks, int32_t n
         return fjsp_internal_fail("fjsp_a2c_policy_step: outputs limited to rewards, term, trunc, status, next_masks, feats");
     // envs [env_begin, env_begin + env_count): whole 64-env tiles (the caller checks the range)
     PolicyArgs A{feats, masks, n, actor_w, critic_w, seed, env_gid0, step, deterministic, actions, values, nullptr,
-                 values ? (env_count + TC - 1) / TC : 0, (env_count + TA - 1) / TA, env_begin / TA};
+                 values ? (env_count + TC - 1) / TC : 0, (env_count + TA - 1) / TA, env_begin / TA, policy_xmap()};
     StepArgs St{S, C, out.rewards, out.term, out.trunc, out.status, out.next_masks, out.feats, tile_cnt, tile_act, autoreset};
     hipLaunchKernelGGL(k_policy_step, dim3((unsigned)(A.nc + NAG * A.na)), dim3(NTHR), 0, stream, A, St);
     const hipError_t err = hipGetLastError();
@@ -1274,7 +1308,7 @@ extern "C" int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t 
     // workgroups: the critic on 32-env tiles (values wanted), then each actor on 64-env tiles
     // (actions wanted)
     PolicyArgs A{feats, masks, n, actor_w, critic_w, seed, env_gid0, step, deterministic, actions, values, probs,
-                 values ? (n + TC - 1) / TC : 0, actions ? (n + TA - 1) / TA : 0};
+                 values ? (n + TC - 1) / TC : 0, actions ? (n + TA - 1) / TA : 0, 0, policy_xmap()};
     hipLaunchKernelGGL(k_policy, dim3((unsigned)(A.nc + NAG * A.na)), dim3(NTHR), 0, (hipStream_t)stream, A);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {

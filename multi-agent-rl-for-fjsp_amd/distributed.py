@@ -26,12 +26,17 @@ import torch.distributed as dist
 
 
 LOCAL = "local"   # group argument meaning "this process only" (no collective, even when initialised)
+# tests: treat an initialised single-rank group as active, so that the collective code paths (the
+# device-tensor branches under RCCL) run on one GPU
+FORCE_ACTIVE = False
 
 
 def active(group=None):
     if group is LOCAL:
         return False
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return FORCE_ACTIVE or dist.get_world_size(group) > 1
 
 
 def rank_world():
@@ -70,6 +75,17 @@ def allreduce_max(t, group=None):
         t = t.clone()
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return t
+
+
+def max_over_ranks(value, group=None, device=None):
+    """max of a non-negative Python int over the ranks (the value itself without a group): RCCL
+    reduces a device tensor, gloo a host one."""
+    if not active(group):
+        return value
+    dev = torch.device("cpu") if _backend(group) == "gloo" else (device or torch.device("cuda", torch.cuda.current_device()))
+    t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
 
 
 def adv_stats(adv, group=None):
@@ -149,25 +165,37 @@ def gather_slabs(slabs, dst=0, group=None):
     collective: every tensor is viewed as bytes and packed into one flat buffer.  Returns on
     `dst` a dict of [world, *shape] tensors, None on the other ranks (single process: the
     slabs with a leading axis of 1)."""
-    names = list(slabs)
+    # widest elements first, every piece padded to 8 bytes: each tensor's bytes start 8-byte
+    # aligned in the flat buffer, so the results are views of the receive buffer (no copies)
+    names = sorted(slabs, key=lambda k: -slabs[k].element_size())
     if not active(group):
-        return {k: slabs[k].unsqueeze(0) for k in names}
+        return {k: slabs[k].unsqueeze(0) for k in slabs}
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    flat = torch.cat([slabs[k].contiguous().view(-1).view(torch.uint8) for k in names])
+    pieces = []
+    for k in names:
+        b = slabs[k].contiguous().view(-1).view(torch.uint8)
+        pieces.append(b)
+        if b.numel() % 8:
+            pieces.append(b.new_zeros(8 - b.numel() % 8))
+    flat = torch.cat(pieces)
     gloo = _backend(group) == "gloo"
     src = flat.cpu() if gloo else flat     # gloo gathers host tensors
-    bufs = [torch.empty_like(src) for _ in range(world)] if rank == dst else None
+    allb = bufs = None
+    if rank == dst:
+        # one preallocated [world, bytes] receive buffer; the gather writes its rows in place
+        allb = torch.empty((world, flat.numel()), dtype=torch.uint8, device=src.device)
+        bufs = list(allb.unbind(0))
     dist.gather(src, gather_list=bufs, dst=dst, group=group)
     if rank != dst:
         return None
-    allb = torch.stack(bufs).to(flat.device)       # [world, bytes]
+    allb = allb.to(flat.device)
     out, off = {}, 0
     for k in names:
         t = slabs[k]
         nb = t.numel() * t.element_size()
-        out[k] = allb[:, off:off + nb].contiguous().view(t.dtype).view((world,) + tuple(t.shape))
-        off += nb
-    return out
+        out[k] = allb[:, off:off + nb].view(t.dtype).view((world,) + tuple(t.shape))   # a strided view
+        off += -(-nb // 8) * 8
+    return {k: out[k] for k in slabs}
 
 
 def broadcast_flat(tensors, src=0, group=None):

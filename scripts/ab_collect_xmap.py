@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""A/B of the collect's actor-workgroup order (FJSP_POLICY_XMAP, csrc/fjsp_policy.hip actor_block):
+one learner per order, each captured with its order, replayed in alternation (256 x N per batch,
+ms per batch), and the rollout slabs compared byte for byte across orders after every batch (the
+order changes which workgroup computes what, never a value).
+
+usage: python scripts/ab_collect_xmap.py [N] [reps] [orders, e.g. 0,1,2]"""
+import importlib
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+A = importlib.import_module("multi-agent-rl-for-fjsp_amd.a2c_vec")
+V = importlib.import_module("multi-agent-rl-for-fjsp_amd.vec_env")
+
+
+def main(n=4096, reps=10, orders=(0, 1, 2), init="random", T=256):
+    learners = {}
+    for x in orders:
+        os.environ["FJSP_POLICY_XMAP"] = str(x)
+        L = A.VecMultiAgentA2C(V.FJSPVecEnv(n), batch_size=T, seed=3)
+        if init == "trained":
+            L.load_state_dicts(A.load_npz_weights(os.path.join(REPO, "tests", "golden", "trained_policy.npz")))
+        L.reset(seeds=torch.arange(n), num_orders=25)
+        for _ in range(3):       # eager, capture, replay (each captured with its own order)
+            L.collect()
+            L.roll_over()
+        learners[x] = L
+    torch.cuda.synchronize()
+    ms = {x: [] for x in orders}
+    equal = True
+    for _ in range(reps):
+        for x in orders:
+            L = learners[x]
+            t0 = time.perf_counter()
+            L.collect()
+            torch.cuda.synchronize()
+            ms[x].append((time.perf_counter() - t0) * 1e3)
+        b0 = learners[orders[0]]._bufs
+        for x in orders[1:]:
+            b = learners[x]._bufs
+            equal &= all(torch.equal(b0[k], b[k]) for k in ("feats", "masks", "actions", "values", "rewards", "term",
+                                                            "trunc", "status"))
+        for x in orders:
+            learners[x].roll_over()
+    med = {x: sorted(v)[len(v) // 2] for x, v in ms.items()}
+    return {"envs": n, "batch": T, "init": init, "collect_ms_median": med, "collect_ms": ms,
+            "slabs_equal_across_orders": bool(equal)}
+
+
+if __name__ == "__main__":
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    orders = tuple(int(x) for x in sys.argv[3].split(",")) if len(sys.argv) > 3 else (0, 1, 2)
+    for init in ("random", "trained"):
+        print(json.dumps(main(n, reps, orders, init)), flush=True)

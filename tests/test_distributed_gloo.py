@@ -183,6 +183,8 @@ def _gather_worker(rank, world, port, out_dir):
     params = torch.cat([p.detach().reshape(-1) for p in list(L.actors.parameters()) + list(L.critic.parameters())])
     slabs = D.gather_slabs({"a": torch.full((2, 3), rank, dtype=torch.int16),
                             "b": torch.full((4,), 0.5 + rank, dtype=torch.float64)}, dst=0)
+    if slabs is not None:     # views of one receive buffer (different dtypes): saved as copies
+        slabs = {k: v.clone() for k, v in slabs.items()}
     torch.save({"al": al, "cl": cl, "params": params, "slabs": slabs, "grads": grads},
                os.path.join(out_dir, f"g{rank}.pt"))
     dist.barrier()
@@ -210,3 +212,50 @@ def test_gather_exchange_equals_single_learner(tmp_path):
     assert s["a"].shape == (2, 2, 3) and bool((s["a"][1] == 1).all()) and bool((s["a"][0] == 0).all())
     assert s["b"].dtype == torch.float64 and float(s["b"][1, 0]) == 1.5
     assert r[1]["slabs"] is None
+
+
+# ---------------------------------------------------------------- learner sharded by network (exchange="shard")
+def _shard_worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+    n = N // world
+    L = _learner(n, rank * n, dist.group.WORLD, "shard")
+    _fill(L, slice(rank * n, (rank + 1) * n))
+    grads = []
+    L.grad_probe = grads.append
+    al, cl = L.update()
+    params = torch.cat([p.detach().reshape(-1) for p in list(L.actors.parameters()) + list(L.critic.parameters())])
+    torch.save({"al": al, "cl": cl, "params": params, "grads": grads, "info": L.shard_info},
+               os.path.join(out_dir, f"s{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shard_exchange_equals_single_learner(tmp_path, world):
+    """exchange="shard": each rank combines its samples into (input, mask, action) / global-state
+    records, one all_to_all routes them to the rank owning the network (actor a on rank a mod
+    world, critic states by key), owners back-propagate, one all_reduce sums the gradients: the
+    single learner's gradients up to summation order, identical parameters on every rank."""
+    assert N % world == 0
+    mp.spawn(_shard_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [torch.load(os.path.join(tmp_path, f"s{k}.pt"), weights_only=True) for k in range(world)]
+    L = _learner(N, 0, None, "allreduce")
+    _fill(L, slice(0, N))
+    grads = []
+    L.grad_probe = grads.append
+    al, cl = L.update()
+    params = torch.cat([p.detach().reshape(-1) for p in list(L.actors.parameters()) + list(L.critic.parameters())])
+    for k in range(world):
+        assert not r[k]["info"]["fallback"]
+        assert len(r[k]["grads"]) == 1
+        assert_grads_close(r[k]["grads"][0], grads[0])
+        assert torch.equal(r[k]["grads"][0], r[0]["grads"][0])   # one all_reduce: the same sums everywhere
+        assert torch.equal(r[k]["params"], r[0]["params"])
+        assert np.allclose(r[k]["al"], al, rtol=1e-5, atol=1e-7) and r[k]["cl"] == pytest.approx(cl, rel=1e-5)
+    assert torch.allclose(r[0]["params"], params, rtol=0, atol=1e-6)
+    # every sample went into exactly one actor record per agent and one critic record
+    assert sum(x["info"]["samples"] for x in r) == T * N
+    assert sum(x["info"]["critic_records_received"] for x in r) == sum(x["info"]["critic_records_sent"] for x in r)
