@@ -65,10 +65,11 @@ def parse():
     ap.add_argument("--no-scale", action="store_true", help="skip the 16x-envs leg of the step workload")
     ap.add_argument("--no-dedup", action="store_true",
                     help="A2C update over every sample (no grouping of repeated inputs)")
-    ap.add_argument("--exchange", choices=["allreduce", "gather"], default="gather",
-                    help="a2c workload with several ranks: the once-per-batch exchange (gather = the north "
-                         "star's experience gather of the transition slabs into rank 0, a2c.py:324-336; "
-                         "allreduce = one flat gradient all_reduce)")
+    ap.add_argument("--exchange", choices=["allreduce", "gather", "shard"], default="shard",
+                    help="a2c workload with several ranks: the once-per-batch exchange (shard = the experience "
+                         "routed to the rank that learns from it: combined records in one all_to_all, actor a on "
+                         "rank a, critic states by key, shard_learner.py; gather = the transition slabs into "
+                         "rank 0, the serial learner of a2c.py:324-336; allreduce = one flat gradient all_reduce)")
     ap.add_argument("--init", choices=["random", "trained"], default="random",
                     help="a2c workload: random-init networks or the reference's trained checkpoint")
     a = ap.parse_args()
@@ -158,8 +159,9 @@ def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=
     """Batched A2C training loop (a2c_vec.VecMultiAgentA2C): env-steps/s over whole batches
     (collect batch_size vector steps with the policy + GAE + one update).  dedup: the update
     runs each network once per distinct input (A2CLosses; the same gradient).  exchange: the
-    multi-rank exchange ("allreduce" of gradients or "gather" of the transition slabs into rank
-    0, a2c.py:324-336).  init "trained": start from the reference's trained checkpoint
+    multi-rank exchange ("shard": combined records to the rank owning each network, one
+    all_to_all + one gradient all_reduce; "allreduce" of gradients; "gather" of the transition
+    slabs into rank 0, a2c.py:324-336).  init "trained": start from the reference's trained checkpoint
     (checkpoints/model.pt, carried as tests/golden/trained_policy.npz)."""
     A = importlib.import_module("multi-agent-rl-for-fjsp_amd.a2c_vec")
     learner = A.VecMultiAgentA2C(env, batch_size=batch_size, seed=0, group=group, dedup=dedup, exchange=exchange)
@@ -202,13 +204,20 @@ def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=
            "update_ms_per_batch": (elapsed - tc) * 1e3 / batches,
            "critic_loss_last": learner.critic_loss_history[-1], "update_dedup": bool(dedup),
            "exchange": exchange if world > 1 else None, "init": init,
-           "note": "fused MFMA predict (k_policy) -> fjsp_step writing a2c features in HBM (hipGraph-captured "
-                   "collect) -> fp64 GAE kernel -> grouped full-batch update (8 actors + critic, Adam); "
-                   "reference a2c.py loop: ~130 env-steps/s on one CPU core (SURVEY.md)"}
+           "note": "collect = one k_policy_step launch per vector step and env group (fused MFMA predict + "
+                   "the env step of each 64-env tile, features and masks written in HBM; hipGraph-captured) -> "
+                   "fp64 GAE kernel -> grouped full-batch update (8 actors + critic, Adam); reference a2c.py "
+                   "loop: ~130 env-steps/s on one CPU core (SURVEY.md)"}
     if world > 1:
-        out["exchange_bytes_per_rank_per_batch"] = (learner.exchange_bytes_per_batch() if exchange == "gather"
-                                                   else 4 * sum(p.numel() for p in list(learner.actors.parameters())
-                                                                + list(learner.critic.parameters())))
+        grad_bytes = 4 * sum(p.numel() for p in list(learner.actors.parameters()) + list(learner.critic.parameters()))
+        if exchange == "gather":
+            out["exchange_bytes_per_rank_per_batch"] = learner.exchange_bytes_per_batch()
+        elif exchange == "shard":
+            # the last batch's records sent to the other ranks (measured) + the gradient all_reduce
+            out["exchange_bytes_per_rank_per_batch"] = learner.exchange_bytes_per_batch() + grad_bytes
+            out["shard_records"] = {k: v for k, v in learner.shard_info.items() if k != "bytes_by_dest"}
+        else:
+            out["exchange_bytes_per_rank_per_batch"] = grad_bytes
     if stats:
         # after the timed region: one more batch with synchronised stage timers (the update's
         # stages on this rank: gather / learn (GAE + update; the learner rank's serial work under
@@ -306,7 +315,9 @@ def main():
                               "exchange": args.exchange if world > 1 else None,
                               "parallelism": f"env-shard x{world}" + (
                                   "" if world == 1 else ", experience gather into rank 0 + parameter broadcast"
-                                  if args.exchange == "gather" else ", one flat gradient all_reduce per batch")},
+                                  if args.exchange == "gather" else ", learner sharded by network: records "
+                                  "all_to_all + one gradient all_reduce" if args.exchange == "shard"
+                                  else ", one flat gradient all_reduce per batch")},
                    "a2c": res}
             print(json.dumps(out), flush=True)
         if dist:

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define FJSP_ABI_VERSION 8
+#define FJSP_ABI_VERSION 9
 
 #define FJSP_NUM_AGENTS 8      /* pickup, agv, small, big, pkg_blue_1, pkg_blue_2, pkg_red, pkg_green */
 #define FJSP_OBS_I32 20        /* pickup 7 + agv 13 (position = 2) int32 observation fields */
@@ -300,6 +300,19 @@ int fjsp_a2c_policy_step(fjsp_handle* h, const float* feats, const int8_t* masks
  * arithmetic as fjsp_a2c_policy's values.  Stream-ordered. */
 int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* critic_w, float* h1, float* h2, float* h3,
                             float* values, void* stream);
+/* The grouped update's critic loss and its backward in one pass over n distinct global states
+ * (a2c.py:683-699 critic(global_states), 713-722 calc_critic_loss; ABI 9): x f32 [n][40] as for
+ * fjsp_a2c_critic_forward, coef f64 [n][3] = (a, b, c) with state u's share of the loss
+ * a/2 V^2 + b V + c (a = 2 n_u / count, b = -2 sum R / (8 count), c = sum R^2 / (8 count)), so
+ * dL / dV = a V + b; critic_w, w3t, w2t packed as for fjsp_a2c_policy / fjsp_a2c_critic_backward.
+ * Writes h1 / h2 f32 [n][256] (post-ReLU), g3 [n][128], g2 / g1 [n][256] (the pre-activation
+ * gradients: the split-K weight gradients' operands), per 32-state tile part f32 [tiles][772] =
+ * layer 1 | 2 | 3 bias gradients (256 | 256 | 128), w4's gradient (128), b4's gradient, 3 zeros,
+ * loss f64 [tiles] (partial sums), values f32 [n] (may be NULL).  x, h1, h2, g3, g2, g1, part
+ * 16-byte aligned.  Stream-ordered. */
+int fjsp_a2c_critic_fused(const float* x, int32_t n, const float* critic_w, const float* w3t, const float* w2t,
+                          const double* coef, float* h1, float* h2, float* g3, float* g2, float* g1, float* part,
+                          double* loss, float* values, void* stream);
 /* The critic's backward through its two 256-wide ReLU layers for the A2C update (a2c.py:692-699
  * critic_loss.backward(); a2c_vec._CriticGrouped): g3 f32 [n][128] (layer 3's pre-activation
  * gradient, fjsp_a2c_value_head_grad), h1 / h2 from fjsp_a2c_critic_forward, w3t / w2t = W3^T
@@ -383,8 +396,9 @@ int fjsp_a2c_value_head_grad(const float* y, const float* gv, const float* w4, i
                              void* stream);
 int fjsp_snapshot(fjsp_handle* h, void* dst);
 int fjsp_restore(fjsp_handle* h, const void* src);
-/* Kernel timing of the last fjsp_step_many / fjsp_step launch in ms (hipEvents on the
- * handle's stream; synchronises). */
+/* Kernel timing of the last fjsp_step_many / fjsp_step / fjsp_a2c_policy_step launch in ms
+ * (hipEvents on the handle's stream; synchronises).  A fjsp_a2c_policy_step launched on another
+ * stream is not timed (it leaves the previous value). */
 int fjsp_last_kernel_ms(fjsp_handle* h, float* ms);
 /* Name of the kernel variant the last fjsp_step / fjsp_step_many launched ("" before any):
  * e.g. "k_step_pipe<lds>" (rocprof shows it as k_step_pipe). */

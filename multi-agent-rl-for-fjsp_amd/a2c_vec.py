@@ -210,9 +210,75 @@ class _CriticGrouped(torch.autograd.Function):
         return (None, gW1, gb1, gW2, gb2, gW3, ps[:C], ps[C:2 * C].view(1, C), ps[2 * C:2 * C + 1])
 
 
+class _CriticOnePass(torch.autograd.Function):
+    """The grouped update's critic loss and its gradients in one kernel pass over the distinct
+    global states (fjsp_a2c_critic_fused: forward, value gradient from the per-state loss
+    coefficients, value head and the two 256-wide layers' backward; a2c.py:683-699, 713-722), then
+    the three split-K weight gradients.  x f32 [U, 40] (sample-major rows), coef f64 [U, 3] =
+    (a, b, c) with state u's loss a/2 V^2 + b V + c (critic_coef) -> the critic loss (0-d f32);
+    backward returns the gradients the forward computed, scaled by the loss's gradient."""
+
+    @staticmethod
+    def forward(ctx, x, coef, W1, b1, W2, b2, W3, b3, W4, b4):
+        U = x.shape[0]
+        dev = x.device
+        cw = pack_critic_weights(W1, b1, W2, b2, W3, b3, W4, b4)
+        w3t, w2t = pack_mfma(W3.t().contiguous()).reshape(-1), pack_mfma(W2.t().contiguous()).reshape(-1)
+        E = lambda *sh: torch.empty(*sh, dtype=torch.float32, device=dev)  # noqa: E731
+        h1, h2, g2, g1, g3 = E(U, 256), E(U, 256), E(U, 256), E(U, 256), E(U, 128)
+        tiles = -(-U // 32)
+        part = E(tiles, nat.CRITIC_FUSED_PW)
+        loss = torch.empty(tiles, dtype=torch.float64, device=dev)
+        V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        c = coef.contiguous()
+        nat.check(nat.lib().fjsp_a2c_critic_fused(V(x), U, V(cw), V(w3t), V(w2t), V(c), V(h1), V(h2), V(g3), V(g2),
+                                                  V(g1), V(part), V(loss), None,
+                                                  ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+        ps = part.sum(0)
+        ctx.grads = (_splitk_wgrad(g1, x[:, :GLOBAL_DIM]), ps[:256], _splitk_wgrad(g2, h1), ps[256:512],
+                     _splitk_wgrad(g3, h2), ps[512:640], ps[640:768].view(1, 128), ps[768:769])
+        return loss.sum().float()
+
+    @staticmethod
+    def backward(ctx, gl):
+        return (None, None) + tuple(g * gl for g in ctx.grads)
+
+
+def critic_coef(g, r3, count):
+    """Per distinct global state u of the (device) RowGroups g (one row: the critic's grouping of
+    the batch's S = T * n samples) the coefficients of its share of calc_critic_loss
+    (a2c.py:713-722): sum over its n_u samples and the 8 agents of (V_u - R)^2 / (8 count) =
+    a/2 V^2 + b V + c, a = 2 n_u / count, b = -2 sum R / (8 count), c = sum R^2 / (8 count), R the
+    f32 returns (r3 f64 [T, 8, n]) summed in f64 in sorted order -> f64 [Umax, 3]."""
+    from .shard_learner import _counts, _group_sums
+    r32 = r3.float().double()
+    S = r32.shape[0] * r32.shape[2]
+    rs = torch.stack([r32.sum(1).reshape(S), (r32 * r32).sum(1).reshape(S)])              # [2, S]
+    sums = _group_sums(g.perm, g.ends, rs)                                                # [2, Umax]
+    return critic_coef_sums(_counts(g.ends)[0].double(), sums[0], sums[1], count)
+
+
+def critic_coef_sums(nu, sr, sr2, count):
+    """critic_coef from per-state sample counts and sums of R and R^2 (f64 [U] each)."""
+    return torch.stack([2.0 * nu / count, -2.0 * sr / (NA * count), sr2 / (NA * count)], dim=1).contiguous()
+
+
+def critic_onepass(critic, x, coef):
+    """The critic loss over distinct states x f32 [U, 40] with coefficients coef f64 [U, 3]
+    (critic_coef), gradients through _CriticOnePass."""
+    n = critic.net
+    assert x.shape[1] == GROUP_ROW
+    return _CriticOnePass.apply(x.contiguous(), coef, n[0].weight, n[0].bias, n[2].weight, n[2].bias, n[4].weight,
+                                n[4].bias, n[6].weight, n[6].bias)
+
+
 # the grouped update's critic through the fused forward kernel (FJSP_CRITIC_FUSED=0: PyTorch GEMMs,
 # for A/B runs)
 critic_fused = os.environ.get("FJSP_CRITIC_FUSED", "1") != "0"
+# ... and its loss, forward and backward in one pass per distinct state (fjsp_a2c_critic_fused;
+# FJSP_CRITIC_ONEPASS=0: the forward kernel, the per-sample loss through autograd, the value head
+# and backward kernels)
+critic_onepass_on = os.environ.get("FJSP_CRITIC_ONEPASS", "1") != "0"
 # its backward through the two 256-wide layers in one kernel (FJSP_CRITIC_BWD=0: GEMMs + ReLU kernels)
 critic_bwd_fused = os.environ.get("FJSP_CRITIC_BWD", "1") != "0"
 
@@ -873,7 +939,11 @@ class A2CLosses:
                 return c[gidx[agents], torch.arange(k, device=idx.device)[:, None], :]
         # the critic first: its GEMMs keep the GPU busy while the host issues the actors' many
         # small launches (after the grouping's host synchronisations the queue is empty)
-        if gc is not None and feats.is_cuda and gc.first.shape[1] >= 65536 and critic_fused:
+        critic_loss = None
+        if gc is not None and feats.is_cuda and critic_fused and critic_onepass_on and gc.gsorted is not None:
+            critic_loss = critic_onepass(critic, rows.index_select(0, gc.first[0]), critic_coef(gc, r3, count))
+            v = None
+        elif gc is not None and feats.is_cuda and gc.first.shape[1] >= 65536 and critic_fused:
             vu = critic_grouped(critic, rows.index_select(0, gc.first[0])).reshape(1, 1, -1)
             v = gc.gather(vu).reshape(-1)                            # [S]
         elif gc is not None and feats.is_cuda:
@@ -903,7 +973,8 @@ class A2CLosses:
             pm = masked_probs(probs, agent_masks(masks, midx))
             logp = categorical_log_prob(pm, acts)                    # [8, S]
             actor_losses = -(adv_n * logp).sum(dim=1) / count - entropy_coef * ent.sum(dim=1) / count
-        critic_loss = ((v.view(T, 1, n) - r3.float()) ** 2).sum() / (NA * count)
+        if critic_loss is None:
+            critic_loss = ((v.view(T, 1, n) - r3.float()) ** 2).sum() / (NA * count)
         return actor_losses, critic_loss
 
 

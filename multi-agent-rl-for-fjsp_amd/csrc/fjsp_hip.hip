@@ -2230,14 +2230,17 @@ int fjsp_a2c_policy_step(fjsp_handle* h, const float* feats, const int8_t* masks
         return fail("fjsp_a2c_policy_step: envs [env_begin, env_begin + env_count) must be whole 64-env tiles of the handle");
     DeviceGuard g(h->device);
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    if (h->timing) HIPCHK(hipEventRecord(h->ev0, st));
+    // the handle's one event pair times launches on its own stream only: a collect that runs its
+    // env groups on several streams would otherwise report whichever launch recorded last
+    const bool timed = h->timing && st == h->stream;
+    if (timed) HIPCHK(hipEventRecord(h->ev0, st));
     h->last_kernel = "k_policy_step";
     const size_t cnt_words = ((size_t)h->ntiles + 63) & ~(size_t)63;
     const int rc = fjsp_internal_policy_step(feats, masks, h->n, actor_w, critic_w, seed, env_gid0, step, deterministic,
                                              actions, values, h->S, h->dcfg, out ? *out : kNoOut, h->tiles,
                                              h->tiles + cnt_words, autoreset, env_begin, env_count, st);
     if (rc) return rc;
-    if (h->timing) {
+    if (timed) {
         HIPCHK(hipEventRecord(h->ev1, st));
         h->timed = 1;
     }

@@ -331,9 +331,16 @@ struct PolicyArgs {
 // every role's tiles, so every L2 pulls all nine networks each launch); 1: role = j mod 8 (one
 // actor per XCD; the AGV's tiles all on one XCD); 2: the roles in four pairs, each pair on two
 // XCDs with the tiles alternating between them (two actors + the critic per L2, the AGV's tiles
-// over 64 CUs).
+// over 64 CUs); 3: two quads of roles, each with one of the two heavy actors (AGV, pickup
+// station) and three stations, each quad on four XCDs with its roles rotating over them round by
+// round (four actors + the critic per L2, every XCD one heavy role's share).
 __device__ __forceinline__ void actor_block(const PolicyArgs& A, int j, int& role, int& tile) {
-    if (A.xmap == 1) {
+    if (A.xmap == 3) {
+        constexpr uint32_t QUAD = 0x7650'4321u;   // nibble 4q + i = role i of quad q
+        const int x = j & 7, k = j >> 3, q = x >> 2;
+        role = (int)((QUAD >> (4 * (4 * q + (((x & 3) + k) & 3)))) & 0xFu);
+        tile = k;
+    } else if (A.xmap == 1) {
         role = j & 7;
         tile = j >> 3;
     } else if (A.xmap == 2) {
@@ -857,6 +864,197 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
     relu_grad_out(a[0], hv, B.g1, B.bp1 + (size_t)tile * HID, col, n, 32 * wave, lane);
 }
 
+// The grouped update's critic in ONE pass per 32-state tile (fjsp_a2c_critic_fused; a2c.py:683-699,
+// 713-722 over the batch's distinct global states, networks.py:41-61).  The critic loss of a batch
+// whose distinct state u occurs n_u times is sum_u sum_{samples, agents} (V_u - R)^2 / (8 count), a
+// quadratic in V_u: loss_u = a_u / 2 V^2 + b_u V + c_u with a_u = 2 n_u / count, b_u = -2 sum R /
+// (8 count), c_u = sum R^2 / (8 count) (coef [n][3], f64, summed per group by the caller), so
+// dL / dV_u = a_u V_u + b_u is known as soon as the forward has V_u, and the backward runs in the
+// same workgroup: forward as critic_tile (x -> h1 -> h2 -> h3 -> V; the ReLU masks of h1 / h2 kept
+// as 16 bits per lane, the C/D positions the backward's g1 / g2 tiles use), then gv (f64), g3 =
+// gv w4 [h3 > 0] from layer 3's accumulators, g2 = (g3 W3) [h2 > 0] and g1 = (g2 W2) [h1 > 0] on
+// the matrix cores (split-bf16, as k_critic_bwd).  Out: h1, h2, g3, g2, g1 (the split-K weight
+// gradients' operands), per tile the bias gradients and w4's / b4's gradients, the loss; nothing
+// else is written or re-read (the three-kernel path wrote h3, read it back for the value head and
+// read h1 / h2 / g3 again for the backward: 8 KB per state against 4.7 KB here).
+struct CriticFused {
+    const double* coef;   // [n][3]: a, b, c
+    const float* w3t;     // P(W3^T [256][128]), as CriticBwd
+    const float* w2t;     // P(W2^T [256][256])
+    float* h1;            // [n][256] post-ReLU
+    float* h2;
+    float* g3;            // [n][128] layer 3's pre-activation gradient
+    float* g2;            // [n][256] pre-activation gradients of layers 2 / 1
+    float* g1;
+    float* part;          // [tiles][FPW]: b1 | b2 | b3 grads, w4 grad [128], b4 grad, 3 zeros
+    double* loss;         // [tiles]
+    float* values;        // [n] or null
+};
+constexpr int FPW = 2 * HID + 2 * 128 + 4;
+// the column (sample) sums of a lane's 16 rows over the tile's 32 columns -> bp[row] (lanes 0 / 32)
+__device__ __forceinline__ void col_sums_out(float t[16], float* __restrict__ bp, int row0, int lane) {
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1)
+#pragma unroll
+        for (int r = 0; r < 16; r++) t[r] += __shfl_xor(t[r], o);
+    if ((lane & 31) == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            *reinterpret_cast<float4*>(bp + row0 + 8 * q + 4 * (lane >> 5)) =
+                make_float4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
+    }
+}
+// acc * mask bits -> HBM rows (sample-major [n][ld]) and the per-tile column sums into bp
+__device__ __forceinline__ void masked_grad_out(f32x16& acc, uint32_t bits, float* __restrict__ g, int ld,
+                                                float* __restrict__ bp, int col, int n, int row0, int lane) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[r] = (bits >> r) & 1u ? acc[r] : 0.0f;
+    if (col < n) {
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            *reinterpret_cast<float4*>(g + (size_t)col * ld + row0 + 8 * q + 4 * (lane >> 5)) =
+                make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+    }
+    float t[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) t[r] = acc[r];   // columns past n are 0 (their gv is 0)
+    col_sums_out(t, bp, row0, lane);
+}
+__device__ __forceinline__ uint32_t relu_bits(const f32x16& acc, const Row16& bias) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int r = 0; r < 16; r++) m |= (acc[r] + bias[r] > 0.0f ? 1u : 0u) << r;
+    return m;
+}
+__global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)))
+k_critic_fused(PolicyArgs A, CriticFused F) {
+    __shared__ __attribute__((aligned(16))) unsigned char s_mem[LDS_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tile = blockIdx.x, n = A.n, e0 = tile * TC;
+    const int col = e0 + (lane & 31);
+    __bf16* s_x = reinterpret_cast<__bf16*>(s_mem);              // inputs [NP][TC][XSC]
+    __bf16* s_h = reinterpret_cast<__bf16*>(s_mem + X_BYTES);    // h1, h2, then g3, g2 planes
+    float* s_part = reinterpret_cast<float*>(s_mem);             // value partials [4][TC] (after layer 1)
+    float* s_gv = reinterpret_cast<float*>(s_mem + X_BYTES + H_BYTES);   // [TC] dL / dV
+    float* part = F.part + (size_t)tile * FPW;
+    const float* wb = A.critic_w;
+    const bf16x8* W1 = reinterpret_cast<const bf16x8*>(wb);
+    const float* B1 = wb + NP * HID * C_DPAD / 2;
+    const bf16x8* W2 = reinterpret_cast<const bf16x8*>(B1 + HID);
+    const float* B2 = B1 + HID + NP * HID * HID / 2;
+    const bf16x8* W3 = reinterpret_cast<const bf16x8*>(B2 + HID);
+    const float* B3 = B2 + HID + NP * 128 * HID / 2;
+    const float* W4 = B3 + 128;
+    const float* B4 = W4 + 128;
+    const bf16x8* W3T = reinterpret_cast<const bf16x8*>(F.w3t);
+    const bf16x8* W2T = reinterpret_cast<const bf16x8*>(F.w2t);
+    // ---- forward (critic_tile<SAVE, ROWS> with the ReLU masks kept)
+    float xv[XI];
+    inputs_load<TC, C_DPAD, true>(A.feats, n, e0, 0, 38, tid, xv);
+    WRing<C_DPAD / 16> r1;
+    wring_start(r1, wblocks<C_DPAD / 16, C_DPAD / 16>(W1, wave, 0, lane));
+    const Row16 b1 = load_rows(B1, 32 * wave, lane);
+    inputs_store<TC, C_DPAD, true>(xv, tid, s_x);
+    __syncthreads();
+    f32x16 a[1];
+    zero_acc<1>(a);
+    mfma_rows<C_DPAD / 16, XSC, XPC, 1>(r1, wblocks<C_DPAD / 16, C_DPAD / 16>(W1, wave, 0, lane), s_x, 0, lane, a);
+    WRing<HID / 16> r2;
+    wring_start(r2, wblocks<HID / 16, HID / 16>(W2, wave, 0, lane));
+    const uint32_t m1 = relu_bits(a[0], b1);
+    store_planes<HSC, HPC>(a[0], 32 * wave, 0, b1, s_h, lane);
+    store_rows_f32(a[0], 32 * wave, b1, F.h1, HID, e0, n, lane);
+    const Row16 b2 = load_rows(B2, 32 * wave, lane);
+    __syncthreads();
+    zero_acc<1>(a);
+    mfma_rows<HID / 16, HSC, HPC, 1>(r2, wblocks<HID / 16, HID / 16>(W2, wave, 0, lane), s_h, 0, lane, a);
+    const int rt3 = wave & 3;
+    WRing<HID / 16> r3;
+    wring_start(r3, wblocks<HID / 16, HID / 16>(W3, rt3, 0, lane));
+    const Row16 b3 = load_rows(B3, 32 * rt3, lane), w4 = load_rows(W4, 32 * rt3, lane);
+    const uint32_t m2 = relu_bits(a[0], b2);
+    __syncthreads();                               // every wave has read h1
+    store_planes<HSC, HPC>(a[0], 32 * wave, 0, b2, s_h, lane);
+    store_rows_f32(a[0], 32 * wave, b2, F.h2, HID, e0, n, lane);
+    __syncthreads();
+    if (wave < 4) {
+        zero_acc<1>(a);
+        mfma_rows<HID / 16, HSC, HPC, 1>(r3, wblocks<HID / 16, HID / 16>(W3, rt3, 0, lane), s_h, 0, lane, a);
+        float v = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; r++) v = fmaf(w4[r], relu(a[0][r] + b3[r]), v);
+        v += __shfl_xor(v, 32);
+        if (lane < 32) s_part[wave * TC + lane] = v;
+    }
+    WRing<8> rb3;
+    wring_start(rb3, wblocks<8, 8>(W3T, wave, 0, lane));
+    __syncthreads();                               // value partials in; layer 3 done with the h2 planes
+    // ---- the value, its gradient and the loss (one lane per state)
+    if (wave == 0) {
+        double lt = 0.0;
+        float gv = 0.0f, vg = 0.0f;
+        if (lane < TC && e0 + lane < n) {
+            float val = B4[0];
+#pragma unroll
+            for (int w = 0; w < 4; w++) val += s_part[w * TC + lane];
+            const double* c = F.coef + (size_t)(e0 + lane) * 3;
+            const double v64 = (double)val;
+            gv = (float)(c[0] * v64 + c[1]);
+            lt = (0.5 * c[0] * v64 + c[1]) * v64 + c[2];
+            vg = gv;
+            if (F.values) F.values[e0 + lane] = val;
+        }
+        if (lane < TC) s_gv[lane] = gv;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            lt += __shfl_xor(lt, o);
+            vg += __shfl_xor(vg, o);
+        }
+        if (lane == 0) {
+            F.loss[tile] = lt;
+            *reinterpret_cast<float4*>(part + 2 * HID + 2 * 128) = make_float4(vg, 0.f, 0.f, 0.f);
+        }
+    }
+    __syncthreads();
+    // ---- value head backward (waves 0..3: layer 3's accumulators): g3 = gv w4 [h3 > 0], w4's
+    // gradient sum gv h3, b3's sum g3; g3 -> HBM and -> bf16 planes for g2
+    constexpr int PL3 = TC * GS3;
+    if (wave < 4) {
+        const float gv = s_gv[lane & 31];
+        float tw[16], tb[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const float h = relu(a[0][r] + b3[r]);
+            tw[r] = gv * h;
+            a[0][r] = h > 0.0f ? gv * w4[r] : 0.0f;
+            tb[r] = a[0][r];
+        }
+        if (col < n) {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                *reinterpret_cast<float4*>(F.g3 + (size_t)col * 128 + 32 * rt3 + 8 * q + 4 * (lane >> 5)) =
+                    make_float4(a[0][4 * q], a[0][4 * q + 1], a[0][4 * q + 2], a[0][4 * q + 3]);
+        }
+        store_planes_raw<GS3, PL3>(a[0], 32 * rt3, s_h, lane);
+        col_sums_out(tb, part + 2 * HID, 32 * rt3, lane);
+        col_sums_out(tw, part + 2 * HID + 128, 32 * rt3, lane);
+    }
+    __syncthreads();
+    // ---- g2 = (g3 W3) [h2 > 0], g1 = (g2 W2) [h1 > 0] (k_critic_bwd's products)
+    zero_acc<1>(a);
+    mfma_rows<8, GS3, PL3, 1>(rb3, wblocks<8, 8>(W3T, wave, 0, lane), s_h, 0, lane, a);
+    WRing<16> rb2;
+    wring_start(rb2, wblocks<16, 16>(W2T, wave, 0, lane));
+    masked_grad_out(a[0], m2, F.g2, HID, part + HID, col, n, 32 * wave, lane);
+    __syncthreads();                               // every wave has read the g3 planes
+    store_planes_raw<HSC, HPC>(a[0], 32 * wave, s_h, lane);
+    __syncthreads();
+    zero_acc<1>(a);
+    mfma_rows<16, HSC, HPC, 1>(rb2, wblocks<16, 16>(W2T, wave, 0, lane), s_h, 0, lane, a);
+    masked_grad_out(a[0], m1, F.g1, HID, part, col, n, 32 * wave, lane);
+}
+
 // Keys of the A2C update's grouping of repeated inputs (a2c_vec.row_keys, the same hash): per
 // sample s = t * n + e of feats f32 [T][38][n], key a < 8 over actor a's 13 padded input columns
 // (its OBS_DIMS[a] a2c features, then zeros), key 8 over all 38; k = fmix64(k * MUL + bits(x_c)
@@ -1144,11 +1342,11 @@ __global__ void __launch_bounds__(256) k_value_head_grad(const float* __restrict
 
 int fjsp_internal_fail(const char* msg);
 
-// actor_block's order for the policy launches: FJSP_POLICY_XMAP=0|1|2 (A/B runs; read per launch,
-// so a captured graph keeps the order it was captured with), default 2
+// actor_block's order for the policy launches: FJSP_POLICY_XMAP=0..3 (A/B runs; read per launch,
+// so a captured graph keeps the order it was captured with), default 0
 static int policy_xmap() {
     const char* e = getenv("FJSP_POLICY_XMAP");
-    return (e && e[0] >= '0' && e[0] <= '2' && !e[1]) ? e[0] - '0' : 2;
+    return (e && e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : 0;
 }
 
 // fjsp_a2c_policy_step's launch (fjsp_hip.hip holds the handle): k_policy_step on the policy's
@@ -1274,6 +1472,25 @@ extern "C" int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* c
     if ((uintptr_t)x & 15u) return fjsp_internal_fail("fjsp_a2c_critic_forward: x must be 16-byte aligned");
     PolicyArgs A{x, nullptr, n, nullptr, critic_w, nullptr, 0u, 0u, 0, nullptr, values, nullptr, (n + TC - 1) / TC, 0};
     hipLaunchKernelGGL(k_critic_fwd, dim3((unsigned)A.nc), dim3(NTHR), 0, (hipStream_t)stream, A, CriticSave{h1, h2, h3});
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int fjsp_a2c_critic_fused(const float* x, int32_t n, const float* critic_w, const float* w3t,
+                                     const float* w2t, const double* coef, float* h1, float* h2, float* g3, float* g2,
+                                     float* g1, float* part, double* loss, float* values, void* stream) {
+    if (n <= 0) return fjsp_internal_fail("fjsp_a2c_critic_fused: n must be > 0");
+    if (!x || !critic_w || !w3t || !w2t || !coef || !h1 || !h2 || !g3 || !g2 || !g1 || !part || !loss)
+        return fjsp_internal_fail("fjsp_a2c_critic_fused: null buffer");
+    if (((uintptr_t)x | (uintptr_t)h1 | (uintptr_t)h2 | (uintptr_t)g3 | (uintptr_t)g2 | (uintptr_t)g1 | (uintptr_t)part) & 15u)
+        return fjsp_internal_fail("fjsp_a2c_critic_fused: x, h1, h2, g3, g2, g1 and part must be 16-byte aligned");
+    PolicyArgs A{x, nullptr, n, nullptr, critic_w, nullptr, 0u, 0u, 0, nullptr, values, nullptr, (n + TC - 1) / TC, 0};
+    const CriticFused F{coef, w3t, w2t, h1, h2, g3, g2, g1, part, loss, values};
+    hipLaunchKernelGGL(k_critic_fused, dim3((unsigned)A.nc), dim3(NTHR), 0, (hipStream_t)stream, A, F);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

@@ -285,7 +285,18 @@ def owner_losses(actors, critic, recv, rank, world, count, entropy_coef):
         la = -(w * logp).sum() / count - entropy_coef * (nrec * ent).sum() / count
         al = al + torch.nn.functional.one_hot(torch.tensor(a, device=dev), NA).float() * la
     g = _regroup(crec[:, 0:2].contiguous().view(torch.int64).reshape(-1))
-    if g is not None:
+    if g is not None and crec.is_cuda and A.critic_fused and A.critic_onepass_on and g.gsorted is not None:
+        # the critic's share in one pass per distinct state (fjsp_a2c_critic_fused): the records of
+        # one state (from every source rank) merged into its sample count and return sums
+        xs = crec[:, 8:8 + A.GLOBAL_DIM]
+        bad = bad | (xs.index_select(0, g.rep[0]) != xs).any()
+        vals = torch.stack([crec[:, 6].double(), crec[:, 2:4].contiguous().view(torch.float64).reshape(-1),
+                            crec[:, 4:6].contiguous().view(torch.float64).reshape(-1)])
+        su = _group_sums(g.perm, g.ends, vals)                                            # [3, Umax]
+        x = torch.nn.functional.pad(xs.index_select(0, g.first[0]).contiguous().view(torch.float32),
+                                    (0, A.GROUP_ROW - A.GLOBAL_DIM))                     # [Umax, 40]
+        cl = A.critic_onepass(critic, x, A.critic_coef_sums(su[0], su[1], su[2], count))
+    elif g is not None:
         xs = crec[:, 8:8 + A.GLOBAL_DIM]
         bad = bad | (xs.index_select(0, g.rep[0]) != xs).any()
         u = g.U[0]

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Summarise the A2C bench's rocprofv3 passes (scripts/gpu_r04_prof.sh: gpurun_out/prof_a2c/{kt,
-fetch,write,hit}) into profiles/<round>/a2c/: the kernel stats CSV and pmc_collect_summary.json,
+"""Summarise the A2C bench's rocprofv3 passes (scripts/gpu.sh <out> prof_a2c: gpurun_out/<out>/a2c_{kt,
+fetch_size,write_size,tcc_hit_sum}) into profiles/<round>/a2c/: the kernel stats CSV and pmc_collect_summary.json,
 per kernel: launches, average duration, HBM bytes per launch ((2 x FETCH_SIZE + WRITE_SIZE) kB,
 MI355X_MICROARCH.md's gfx950 correction), per env, against the algorithmic bytes, and the L2 hit
 rate (TCC_HIT / (TCC_HIT + TCC_MISS)).
@@ -52,12 +52,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("round")
     ap.add_argument("--envs", type=int, default=4096)
-    ap.add_argument("--src", default=os.path.join(REPO, "gpurun_out", "prof_a2c"))
+    ap.add_argument("--src", required=True, help="gpurun_out/<out> of a `scripts/gpu.sh <out> prof_a2c` run")
     a = ap.parse_args()
     dst = os.path.join(REPO, "profiles", a.round, "a2c")
     os.makedirs(dst, exist_ok=True)
     stats = {}
-    sp = find(os.path.join(a.src, "kt"), "kernel_stats.csv")
+    sp = find(os.path.join(a.src, "a2c_kt"), "kernel_stats.csv")
     with open(sp) as f:
         for row in csv.DictReader(f):
             stats[short(row["Name"])] = {"calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
@@ -65,8 +65,8 @@ def main():
                                          "pct": float(row["Percentage"])}
     shutil.copy(sp, os.path.join(dst, f"kernel_stats_a2c{a.envs}.csv"))
     c = {}
-    for p in ("fetch", "write", "hit"):
-        f = find(os.path.join(a.src, p), "counter_collection.csv")
+    for p in ("fetch_size", "write_size", "tcc_hit_sum"):
+        f = find(os.path.join(a.src, "a2c_" + p), "counter_collection.csv")
         if f:
             c.update(counters(f))
     res = {"workload": f"bench.py --workload a2c ({a.envs} envs, batch 256), kernel trace + separate PMC passes",

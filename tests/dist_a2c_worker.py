@@ -72,7 +72,8 @@ def main():
     torch.cuda.synchronize()
     torch.save({"first": first, "params1": params1, "params": flat(L), "critic": L.critic_loss_history,
                 "actor": [L.actor_loss_history[k] for k in A.AGENTS], "grads1": grads[0] if grads else None,
-                "exchange_bytes": L.exchange_bytes_per_batch(), "t_update": t_update},
+                "exchange_bytes": L.exchange_bytes_per_batch(), "t_update": t_update,
+                "shard_info": {k: v for k, v in L.shard_info.items() if not isinstance(v, list)}},
                os.path.join(a.shard_out, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()

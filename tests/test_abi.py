@@ -20,7 +20,7 @@ def test_library_exports_every_symbol():
     L = G.native.lib()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.fjsp_abi_version() == G.native.ABI_VERSION == 8
+    assert L.fjsp_abi_version() == G.native.ABI_VERSION == 9
 
 
 def test_config_validation_without_gpu():
@@ -72,3 +72,21 @@ def test_grouping_entries_validate_arguments_without_gpu():
     assert L.fjsp_a2c_run_sums(one, 29, one, None, one, one, 100, 8, one, 0, one, None) != 0
     assert b"temp buffer too small" in L.fjsp_last_error()
     assert L.fjsp_a2c_run_sums(one, 70000, one, None, one, one, 100, 8, one, 1 << 30, one, None) != 0
+
+
+def test_critic_fused_validates_arguments_without_gpu():
+    """fjsp_a2c_critic_fused (ABI 9) rejects an empty batch, null buffers and unaligned rows before
+    launching."""
+    L = G.native.lib()
+    P = ctypes.c_void_p
+    a = P(1 << 20)
+    args = [a, 64, a, a, a, a, a, a, a, a, a, a, a, None, None]
+    bad = list(args)
+    bad[1] = 0
+    assert L.fjsp_a2c_critic_fused(*bad) != 0 and b"n must be > 0" in L.fjsp_last_error()
+    bad = list(args)
+    bad[5] = None
+    assert L.fjsp_a2c_critic_fused(*bad) != 0 and b"null" in L.fjsp_last_error()
+    bad = list(args)
+    bad[0] = P((1 << 20) + 4)
+    assert L.fjsp_a2c_critic_fused(*bad) != 0 and b"16-byte aligned" in L.fjsp_last_error()

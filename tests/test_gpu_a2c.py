@@ -521,6 +521,50 @@ def test_fused_critic_forward_backward_matches_torch(M):
         assert a <= max(3 * b, 3e-3), (ef[1], et[1])
 
 
+def test_critic_onepass_matches_float64(M):
+    """The one-pass critic (a2c_vec._CriticOnePass: fjsp_a2c_critic_fused's forward, value
+    gradient from the per-state loss coefficients, value-head and hidden-layer backward in one
+    kernel, then the split-K weight gradients) against a float64 evaluation of the same loss,
+    sum_u a_u/2 V_u^2 + b_u V_u + c_u, beside the three-kernel path (critic_grouped + autograd of
+    the same loss): loss within 1e-6 relative, every gradient within max(3x the three-kernel
+    path's error, 3e-3) relative (ReLU units within rounding of 0 flip in either f32 path, see
+    test_fused_critic_forward_backward_matches_torch); a padding state (0 coefficients)
+    contributes nothing."""
+    import copy
+    A = M["A"]
+    torch.manual_seed(4)
+    _, critic = A.init_networks(seed=2, device="cuda")
+    U = 70001
+    xT = (torch.rand(38, U, device="cuda") * torch.randint(0, 30, (38, 1), device="cuda")).float()
+    nu = torch.randint(1, 6, (U,), device="cuda").double()
+    sr = torch.randn(U, device="cuda", dtype=torch.float64) * nu * 8 * 3
+    sr2 = sr * sr / (8 * nu) + torch.rand(U, device="cuda", dtype=torch.float64) * 50
+    count = float(nu.sum())
+    coef = A.critic_coef_sums(nu, sr, sr2, count)
+    coef[-1] = 0.0                                   # a padding state: no samples
+    c64 = copy.deepcopy(critic).double()
+    v64 = c64.net(xT.double().t()).reshape(-1)
+    l64 = (0.5 * coef[:, 0] * v64 * v64 + coef[:, 1] * v64 + coef[:, 2]).sum()
+    l64.backward()
+    g64 = [p.grad for p in c64.parameters()]
+    xr = torch.nn.functional.pad(xT.t(), (0, 2)).contiguous()
+    res = {}
+    for name, fwd in (("onepass", lambda: A.critic_onepass(critic, xr, coef)),
+                      ("three_kernel", lambda: (lambda v: (0.5 * coef[:, 0] * v * v + coef[:, 1] * v + coef[:, 2]).sum())(
+                          A.critic_grouped(critic, xr).double()))):
+        critic.zero_grad(set_to_none=True)
+        loss = fwd()
+        loss.backward()
+        res[name] = (float(loss), [p.grad.detach().clone() for p in critic.parameters()])
+    lo, go = res["onepass"]
+    lt, gt = res["three_kernel"]
+    assert abs(lo - float(l64)) <= 1e-6 * abs(float(l64)), (lo, float(l64))
+    for p_o, p_t, g in zip(go, gt, g64):
+        eo = float((p_o.double() - g).norm() / g.norm())
+        et = float((p_t.double() - g).norm() / g.norm())
+        assert eo <= max(3 * et, 3e-3), (eo, et)
+
+
 def test_prefix_at_equals_full_prefix_sum_on_gpu(M):
     """_prefix_at (the run sums' prefix values at the run ends only, the f64 cast inside the scan)
     is bit-identical to the full f64 prefix sum gathered at the same positions, on the GPU's scan."""
@@ -571,13 +615,15 @@ def test_row_groups_kernels_equal_stable_sort(M):
         assert np.array_equal(getattr(G, name).cpu().numpy(), want), name
 
 
-@pytest.mark.parametrize("S", [1, 1023, 50001, 300000])
+@pytest.mark.parametrize("S", [1, 1023, 50001, 300000, 1300000])
 def test_run_sums_kernel_equals_float64_group_sums(M, S):
     """fjsp_a2c_run_sums (the per-group gradient sums of the grouped update, one pass over the
     sorted runs) against float64 group sums of the same f32 products: groups of one sample,
     groups spanning many 1 024-position chunks, a row that is one group, scaled rows; within one
     f32 rounding of the f64 sum (+ f64 summation error).  The _GatherRuns backward (_run_sums)
-    takes the same kernel."""
+    takes the same kernel.  S = 1 300 000 has 1 270 chunks per row, so k_run_carry's second tile
+    of 1 024 chunks runs (the gather learner's 8.4 M samples have 8 192): the one-group row and
+    the 3-group row's runs carry their sums across the tile boundary."""
     A = M["A"]
     R = 5
     g = torch.Generator().manual_seed(S)

@@ -102,6 +102,15 @@ def test_agents_two_rounds_of_workgroups(G):
         assert P.bits_equal(runs[0][0][k], runs[1][0][k]), k
     assert (runs[0][0]["trunc"].sum() > n)
     _same_views(runs[0][1], runs[1][1])
+    # sampled envs of the first round, of the second round and of its partial last workgroup
+    # against the oracle at their ids (k_step_ag's own direct pin in this regime)
+    got = runs[0][0]
+    for e0 in (0, 16380, 19992):
+        rec, _, _ = O.rollout(8, sum(chunks), seeds=np.arange(e0, e0 + 8) * 5 + 3, gid0=e0, num_orders=10,
+                              action_seed=33, policy=0, max_episode_steps=50)
+        for k in ("obs_i32", "obs_i8", "obs_f32", "masks", "rewards"):
+            assert P.bits_equal(got[k][:, e0:e0 + 8], rec[k]), (e0, k)
+        assert np.array_equal(got["trunc"][:, e0:e0 + 8], rec["trunc"]), e0
 
 
 def test_agents_all_orders_done_resets(G):

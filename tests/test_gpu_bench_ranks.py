@@ -42,3 +42,14 @@ def test_bench_gpus2_a2c_gather():
     a = d["a2c"]
     assert a["exchange_bytes_per_rank_per_batch"] == 256 * 4096 * 258 + 4096 * 4
     assert a["n_gpus"] == 2 and a["value"] > 0
+
+
+def test_bench_gpus2_a2c_shard():
+    d = _bench("--workload", "a2c", "--steps", "1", "--warmup", "1")     # the a2c default exchange
+    assert d["n_gpus"] == 2 and d["config"]["exchange"] == "shard"
+    a = d["a2c"]
+    rec = a["shard_records"]
+    assert not rec["fallback"] and rec["samples"] == 256 * 4096
+    # the records sent to the other rank, plus the 2.7 MB gradient all_reduce: far below the slab
+    assert 0 < a["exchange_bytes_per_rank_per_batch"] < 256 * 4096 * 258
+    assert a["n_gpus"] == 2 and a["value"] > 0

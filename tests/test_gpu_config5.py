@@ -6,8 +6,9 @@
   the bytes of the oracle at their global ids.
 * Training: 8 ranks (gloo between them, all on cuda:0, launched as fresh processes by
   torch.distributed.run) each run VecMultiAgentA2C on its 4 096-env shard for one 256-step
-  batch with exchange "allreduce" (gradients summed over ranks) or "gather" (every rank's
-  transition slab into the learner rank).  Their first batch is byte-identical to the
+  batch with exchange "allreduce" (gradients summed over ranks), "gather" (every rank's
+  transition slab into the learner rank) or "shard" (each rank's combined records to the rank
+  that owns the network: actor a on rank a, critic states by key; shard_learner.py).  Their first batch is byte-identical to the
   corresponding slice of one 32 768-env learner's (sha256 per buffer), and the reduced
   gradients before clipping / Adam equal that learner's to 1e-5 relative per parameter
   tensor."""
@@ -86,7 +87,7 @@ def single(G):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("exchange", ["allreduce", "gather"])
+@pytest.mark.parametrize("exchange", ["allreduce", "gather", "shard"])
 def test_eight_rank_a2c_equals_one_32768_env_learner(G, single, tmp_path, exchange):
     ranks = run_ranks(WORLD, NS, T, 1, exchange, tmp_path, digest=True, timeout=900)
     for r, rk in enumerate(ranks):
@@ -102,9 +103,11 @@ def test_eight_rank_a2c_equals_one_32768_env_learner(G, single, tmp_path, exchan
                        "max_rel_grad_error": max(e for _, e in errs),
                        "rel_grad_error_per_tensor": [[list(s), e] for s, e in errs],
                        "rank_update_s": [rk["t_update"] for rk in ranks]}, f)
-    if exchange == "allreduce":
+    if exchange in ("allreduce", "shard"):
         for rk in ranks[1:]:
             assert torch.equal(rk["grads1"], ranks[0]["grads1"])
+        if exchange == "shard":   # the records each rank sent to the other seven (measured)
+            assert all(0 < rk["exchange_bytes"] < T * NS * 258 for rk in ranks)
     else:
         assert all(rk["grads1"] is None for rk in ranks[1:])
         assert ranks[0]["exchange_bytes"] == T * NS * 258 + NS * 4

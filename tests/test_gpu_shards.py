@@ -133,7 +133,7 @@ def run_ranks(world, n, T, batches, exchange, out, digest=False, timeout=240):
     return [torch.load(out / f"rank{k}.pt", weights_only=True) for k in range(world)]
 
 
-@pytest.mark.parametrize("exchange", ["allreduce", "gather"])
+@pytest.mark.parametrize("exchange", ["allreduce", "gather", "shard"])
 def test_two_rank_a2c_equals_single_learner(G, tmp_path, exchange):
     n, T = 64, 32
     ranks = run_ranks(2, n, T, 2, exchange, tmp_path)
@@ -146,7 +146,7 @@ def test_two_rank_a2c_equals_single_learner(G, tmp_path, exchange):
     # learner's: per tensor ||g - g_ref|| <= 1e-5 ||g_ref|| (all-reduce: every rank; gather:
     # the learner rank, the others compute none)
     P.assert_grads_close(ranks[0]["grads1"], grads)
-    if exchange == "allreduce":
+    if exchange in ("allreduce", "shard"):
         assert torch.equal(ranks[0]["grads1"], ranks[1]["grads1"])
     else:
         assert ranks[1]["grads1"] is None
