@@ -1104,6 +1104,37 @@ __global__ void __launch_bounds__(256) k_group_keys(const float* __restrict__ fe
     }
 }
 
+// The shard learner's combiner keys (shard_learner.combine): per (agent a, sample s = t n + e)
+// info = the agent's mask bits | action << 8 and the record key fmix64(key_a ^ fmix64(info * MIX +
+// 1)) over the actor input key of fjsp_a2c_group_keys (the same wrapping 64-bit arithmetic as
+// a2c_vec._fmix64), so that samples with equal (input, mask, action) share a key; bad[block] = 1
+// where a mask byte is neither 0 nor 1 (the bits would not carry it).
+__global__ void __launch_bounds__(256) k_shard_keys(const uint64_t* __restrict__ keys, const int8_t* __restrict__ masks,
+                                                    const uint8_t* __restrict__ actions, int T, int n,
+                                                    uint64_t* __restrict__ tk, int32_t* __restrict__ info,
+                                                    int32_t* __restrict__ bad) {
+    const size_t S = (size_t)T * n;
+    const size_t s = (size_t)blockIdx.x * 256 + threadIdx.x;
+    int nb = 0;
+    if (s < S) {
+        const size_t t = s / (size_t)n, e = s - t * (size_t)n;
+        uint32_t bits = 0;
+        for (int c = 0; c < 29; c++) {
+            const int m = masks[(t * 29 + c) * (size_t)n + e];
+            bits |= (uint32_t)(m != 0) << c;
+            nb |= m != 0 && m != 1;
+        }
+#pragma unroll
+        for (int a = 0; a < NAG; a++) {
+            const uint32_t ab = (bits >> c_mask_off[a]) & ((1u << c_nact[a]) - 1u);
+            const uint32_t w = ab | ((uint32_t)actions[(t * NAG + a) * (size_t)n + e] << 8);
+            info[(size_t)a * S + s] = (int32_t)w;
+            tk[(size_t)a * S + s] = gk_fmix(keys[(size_t)a * S + s] ^ gk_fmix((uint64_t)w * 0x9E3779B97F4A7C15ull + 1ull));
+        }
+    }
+    if (__syncthreads_or(nb) && threadIdx.x == 0) bad[blockIdx.x] = 1;
+}
+
 // The actor loss head of the grouped A2C update for one (agent, sample): the reference's
 // entropy, masked renormalisation / uniform fallback, Categorical log-prob and actor loss
 // (a2c.py:204-220, 705-731; a2c_vec.A2CLosses) and its gradient with respect to the sample's
@@ -1398,6 +1429,21 @@ extern "C" int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uin
     if (rows && ((uintptr_t)rows & 15u)) return fjsp_internal_fail("fjsp_a2c_group_keys: rows must be 16-byte aligned");
     hipLaunchKernelGGL(k_group_keys, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, feats, T, n,
                        keys, rows);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int fjsp_a2c_shard_keys(const uint64_t* keys, const int8_t* masks, const uint8_t* actions, int32_t T,
+                                   int32_t n, uint64_t* tk, int32_t* info, int32_t* bad, void* stream) {
+    if (T <= 0 || n <= 0) return fjsp_internal_fail("fjsp_a2c_shard_keys: T and n must be > 0");
+    if (!keys || !masks || !actions || !tk || !info || !bad) return fjsp_internal_fail("fjsp_a2c_shard_keys: null buffer");
+    const size_t S = (size_t)T * (size_t)n;
+    hipLaunchKernelGGL(k_shard_keys, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, keys, masks,
+                       actions, T, n, tk, info, bad);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

@@ -105,6 +105,21 @@ class Combined:
         return [4 * (AW * na + CW * nc) for na, nc in self.counts.tolist()]
 
 
+def shard_info_words(masks, actions):
+    """Per (agent, sample s = t n + e): the agent's mask bits | its action << 8 (int32 [8, S]) from
+    masks int8 [T, 29, n] (0 / 1) and actions u8 [T, 8, n]."""
+    T, _, n = masks.shape
+    S = T * n
+    dev = masks.device
+    sh = torch.arange(A.MASK_DIM, dtype=torch.int32, device=dev).view(1, -1, 1)
+    bits29 = ((masks != 0).to(torch.int32) << sh).sum(1, dtype=torch.int32).reshape(S)  # [S]
+    offs = A._index_tensor(tuple(A.MASK_OFFS), dev).to(torch.int32)
+    low = A._index_tensor(tuple((1 << k) - 1 for k in A.N_ACTIONS), dev).to(torch.int32)
+    bits = (bits29[None, :] >> offs[:, None]) & low[:, None]                             # [8, S]
+    act = actions.permute(1, 0, 2).reshape(NA, S).to(torch.int32)
+    return bits | (act << 8)
+
+
 def combine(feats, masks, actions, ret, adv, mean, std, world):
     """The combiner: this rank's [T, ., n] batch (feats f32 [T, 38, n], masks int8 [T, 29, n],
     actions u8 [T, 8, n], ret / adv f64 [T, 8, n]) -> its actor and critic records, routed.
@@ -121,16 +136,22 @@ def combine(feats, masks, actions, ret, adv, mean, std, world):
         keys = A.group_keys(f3)
         rows = A.feature_rows(f3)
     m = masks.contiguous()
-    bad = (~((m == 0) | (m == 1))).any()
-    sh = torch.arange(A.MASK_DIM, dtype=torch.int32, device=dev).view(1, -1, 1)
-    bits29 = (m.to(torch.int32) << sh).sum(1, dtype=torch.int32).reshape(S)             # [S]
-    offs = A._index_tensor(tuple(A.MASK_OFFS), dev).to(torch.int32)
-    low = A._index_tensor(tuple((1 << k) - 1 for k in A.N_ACTIONS), dev).to(torch.int32)
-    bits = (bits29[None, :] >> offs[:, None]) & low[:, None]                             # [8, S]
-    act = actions.permute(1, 0, 2).reshape(NA, S).to(torch.int32)
-    info = bits | (act << 8)                                                             # [8, S]
-    tk = A._fmix64(keys[:NA] ^ A._fmix64(info.to(torch.int64) * _MIX + 1))
-    g = A.RowGroups(torch.cat([tk, keys[NA:]]))                                          # 8 + 1 rows
+    if f3.is_cuda:
+        # info and record keys in one pass (fjsp_a2c_shard_keys: the torch formula below)
+        import ctypes
+        tk = torch.empty(NA + 1, S, dtype=torch.int64, device=dev)
+        info = torch.empty(NA, S, dtype=torch.int32, device=dev)
+        nb = torch.zeros(-(-S // 256), dtype=torch.int32, device=dev)
+        V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        A.nat.check(A.nat.lib().fjsp_a2c_shard_keys(V(keys), V(m), V(actions.contiguous()), T, n, V(tk), V(info), V(nb),
+                                                    ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+        tk[NA].copy_(keys[NA])
+        bad = nb.any()
+    else:
+        bad = (~((m == 0) | (m == 1))).any()
+        info = shard_info_words(m, actions)
+        tk = torch.cat([A._fmix64(keys[:NA] ^ A._fmix64(info.to(torch.int64) * _MIX + 1)), keys[NA:]])
+    g = A.RowGroups(tk)                                                                  # 8 + 1 rows
     U = g.U
     # every sample equals its group's representative: the input bitwise, the mask bits and action
     if rows.is_cuda:

@@ -521,6 +521,36 @@ def test_fused_critic_forward_backward_matches_torch(M):
         assert a <= max(3 * b, 3e-3), (ef[1], et[1])
 
 
+def test_shard_keys_kernel_equals_torch(M):
+    """fjsp_a2c_shard_keys (the shard learner's combiner keys) equals the torch formula of
+    shard_learner.combine's CPU path bit for bit, and flags a non-binary mask byte."""
+    A = M["A"]
+    SL = __import__("importlib").import_module("multi-agent-rl-for-fjsp_amd.shard_learner")
+    import ctypes
+    T, n = 5, 1000
+    g = torch.Generator().manual_seed(9)
+    masks = (torch.rand(T, 29, n, generator=g) < 0.5).to(torch.int8)
+    actions = torch.randint(0, 8, (T, 8, n), generator=g, dtype=torch.uint8)
+    keys = torch.randint(-2 ** 62, 2 ** 62, (9, T * n), generator=g, dtype=torch.int64)
+    info = SL.shard_info_words(masks, actions)
+    want = A._fmix64(keys[:8] ^ A._fmix64(info.to(torch.int64) * SL._MIX + 1))
+    for bad_byte in (False, True):
+        m = masks.clone()
+        if bad_byte:
+            m[3, 11, 777] = 2
+        dm, da, dk = m.cuda(), actions.cuda(), keys.cuda()
+        tk = torch.empty(9, T * n, dtype=torch.int64, device="cuda")
+        inf = torch.empty(8, T * n, dtype=torch.int32, device="cuda")
+        nb = torch.zeros(-(-T * n // 256), dtype=torch.int32, device="cuda")
+        V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        A.nat.check(A.nat.lib().fjsp_a2c_shard_keys(V(dk), V(dm), V(da), T, n, V(tk), V(inf), V(nb), None))
+        torch.cuda.synchronize()
+        assert bool(nb.any()) == bad_byte
+        if not bad_byte:
+            assert torch.equal(inf.cpu(), info)
+            assert torch.equal(tk[:8].cpu(), want)
+
+
 def test_critic_onepass_matches_float64(M):
     """The one-pass critic (a2c_vec._CriticOnePass: fjsp_a2c_critic_fused's forward, value
     gradient from the per-state loss coefficients, value-head and hidden-layer backward in one
