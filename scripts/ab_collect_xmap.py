@@ -4,7 +4,7 @@ one learner per order, each captured with its order, replayed in alternation (25
 ms per batch), and the rollout slabs compared byte for byte across orders after every batch (the
 order changes which workgroup computes what, never a value).
 
-usage: python scripts/ab_collect_xmap.py [N] [reps] [orders, e.g. 0,1,2]"""
+usage: python scripts/ab_collect_xmap.py [N] [reps] [orders, e.g. 0+1+2]"""
 import importlib
 import json
 import os
@@ -56,6 +56,6 @@ def main(n=4096, reps=10, orders=(0, 1, 2), init="random", T=256):
 if __name__ == "__main__":
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-    orders = tuple(int(x) for x in sys.argv[3].split(",")) if len(sys.argv) > 3 else (0, 1, 2)
+    orders = tuple(int(x) for x in sys.argv[3].replace(",", "+").split("+")) if len(sys.argv) > 3 else (0, 1, 2)
     for init in ("random", "trained"):
         print(json.dumps(main(n, reps, orders, init)), flush=True)

@@ -75,7 +75,7 @@ def main():
             off += -(-nb // 8) * 8
         bufs.append(torch.cat([parts[k] for k in SLAB]))
     a, b = old(bufs), new(allb, order)
-    same = all(torch.equal(a[k], b[k]) for k in SLAB)
+    same = all(torch.equal(a[k].contiguous().view(torch.uint8), b[k].contiguous().view(torch.uint8)) for k in SLAB)
     del a, b
     res = {"world": W, "steps": T, "envs_per_rank": n, "gathered_bytes": W * tot_old, "outputs_equal": same,
            "r04_unpack_ms": timed(lambda: old(bufs)), "head_unpack_ms": timed(lambda: new(allb, order))}

@@ -7,6 +7,7 @@
 #   bench             the driver-form bench line (N=1)
 #   bench_a2c[:args]  bench.py --workload a2c (extra args after ':' with ',' for ' ')
 #   py:<script,args>  python3 <script> <args> (',' for ' '), stdout to <stage-index>.json
+#   pyenv:<VAR=VAL+..>:<script,args>  the same with environment variables
 #   prof_step         the step bench's kernel trace + FETCH_SIZE / WRITE_SIZE passes
 #   prof_a2c[:args]   the A2C bench's kernel trace + FETCH / WRITE / L2-hit passes
 #   pmc:<ctr,..>:<script,args>  one counter pass over a python script
@@ -41,6 +42,11 @@ for stage in "$@"; do
       rc=$?; tail -c 1200 "$OUT/bench_a2c_$i.json" ;;
     py)
       timeout -k 10 900 python3 -u $args > "$OUT/py_$i.json" 2> "$OUT/py_$i.err"
+      rc=$?; tail -c 1500 "$OUT/py_$i.json"; [ $rc -ne 0 ] && tail -20 "$OUT/py_$i.err" ;;
+    pyenv)
+      # pyenv:VAR=VAL[+VAR=VAL]:script,args
+      ev="${arg%%:*}"; rest="${arg#*:}"
+      env ${ev//+/ } timeout -k 10 900 python3 -u ${rest//,/ } > "$OUT/py_$i.json" 2> "$OUT/py_$i.err"
       rc=$?; tail -c 1500 "$OUT/py_$i.json"; [ $rc -ne 0 ] && tail -20 "$OUT/py_$i.err" ;;
     prof_step)
       bash scripts/gpu_profile.sh; rc=$? ;;

@@ -215,11 +215,14 @@ def test_gather_exchange_equals_single_learner(tmp_path):
 
 
 # ---------------------------------------------------------------- learner sharded by network (exchange="shard")
-def _shard_worker(rank, world, port, out_dir):
+def _shard_worker(rank, world, port, out_dir, collide=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(2)
+    if collide:   # 4-bit grouping keys: different inputs collide, the combiner's check must catch it
+        gk = A.group_keys
+        A.group_keys = lambda f3, rows=None: gk(f3, rows) & 0xF
     n = N // world
     L = _learner(n, rank * n, dist.group.WORLD, "shard")
     _fill(L, slice(rank * n, (rank + 1) * n))
@@ -259,3 +262,22 @@ def test_shard_exchange_equals_single_learner(tmp_path, world):
     # every sample went into exactly one actor record per agent and one critic record
     assert sum(x["info"]["samples"] for x in r) == T * N
     assert sum(x["info"]["critic_records_received"] for x in r) == sum(x["info"]["critic_records_sent"] for x in r)
+
+
+def test_shard_exchange_hash_collision_falls_back(tmp_path):
+    """A hash collision in the combiner's grouping (forced: 4-bit keys) is caught by the bitwise
+    check against the representatives, flagged through the gradient all_reduce, and every rank
+    redoes the batch with the all-reduce exchange (whose own grouping check then takes the dense
+    update): the single learner's gradients, identical parameters on every rank."""
+    world = 2
+    mp.spawn(_shard_worker, args=(world, _free_port(), str(tmp_path), True), nprocs=world, join=True)
+    r = [torch.load(os.path.join(tmp_path, f"s{k}.pt"), weights_only=True) for k in range(world)]
+    L = _learner(N, 0, None, "allreduce")
+    _fill(L, slice(0, N))
+    grads = []
+    L.grad_probe = grads.append
+    L.update()
+    for k in range(world):
+        assert r[k]["info"]["fallback"]
+        assert_grads_close(r[k]["grads"][0], grads[0])
+        assert torch.equal(r[k]["params"], r[0]["params"])
