@@ -8,8 +8,8 @@ own agent's (observation, mask, action, advantage) samples, and one centralised 
 (global state, returns).  So the learner splits by network:
 
   * actor a is owned by rank a mod world; the critic's distinct global states are owned by the
-    rank their group key hashes to (key mod world), so every distinct state is learned on
-    exactly one rank;
+    rank their group key hashes to (16 key bits, dealt in proportion to per-rank weights: the AGV
+    actor's owner takes half a share), so every distinct state is learned on exactly one rank;
   * each rank first COMBINES its own samples (a combiner in the map-reduce sense): the actor
     loss is linear in the normalised advantage for a fixed (input, mask, action), and the
     critic's loss gradient in the returns for a fixed state, so
@@ -49,8 +49,28 @@ def owner_of_agent(a, world):
     return a % world
 
 
+# the critic's states are dealt to the ranks by 16 bits of their key in proportion to these
+# weights: the rank that owns the AGV's actor (1.2 M of config 5's 1.3 M actor records) takes half
+# a share of the critic, so the ranks' learner shares even out
+AGV = 1
+AGV_CRITIC_SHARE = 0.5
+
+
+def critic_bounds(world):
+    """Upper bucket edges (16-bit hash values) of ranks 0 .. world - 2 for the critic's states."""
+    w = [AGV_CRITIC_SHARE if owner_of_agent(AGV, world) == r else 1.0 for r in range(world)]
+    tot, acc, out = sum(w), 0.0, []
+    for r in range(world - 1):
+        acc += w[r]
+        out.append(int(round(65536 * acc / tot)))
+    return out
+
+
 def _critic_dest(key, world):
-    return torch.remainder(key & 0xFFFF, world)
+    if world == 1:
+        return torch.zeros_like(key)
+    b = torch.tensor(critic_bounds(world), dtype=torch.int64, device=key.device)
+    return torch.searchsorted(b, (key >> 16) & 0xFFFF, right=True)
 
 
 def _group_sums(perm, ends, vals):
