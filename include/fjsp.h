@@ -308,6 +308,15 @@ int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* critic_w, fl
  * cleared) where a mask byte is neither 0 nor 1.  Stream-ordered. */
 int fjsp_a2c_shard_keys(const uint64_t* keys, const int8_t* masks, const uint8_t* actions, int32_t T, int32_t n,
                         uint64_t* tk, int32_t* info, int32_t* bad, void* stream);
+/* The shard learner's actor loss head over one agent's records (shard_learner.owner_losses; the
+ * per-agent actor loss of a2c.py:724-731 with a record standing for n samples of equal (input,
+ * mask, action) whose normalised advantages sum to w; ABI 9): pu f32 [8][umax] = the agent's
+ * probabilities per distinct input, inv i64 [R] = each record's input group, info i32 [R] = mask
+ * bits | action << 8, wsum f64 [R], cnt i32 [R] -> grad f32 [nact][R] = dL / dp_j per record and
+ * sums f64 [ceil(R / 256)][2] = per-block partial sums of (w logp, n entropy).  Stream-ordered. */
+int fjsp_a2c_record_head(const float* pu, int32_t umax, const int64_t* inv, int32_t R, int32_t nact, const int32_t* info,
+                         const double* wsum, const int32_t* cnt, float inv_count, float ent_coef, float* grad,
+                         double* sums, void* stream);
 /* The grouped update's critic loss and its backward in one pass over n distinct global states
  * (a2c.py:683-699 critic(global_states), 713-722 calc_critic_loss; ABI 9): x f32 [n][40] as for
  * fjsp_a2c_critic_forward, coef f64 [n][3] = (a, b, c) with state u's share of the loss

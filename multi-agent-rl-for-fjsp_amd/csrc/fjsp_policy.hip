@@ -1227,6 +1227,84 @@ __global__ void __launch_bounds__(256) k_actor_head(const float* __restrict__ pu
     }
 }
 
+// The shard learner's actor loss head over an owner's records (shard_learner.owner_losses): a
+// record stands for n samples of one agent with equal (input, mask, action) and carries w = the
+// f64 sum of their normalised advantages; the samples' loss terms and gradients are linear in the
+// advantage and share everything else, so per record: -(w logp) / count - c n entropy / count, and
+// grad[j][r] = dL / dp_j of the record (k_actor_head's formulas with adv -> w and the entropy
+// weighted by n).  pu [8][umax] = the agent's probabilities per distinct input, inv [R] = each
+// record's input group; info [R] = mask bits | action << 8.
+__global__ void __launch_bounds__(256) k_record_head(const float* __restrict__ pu, int umax,
+                                                     const int64_t* __restrict__ inv, int R, int na,
+                                                     const int32_t* __restrict__ info, const double* __restrict__ wsum,
+                                                     const int32_t* __restrict__ cnt, float inv_count, float ent_coef,
+                                                     float* __restrict__ grad, double* __restrict__ sums) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    double sl = 0.0, se = 0.0;
+    if (r < R) {
+        const size_t u = (size_t)inv[r];
+        const uint32_t w0 = (uint32_t)info[r];
+        const int act = (int)((w0 >> 8) & 0xFFu);
+        const float adv = (float)wsum[r];
+        const float nr = (float)cnt[r];
+        float p[8], m[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            p[j] = pu[(size_t)j * umax + u];
+            m[j] = j < na ? (float)((w0 >> j) & 1u) : 0.0f;
+        }
+        float ent = 0.0f, g[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const float pe = p[j] + 1e-10f;
+            ent += p[j] * logf(pe);
+            g[j] = -ent_coef * inv_count * nr * -(logf(pe) + p[j] / pe);
+        }
+        ent = -ent;
+        float sr = 0.0f, sm = 0.0f, pm[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) { sr += p[j] * m[j]; sm += m[j]; }
+#pragma unroll
+        for (int j = 0; j < 8; j++) pm[j] = sr > 0.0f ? (p[j] * m[j]) / sr : m[j] / sm;
+        float s2 = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; j++) s2 += pm[j];
+        float qa = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; j++) qa = j == act ? pm[j] / s2 : qa;
+        const float eps = 1.1920928955078125e-07f;
+        const float qc = fminf(fmaxf(qa, eps), 1.0f - eps);
+        const float logp = logf(qc);
+        const float gq = (qa >= eps && qa <= 1.0f - eps) ? (-adv * inv_count) / qc : 0.0f;
+        if (sr > 0.0f) {
+            float gpm[8], dot = 0.0f;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                gpm[j] = (j == act ? gq / s2 : 0.0f) - gq * qa / s2;
+                dot += gpm[j] * (p[j] * m[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) g[j] += m[j] * (gpm[j] / sr - dot / (sr * sr));
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (j < na) grad[(size_t)j * R + r] = g[j];
+        sl = (double)adv * (double)logp;
+        se = (double)nr * (double)ent;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        sl += __shfl_xor(sl, off);
+        se += __shfl_xor(se, off);
+    }
+    __shared__ double s_part[4][2];
+    if ((threadIdx.x & 63) == 0) { s_part[threadIdx.x >> 6][0] = sl; s_part[threadIdx.x >> 6][1] = se; }
+    __syncthreads();
+    if (threadIdx.x < 2)
+        sums[(size_t)blockIdx.x * 2 + threadIdx.x] =
+            s_part[0][threadIdx.x] + s_part[1][threadIdx.x] + s_part[2][threadIdx.x] + s_part[3][threadIdx.x];
+}
+
 // The grouping check of the A2C update (a2c_vec.A2CLosses, replaces the torch gather-and-compare
 // of every input with its group's representative): sample s is bad when any of actor a's input
 // columns differs bitwise from those of rep_a[a][s], or any of its 38 global-state columns from
@@ -1429,6 +1507,22 @@ extern "C" int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uin
     if (rows && ((uintptr_t)rows & 15u)) return fjsp_internal_fail("fjsp_a2c_group_keys: rows must be 16-byte aligned");
     hipLaunchKernelGGL(k_group_keys, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, feats, T, n,
                        keys, rows);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int fjsp_a2c_record_head(const float* pu, int32_t umax, const int64_t* inv, int32_t R, int32_t nact,
+                                    const int32_t* info, const double* wsum, const int32_t* cnt, float inv_count,
+                                    float ent_coef, float* grad, double* sums, void* stream) {
+    if (R <= 0 || umax <= 0 || nact <= 0 || nact > 8)
+        return fjsp_internal_fail("fjsp_a2c_record_head: need R > 0, umax > 0, 0 < nact <= 8");
+    if (!pu || !inv || !info || !wsum || !cnt || !grad || !sums) return fjsp_internal_fail("fjsp_a2c_record_head: null buffer");
+    hipLaunchKernelGGL(k_record_head, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, (hipStream_t)stream, pu, umax, inv, R,
+                       nact, info, wsum, cnt, inv_count, ent_coef, grad, sums);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

@@ -280,6 +280,42 @@ def emulate(combs):
     return out
 
 
+class _RecordHead(torch.autograd.Function):
+    """One agent's actor loss over its records on the GPU (fjsp_a2c_record_head): forward the loss
+    and each record's gradient with respect to its input's eight probabilities; backward the
+    records' gradients summed per input group (runs of the sorted order, fjsp_a2c_run_sums).
+    pu f32 [8, Umax] per distinct input (RowGroups g, one row), info i32 [R], wsum f64 [R], cnt
+    i32 [R]."""
+
+    @staticmethod
+    def forward(ctx, pu, g, info, wsum, cnt, na, count, coef):
+        import ctypes
+        R = info.shape[0]
+        um = pu.shape[1]
+        dev = pu.device
+        grad = torch.empty(na, R, dtype=torch.float32, device=dev)
+        sums = torch.empty(-(-R // 256), 2, dtype=torch.float64, device=dev)
+        pc = pu.detach().contiguous()
+        V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        A.nat.check(A.nat.lib().fjsp_a2c_record_head(V(pc), um, V(g.inv[0].contiguous()), R, na, V(info), V(wsum),
+                                                     V(cnt), 1.0 / count, float(coef), V(grad), V(sums),
+                                                     ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+        s = sums.sum(0)
+        ctx.g, ctx.na, ctx.um = g, na, um
+        ctx.save_for_backward(grad)
+        return ((-s[0] - coef * s[1]) / count).float()
+
+    @staticmethod
+    def backward(ctx, gl):
+        (grad,) = ctx.saved_tensors
+        na, um = ctx.na, ctx.um
+        rowmap = torch.zeros(na, dtype=torch.int32, device=grad.device)
+        rs = A.run_sums(grad, rowmap, gl.reshape(1).expand(na).float(), ctx.g)                  # [na, Umax]
+        out = torch.zeros(8, um, dtype=grad.dtype, device=grad.device)
+        out[:na] = rs
+        return out, None, None, None, None, None, None, None
+
+
 def _regroup(key):
     """RowGroups of one row of record keys, or None for no records."""
     if key.numel() == 0:
@@ -313,9 +349,14 @@ def owner_losses(actors, critic, recv, rank, world, count, entropy_coef):
         um = g.first.shape[1]
         if um > u:
             pu = torch.nn.functional.pad(pu, (0, um - u))
-        p = g.gather(pu[None])                                                            # [1, 8, R]
         info = r[:, AW - 3]
         k = A.N_ACTIONS[a]
+        if r.is_cuda and g.gsorted is not None:
+            la = _RecordHead.apply(pu, g, info.contiguous(), r[:, 2:4].contiguous().view(torch.float64).reshape(-1),
+                                   r[:, AW - 2].contiguous(), k, count, entropy_coef)
+            al = al + torch.nn.functional.one_hot(torch.tensor(a, device=dev), NA).float() * la
+            continue
+        p = g.gather(pu[None])                                                            # [1, 8, R]
         j = torch.arange(8, device=dev, dtype=torch.int32)
         m = (((info[None, :] >> j[:, None]) & 1) * (j[:, None] < k)).to(torch.float32)[None]  # [1, 8, R]
         act = ((info >> 8) & 0xFF).long()[None]

@@ -552,6 +552,48 @@ def test_shard_keys_kernel_equals_torch(M):
             assert torch.equal(tk[:8].cpu(), want)
 
 
+@pytest.mark.parametrize("k", [3, 8])
+def test_record_head_kernel_matches_torch(M, k):
+    """fjsp_a2c_record_head (the shard learner's per-record actor loss head) against the same loss
+    written in torch ops and differentiated by autograd (shard_learner.owner_losses' CPU path):
+    loss and the gradient with respect to the per-input probabilities within f32 rounding, for a
+    3-action station and the 8-action AGV, with masks that leave nothing valid (uniform fallback)
+    and records of many samples."""
+    A = M["A"]
+    SL = __import__("importlib").import_module("multi-agent-rl-for-fjsp_amd.shard_learner")
+    torch.manual_seed(5)
+    U, R = 3000, 50000
+    logits = torch.randn(8, U, device="cuda")
+    logits[k:] = float("-inf")
+    keys = torch.randint(0, U, (R,), device="cuda")
+    g = A.RowGroups((keys * 7919 + 11)[None])
+    um = g.first.shape[1]
+    # the group of input u gets the probabilities of keys[first]: build per-group probabilities
+    pu = torch.softmax(logits[:, keys.index_select(0, g.first[0])], dim=0).contiguous().requires_grad_(True)
+    bits = torch.randint(0, 1 << k, (R,), device="cuda", dtype=torch.int32)
+    bits[::97] = 0                                    # nothing valid: the uniform fallback over no action
+    act = torch.randint(0, k, (R,), device="cuda", dtype=torch.int32)
+    info = (bits | (act << 8)).contiguous()
+    wsum = torch.randn(R, device="cuda", dtype=torch.float64) * 5
+    cnt = torch.randint(1, 40, (R,), device="cuda", dtype=torch.int32)
+    count, coef = 123456.0, 0.01
+    got = SL._RecordHead.apply(pu, g, info, wsum, cnt, k, count, coef)
+    got.backward()
+    g_got = pu.grad.clone()
+    pu.grad = None
+    p = g.gather(pu[None])
+    j = torch.arange(8, device="cuda", dtype=torch.int32)
+    m = (((info[None, :] >> j[:, None]) & 1) * (j[:, None] < k)).to(torch.float32)[None]
+    ent = A.entropy_of(p)[0]
+    logp = A.categorical_log_prob(A.masked_probs(p, m), ((info >> 8) & 0xFF).long()[None])[0]
+    want = -(wsum.float() * logp).sum() / count - coef * (cnt.float() * ent).sum() / count
+    want.backward()
+    ok = torch.isfinite(pu.grad)
+    assert abs(float(got) - float(want)) <= 1e-5 * abs(float(want)), (float(got), float(want))
+    d = (g_got - pu.grad)[:k][ok[:k]]
+    assert float(d.abs().max()) <= 1e-4 * float(pu.grad[:k][ok[:k]].abs().max()), float(d.abs().max())
+
+
 def test_critic_onepass_matches_float64(M):
     """The one-pass critic (a2c_vec._CriticOnePass: fjsp_a2c_critic_fused's forward, value
     gradient from the per-state loss coefficients, value-head and hidden-layer backward in one
