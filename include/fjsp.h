@@ -308,6 +308,13 @@ int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* critic_w, fl
  * cleared) where a mask byte is neither 0 nor 1.  Stream-ordered. */
 int fjsp_a2c_shard_keys(const uint64_t* keys, const int8_t* masks, const uint8_t* actions, int32_t T, int32_t n,
                         uint64_t* tk, int32_t* info, int32_t* bad, void* stream);
+/* Weights into the policy / critic kernels' operand layout (a2c_vec.pack_mfma; ABI 9): W f32
+ * [B][R][K] (transposed = 1: a [B][K][R] source packed as its transpose) -> out [B][R/32][K/16]
+ * [3][64][8] bf16 (as floats: [.., 3, 64, 4]), element (b, t, kb, p, l, j) = plane p of the
+ * three-bf16 split of W[b][32 t + (l & 31)][16 kb + 8 (l >> 5) + j] (hi = bf16(x), mid =
+ * bf16(x - hi), lo = bf16(x - hi - mid), round to nearest even).  R % 32 == 0, K % 16 == 0.
+ * Stream-ordered. */
+int fjsp_a2c_pack_mfma(const float* W, int32_t B, int32_t R, int32_t K, int32_t transposed, float* out, void* stream);
 /* The shard learner's actor loss head over one agent's records (shard_learner.owner_losses; the
  * per-agent actor loss of a2c.py:724-731 with a record standing for n samples of equal (input,
  * mask, action) whose normalised advantages sum to w; ABI 9): pu f32 [8][umax] = the agent's

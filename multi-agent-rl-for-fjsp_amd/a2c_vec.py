@@ -194,7 +194,7 @@ class _CriticGrouped(torch.autograd.Function):
         gW3 = _splitk_wgrad(g3, h2)
         if critic_bwd_fused:
             # both 256-wide ReLU layers' input gradients in one pass (fjsp_a2c_critic_backward)
-            w3t, w2t = pack_mfma(W3.t().contiguous()).reshape(-1), pack_mfma(W2.t().contiguous()).reshape(-1)
+            w3t, w2t = pack_mfma(W3.detach().t()).reshape(-1), pack_mfma(W2.detach().t()).reshape(-1)
             g2, g1 = torch.empty_like(h2), torch.empty_like(h1)
             nt = -(-B // 32)
             bp2 = torch.empty(nt, h2.shape[1], dtype=torch.float32, device=h2.device)
@@ -223,7 +223,7 @@ class _CriticOnePass(torch.autograd.Function):
         U = x.shape[0]
         dev = x.device
         cw = pack_critic_weights(W1, b1, W2, b2, W3, b3, W4, b4)
-        w3t, w2t = pack_mfma(W3.t().contiguous()).reshape(-1), pack_mfma(W2.t().contiguous()).reshape(-1)
+        w3t, w2t = pack_mfma(W3.detach().t()).reshape(-1), pack_mfma(W2.detach().t()).reshape(-1)
         E = lambda *sh: torch.empty(*sh, dtype=torch.float32, device=dev)  # noqa: E731
         h1, h2, g2, g1, g3 = E(U, 256), E(U, 256), E(U, 256), E(U, 256), E(U, 128)
         tiles = -(-U // 32)
@@ -1006,7 +1006,34 @@ def pack_mfma(W):
     """[..., R, K] f32 -> [..., R/32, K/16, 3, 64, 4] f32 words holding [..., 3, 64, 8] bf16 with
     (t, kb, p, l, j) = plane p of W[32 t + (l & 31)][16 kb + 8 (l >> 5) + j]: the A-operand lane order
     of v_mfma_f32_32x32x16_bf16, one 16-byte load per lane per plane and 16-deep block, the three
-    planes of split_bf16x3 (csrc/fjsp_policy.hip, include/fjsp.h)."""
+    planes of split_bf16x3 (csrc/fjsp_policy.hip, include/fjsp.h).  On the GPU one launch of
+    fjsp_a2c_pack_mfma (bit-equal to the torch formulation below); W may be a transposed view of
+    a contiguous [..., K, R] tensor."""
+    *lead, R, K = W.shape
+    if W.is_cuda and W.dtype == torch.float32 and R % 32 == 0 and K % 16 == 0 and pack_kernel_on:
+        B = 1
+        for d in lead:
+            B *= d
+        tr = 0
+        src = W
+        if not W.is_contiguous():
+            if W.dim() >= 2 and W.transpose(-1, -2).is_contiguous():
+                src, tr = W.transpose(-1, -2), 1
+            else:
+                src = W.contiguous()
+        out = torch.empty(*lead, R // 32, K // 16, 3, 64, 4, dtype=torch.float32, device=W.device)
+        nat.check(nat.lib().fjsp_a2c_pack_mfma(ctypes.c_void_p(src.data_ptr()), B, R, K, tr,
+                                               ctypes.c_void_p(out.data_ptr()),
+                                               ctypes.c_void_p(torch.cuda.current_stream(W.device).cuda_stream)))
+        return out
+    return pack_mfma_torch(W)
+
+
+pack_kernel_on = os.environ.get("FJSP_PACK_KERNEL", "1") != "0"
+
+
+def pack_mfma_torch(W):
+    """pack_mfma in torch ops (CPU, and the GPU test's reference)."""
     *lead, R, K = W.shape
     nl = len(lead)
     Pl = torch.stack(split_bf16x3(W), dim=nl)                                # [..., 3, R, K]

@@ -1104,6 +1104,43 @@ __global__ void __launch_bounds__(256) k_group_keys(const float* __restrict__ fe
     }
 }
 
+// Weights into the matrix cores' operand order (a2c_vec.pack_mfma, include/fjsp.h): W f32 [B][R][K]
+// (or, transposed, the K x R source [B][K][R] read as its transpose) -> [B][R/32][K/16][3][64][8]
+// bf16, element (b, t, kb, p, l, j) = plane p of split3(W[b][32 t + (l & 31)][16 kb + 8 (l >> 5)
+// + j]).  One thread per (b, t, kb, l, 4 consecutive j): reads 4 values, writes 4 bf16 of each
+// plane.  Replaces ~9 elementwise / stack / permute launches per matrix after every update.
+__global__ void __launch_bounds__(256) k_pack_mfma(const float* __restrict__ W, int B, int R, int K, int tr,
+                                                   __bf16* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int KB = K / 16, RT = R / 32;
+    const int64_t total = (int64_t)B * RT * KB * 64 * 2;
+    if (i >= total) return;
+    const int q = (int)(i & 1);                       // j half: 4 q .. 4 q + 3
+    const int l = (int)((i >> 1) & 63);
+    int64_t rest = i >> 7;
+    const int kb = (int)(rest % KB);
+    rest /= KB;
+    const int t = (int)(rest % RT);
+    const int b = (int)(rest / RT);
+    const int row = 32 * t + (l & 31), k0 = 16 * kb + 8 * (l >> 5) + 4 * q;
+    const float* src = W + (size_t)b * R * K;
+    bf16x4 ph, pm, pl;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const float v = tr ? src[(size_t)(k0 + j) * R + row] : src[(size_t)row * K + k0 + j];
+        __bf16 x0, x1, x2;
+        split3(v, x0, x1, x2);
+        ph[j] = x0;
+        pm[j] = x1;
+        pl[j] = x2;
+    }
+    // [b][t][kb][p][l][j]: plane stride 64 * 8 bf16
+    __bf16* o = out + ((((size_t)b * RT + t) * KB + kb) * NP * 64 + l) * 8 + 4 * q;
+    *reinterpret_cast<bf16x4*>(o) = ph;
+    *reinterpret_cast<bf16x4*>(o + 64 * 8) = pm;
+    *reinterpret_cast<bf16x4*>(o + 2 * 64 * 8) = pl;
+}
+
 // The shard learner's combiner keys (shard_learner.combine): per (agent a, sample s = t n + e)
 // info = the agent's mask bits | action << 8 and the record key fmix64(key_a ^ fmix64(info * MIX +
 // 1)) over the actor input key of fjsp_a2c_group_keys (the same wrapping 64-bit arithmetic as
@@ -1507,6 +1544,23 @@ extern "C" int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uin
     if (rows && ((uintptr_t)rows & 15u)) return fjsp_internal_fail("fjsp_a2c_group_keys: rows must be 16-byte aligned");
     hipLaunchKernelGGL(k_group_keys, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, feats, T, n,
                        keys, rows);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int fjsp_a2c_pack_mfma(const float* W, int32_t B, int32_t R, int32_t K, int32_t transposed, float* out,
+                                  void* stream) {
+    if (B <= 0 || R <= 0 || K <= 0 || R % 32 || K % 16)
+        return fjsp_internal_fail("fjsp_a2c_pack_mfma: need B > 0, R a multiple of 32, K a multiple of 16");
+    if (!W || !out) return fjsp_internal_fail("fjsp_a2c_pack_mfma: null buffer");
+    if ((uintptr_t)out & 7u) return fjsp_internal_fail("fjsp_a2c_pack_mfma: out must be 8-byte aligned");
+    const int64_t total = (int64_t)B * (R / 32) * (K / 16) * 128;
+    hipLaunchKernelGGL(k_pack_mfma, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, W, B, R, K,
+                       transposed, reinterpret_cast<__bf16*>(out));
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

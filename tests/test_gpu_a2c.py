@@ -593,6 +593,22 @@ def test_record_head_kernel_matches_torch(M, k):
     assert float(d.abs().max()) <= 1e-4 * float(pu.grad[:k][ok[:k]].abs().max()), float(d.abs().max())
 
 
+def test_pack_mfma_kernel_equals_torch(M):
+    """fjsp_a2c_pack_mfma (the weights' split-bf16 operand packing, one launch per matrix) equals
+    the torch formulation bit for bit: stacked actor layers, the critic's layers, and the
+    transposed views the backward packs."""
+    A = M["A"]
+    g = torch.Generator(device="cuda").manual_seed(2)
+    cases = [torch.randn(8, 256, 16, device="cuda", generator=g), torch.randn(8, 256, 256, device="cuda", generator=g),
+             torch.randn(256, 48, device="cuda", generator=g) * 1e-3, torch.randn(128, 256, device="cuda", generator=g)]
+    cases += [torch.randn(128, 256, device="cuda", generator=g).t(), torch.randn(256, 256, device="cuda", generator=g).t()]
+    for W in cases:
+        got = A.pack_mfma(W)
+        want = A.pack_mfma_torch(W)
+        assert got.shape == want.shape
+        assert torch.equal(got.view(torch.int32), want.view(torch.int32)), tuple(W.shape)
+
+
 def test_critic_onepass_matches_float64(M):
     """The one-pass critic (a2c_vec._CriticOnePass: fjsp_a2c_critic_fused's forward, value
     gradient from the per-state loss coefficients, value-head and hidden-layer backward in one
