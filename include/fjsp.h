@@ -308,6 +308,14 @@ int fjsp_a2c_critic_forward(const float* x, int32_t n, const float* critic_w, fl
  * cleared) where a mask byte is neither 0 nor 1.  Stream-ordered. */
 int fjsp_a2c_shard_keys(const uint64_t* keys, const int8_t* masks, const uint8_t* actions, int32_t T, int32_t n,
                         uint64_t* tk, int32_t* info, int32_t* bad, void* stream);
+/* The grouped update's batch statistics from the GAE outputs ret / adv f64 [T][8][N] in one pass
+ * (ABI 9): rsum / rsq f64 [T][N] = per sample the sums over the 8 agents of the f32-rounded
+ * return and of its square (calc_critic_loss's FloatTensor(returns), a2c.py:713-722), part f64
+ * [T][ceil(N / 256)][8][2] = per-workgroup sums of the f32-rounded advantage and of its square
+ * per agent (calc_actor_loss's normalisation, a2c.py:724-731).  Either input may be NULL (its
+ * outputs are then not written).  Stream-ordered. */
+int fjsp_a2c_slab_stats(const double* ret, const double* adv, int32_t T, int32_t N, double* rsum, double* rsq,
+                        double* part, void* stream);
 /* Weights into the policy / critic kernels' operand layout (a2c_vec.pack_mfma; ABI 9): W f32
  * [B][R][K] (transposed = 1: a [B][K][R] source packed as its transpose) -> out [B][R/32][K/16]
  * [3][64][8] bf16 (as floats: [.., 3, 64, 4]), element (b, t, kb, p, l, j) = plane p of the

@@ -244,6 +244,24 @@ class _CriticOnePass(torch.autograd.Function):
         return (None, None) + tuple(g * gl for g in ctx.grads)
 
 
+def slab_stats(ret=None, adv=None):
+    """fjsp_a2c_slab_stats over the GAE outputs f64 [T, 8, N] (GPU): (rs f64 [2, T*N] = per sample the
+    sums over the agents of the f32-rounded return and of its square, or None; sums f64 [8, 2] = per
+    agent the sums of the f32-rounded advantage and of its square, or None)."""
+    x = ret if ret is not None else adv
+    T, _, N = x.shape
+    dev = x.device
+    V = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    rs = torch.empty(2, T * N, dtype=torch.float64, device=dev) if ret is not None else None
+    part = torch.empty(T, -(-N // 256), NA, 2, dtype=torch.float64, device=dev) if adv is not None else None
+    r = None if ret is None else ret.contiguous()
+    a = None if adv is None else adv.contiguous()
+    nat.check(nat.lib().fjsp_a2c_slab_stats(V(r), V(a), T, N, None if rs is None else V(rs[0]),
+                                            None if rs is None else V(rs[1]), V(part),
+                                            ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    return rs, None if part is None else part.sum(dim=(0, 1))
+
+
 def critic_coef(g, r3, count):
     """Per distinct global state u of the (device) RowGroups g (one row: the critic's grouping of
     the batch's S = T * n samples) the coefficients of its share of calc_critic_loss
@@ -251,9 +269,12 @@ def critic_coef(g, r3, count):
     a/2 V^2 + b V + c, a = 2 n_u / count, b = -2 sum R / (8 count), c = sum R^2 / (8 count), R the
     f32 returns (r3 f64 [T, 8, n]) summed in f64 in sorted order -> f64 [Umax, 3]."""
     from .shard_learner import _counts, _group_sums
-    r32 = r3.float().double()
-    S = r32.shape[0] * r32.shape[2]
-    rs = torch.stack([r32.sum(1).reshape(S), (r32 * r32).sum(1).reshape(S)])              # [2, S]
+    if r3.is_cuda:
+        rs, _ = slab_stats(ret=r3)                                                        # [2, S]
+    else:
+        r32 = r3.float().double()
+        S = r32.shape[0] * r32.shape[2]
+        rs = torch.stack([r32.sum(1).reshape(S), (r32 * r32).sum(1).reshape(S)])
     sums = _group_sums(g.perm, g.ends, rs)                                                # [2, Umax]
     return critic_coef_sums(_counts(g.ends)[0].double(), sums[0], sums[1], count)
 

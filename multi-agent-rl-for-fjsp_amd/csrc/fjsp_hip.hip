@@ -2361,6 +2361,64 @@ int fjsp_gae_f64(const double* rewards, const double* values, const uint8_t* don
     return 0;
 }
 
+// The batch statistics the grouped update reads from the GAE outputs (f64 [T][8][N]), in one
+// pass: per sample (t, e) the f64 sums over the 8 agents of the f32-rounded return and of its
+// square (the critic loss's coefficients, a2c_vec.critic_coef; calc_critic_loss uses
+// FloatTensor(returns), a2c.py:713-722), and per agent the f64 sums of the f32-rounded advantage
+// and of its square (calc_actor_loss's normalisation, a2c.py:724-731), as per-workgroup partials
+// part[t][block][8][2] summed by the caller in a fixed order.  ret / adv may be null (that half
+// skipped).
+__global__ void __launch_bounds__(256) k_slab_stats(const double* __restrict__ ret, const double* __restrict__ adv,
+                                                    int T, int N, double* __restrict__ rsum, double* __restrict__ rsq,
+                                                    double* __restrict__ part) {
+    const int t = blockIdx.y;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    const bool in = e < N;
+    if (ret) {
+        double s = 0.0, q = 0.0;
+        if (in) {
+#pragma unroll
+            for (int a = 0; a < NA; a++) {
+                const double r = (double)(float)ret[((size_t)t * NA + a) * N + e];
+                s += r;
+                q += r * r;
+            }
+            rsum[(size_t)t * N + e] = s;
+            rsq[(size_t)t * N + e] = q;
+        }
+    }
+    if (adv) {
+        __shared__ double s_p[4][NA][2];
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+            double x = in ? (double)(float)adv[((size_t)t * NA + a) * N + e] : 0.0;
+            double x2 = x * x;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                x += __shfl_xor(x, o);
+                x2 += __shfl_xor(x2, o);
+            }
+            if (lane == 0) { s_p[w][a][0] = x; s_p[w][a][1] = x2; }
+        }
+        __syncthreads();
+        if (threadIdx.x < NA * 2) {
+            const int a = threadIdx.x >> 1, c = threadIdx.x & 1;
+            part[(((size_t)t * gridDim.x + blockIdx.x) * NA + a) * 2 + c] = s_p[0][a][c] + s_p[1][a][c] + s_p[2][a][c] + s_p[3][a][c];
+        }
+    }
+}
+
+int fjsp_a2c_slab_stats(const double* ret, const double* adv, int32_t T, int32_t N, double* rsum, double* rsq,
+                        double* part, void* stream) {
+    if (T <= 0 || N <= 0) return fail("fjsp_a2c_slab_stats: T and N must be > 0");
+    if ((!ret && !adv) || (ret && (!rsum || !rsq)) || (adv && !part)) return fail("fjsp_a2c_slab_stats: null buffer");
+    hipLaunchKernelGGL(k_slab_stats, dim3((unsigned)((N + 255) / 256), (unsigned)T), dim3(256), 0, (hipStream_t)stream, ret,
+                       adv, T, N, rsum, rsq, part);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 int fjsp_gae_shared(const double* rewards, const float* values, const uint8_t* done, int32_t T, int32_t N,
                     int32_t agents, double gamma, double lamb, double* ret, double* adv, void* stream) {
     if (T <= 0 || N <= 0 || agents <= 0 || (int64_t)agents * N > INT32_MAX)

@@ -120,9 +120,14 @@ def adv_stats_slab(adv, group=None):
     T, A, N = adv.shape
     if not active(group) and (not adv.is_cuda or T * N < 65536):
         return adv_stats(adv.float().permute(1, 0, 2).reshape(A, T * N), group)
-    x = adv.float().double()
-    s = torch.stack([x.sum(dim=(0, 2)), (x * x).sum(dim=(0, 2)),
-                     torch.full((A,), float(T * N), dtype=torch.float64, device=adv.device)], dim=1)
+    if adv.is_cuda and A == 8:
+        from .a2c_vec import slab_stats
+        _, sums = slab_stats(adv=adv)                                                     # one pass
+        s = torch.cat([sums, torch.full((A, 1), float(T * N), dtype=torch.float64, device=adv.device)], dim=1)
+    else:
+        x = adv.float().double()
+        s = torch.stack([x.sum(dim=(0, 2)), (x * x).sum(dim=(0, 2)),
+                         torch.full((A,), float(T * N), dtype=torch.float64, device=adv.device)], dim=1)
     if active(group):
         dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
     n = s[0, 2]

@@ -609,6 +609,24 @@ def test_pack_mfma_kernel_equals_torch(M):
         assert torch.equal(got.view(torch.int32), want.view(torch.int32)), tuple(W.shape)
 
 
+def test_slab_stats_kernel_matches_torch(M):
+    """fjsp_a2c_slab_stats: per-sample sums over the agents of the f32-rounded returns and their
+    squares, per-agent sums of the f32-rounded advantages and their squares, against torch f64
+    sums of the same values (1e-12 relative: only the f64 summation order differs); partial tiles."""
+    A = M["A"]
+    g = torch.Generator(device="cuda").manual_seed(6)
+    T, N = 37, 1000
+    ret = torch.randn(T, 8, N, device="cuda", dtype=torch.float64, generator=g) * 30
+    adv = torch.randn(T, 8, N, device="cuda", dtype=torch.float64, generator=g) * 3
+    rs, sums = A.slab_stats(ret, adv)
+    r32 = ret.float().double()
+    assert torch.allclose(rs[0], r32.sum(1).reshape(-1), rtol=1e-12, atol=1e-9)
+    assert torch.allclose(rs[1], (r32 * r32).sum(1).reshape(-1), rtol=1e-12, atol=1e-9)
+    a32 = adv.float().double()
+    want = torch.stack([a32.sum(dim=(0, 2)), (a32 * a32).sum(dim=(0, 2))], dim=1)
+    assert torch.allclose(sums, want, rtol=1e-12, atol=1e-9)
+
+
 def test_critic_onepass_matches_float64(M):
     """The one-pass critic (a2c_vec._CriticOnePass: fjsp_a2c_critic_fused's forward, value
     gradient from the per-state loss coefficients, value-head and hidden-layer backward in one
