@@ -98,6 +98,38 @@ class _LinearSplitK(torch.autograd.Function):
         return gx, gW, gy.sum(0) if gb is None else gb, None
 
 
+def wgrad_mfma(gy, x, nx=None):
+    """gy^T x[:, :nx] (a critic layer's weight gradient over a long batch of sample-major rows) on
+    the matrix cores with split-bf16 products (fjsp_a2c_wgrad), or None when the shape is not one
+    of the kernel's: gy f32 [U, M] (M = 256 or 128), x f32 [U, ld] contiguous rows, nx = 256
+    (M = 128 or 256) or <= 64 (M = 256).  Per-workgroup partial sums, added in a fixed order."""
+    U, M = gy.shape
+    nx = x.shape[1] if nx is None else nx
+    if not (wgrad_mfma_on and gy.is_cuda and gy.is_contiguous() and x.is_contiguous() and U >= 4096
+            and ((M == 256 and (nx == 256 or nx <= 64)) or (M == 128 and nx == 256))):
+        return None
+    N = 256 if nx == 256 else 64
+    nwg = min(256, -(-U // 1024))
+    part = torch.empty(nwg, M, N, dtype=torch.float32, device=gy.device)
+    V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    nat.check(nat.lib().fjsp_a2c_wgrad(V(gy), M, M, V(x), x.shape[1], nx, U, nwg, V(part),
+                                       ctypes.c_void_p(torch.cuda.current_stream(gy.device).cuda_stream)))
+    out = part.sum(0)
+    return out if nx == N else out[:, :nx].contiguous()
+
+
+wgrad_mfma_on = os.environ.get("FJSP_WGRAD_MFMA", "1") != "0"
+
+
+def _critic_wgrad(gy, x, nx=None):
+    """A critic layer's weight gradient: the matrix-core kernel where its shape fits, else the
+    split-K GEMM."""
+    w = wgrad_mfma(gy, x, nx)
+    if w is not None:
+        return w
+    return _splitk_wgrad(gy, x if nx is None else x[:, :nx])
+
+
 def _splitk_wgrad(gy, x):
     """gy^T x over a long batch B: c chunks of B // c rows as strided views (no padded copies)
     in one batched GEMM, summed; the B - c * (B // c) tail apart."""
@@ -235,8 +267,8 @@ class _CriticOnePass(torch.autograd.Function):
                                                   V(g1), V(part), V(loss), None,
                                                   ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
         ps = part.sum(0)
-        ctx.grads = (_splitk_wgrad(g1, x[:, :GLOBAL_DIM]), ps[:256], _splitk_wgrad(g2, h1), ps[256:512],
-                     _splitk_wgrad(g3, h2), ps[512:640], ps[640:768].view(1, 128), ps[768:769])
+        ctx.grads = (_critic_wgrad(g1, x, GLOBAL_DIM), ps[:256], _critic_wgrad(g2, h1), ps[256:512],
+                     _critic_wgrad(g3, h2), ps[512:640], ps[640:768].view(1, 128), ps[768:769])
         return loss.sum().float()
 
     @staticmethod
