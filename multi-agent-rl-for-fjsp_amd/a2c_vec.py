@@ -90,7 +90,7 @@ class _LinearSplitK(torch.autograd.Function):
             gy, gb = _relu_bias_grad(gy.contiguous(), y)            # one pass (HIP kernel)
         elif ctx.relu:
             gy = torch.ops.aten.threshold_backward(gy, y, 0.0)      # relu' from the output
-        gW = _splitk_wgrad(gy, x)
+        gW = _critic_wgrad(gy, x)                                   # matrix-core kernel where it fits
         gx = None
         if ctx.needs_input_grad[0]:
             # one output (the value head): an outer product, elementwise (a K = 1 GEMM is slow)
