@@ -90,3 +90,25 @@ def test_critic_fused_validates_arguments_without_gpu():
     bad = list(args)
     bad[0] = P((1 << 20) + 4)
     assert L.fjsp_a2c_critic_fused(*bad) != 0 and b"16-byte aligned" in L.fjsp_last_error()
+
+
+def test_update_kernels_validate_arguments_without_gpu():
+    """The ABI-9 update entries (record head, weight packing, slab statistics, weight gradients,
+    combiner keys) reject bad shapes and null buffers before launching."""
+    L = G.native.lib()
+    P = ctypes.c_void_p
+    a = P(1 << 20)
+    assert L.fjsp_a2c_record_head(a, 8, a, 0, 3, a, a, a, 1.0, 0.01, a, a, None) != 0
+    assert L.fjsp_a2c_record_head(a, 8, a, 10, 9, a, a, a, 1.0, 0.01, a, a, None) != 0
+    assert L.fjsp_a2c_record_head(a, 8, None, 10, 3, a, a, a, 1.0, 0.01, a, a, None) != 0
+    assert L.fjsp_a2c_pack_mfma(a, 1, 48, 16, 0, a, None) != 0 and b"multiple of 32" in L.fjsp_last_error()
+    assert L.fjsp_a2c_pack_mfma(a, 1, 64, 20, 0, a, None) != 0
+    assert L.fjsp_a2c_pack_mfma(a, 1, 64, 16, 0, P((1 << 20) + 4), None) != 0
+    assert L.fjsp_a2c_slab_stats(None, None, 4, 4, a, a, a, None) != 0
+    assert L.fjsp_a2c_slab_stats(a, None, 4, 4, None, a, None, None) != 0
+    assert L.fjsp_a2c_slab_stats(a, a, 0, 4, a, a, a, None) != 0
+    assert L.fjsp_a2c_wgrad(a, 256, 256, a, 256, 100, 1000, 8, a, None) != 0 and b"shapes" in L.fjsp_last_error()
+    assert L.fjsp_a2c_wgrad(a, 128, 256, a, 256, 256, 1000, 8, a, None) != 0      # ldg < M
+    assert L.fjsp_a2c_wgrad(a, 256, 256, None, 256, 256, 1000, 8, a, None) != 0
+    assert L.fjsp_a2c_shard_keys(a, a, a, 0, 4, a, a, a, None) != 0
+    assert L.fjsp_a2c_shard_keys(a, None, a, 4, 4, a, a, a, None) != 0
