@@ -236,7 +236,7 @@ def _shard_worker(rank, world, port, out_dir, collide=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_shard_exchange_equals_single_learner(tmp_path, world):
     """exchange="shard": each rank combines its samples into (input, mask, action) / global-state
     records, one all_to_all routes them to the rank owning the network (actor a on rank a mod
