@@ -252,28 +252,47 @@ class _CriticOnePass(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, coef, W1, b1, W2, b2, W3, b3, W4, b4):
-        U = x.shape[0]
-        dev = x.device
-        cw = pack_critic_weights(W1, b1, W2, b2, W3, b3, W4, b4)
-        w3t, w2t = pack_mfma(W3.detach().t()).reshape(-1), pack_mfma(W2.detach().t()).reshape(-1)
-        E = lambda *sh: torch.empty(*sh, dtype=torch.float32, device=dev)  # noqa: E731
-        h1, h2, g2, g1, g3 = E(U, 256), E(U, 256), E(U, 256), E(U, 256), E(U, 128)
-        tiles = -(-U // 32)
-        part = E(tiles, nat.CRITIC_FUSED_PW)
-        loss = torch.empty(tiles, dtype=torch.float64, device=dev)
-        V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-        c = coef.contiguous()
-        nat.check(nat.lib().fjsp_a2c_critic_fused(V(x), U, V(cw), V(w3t), V(w2t), V(c), V(h1), V(h2), V(g3), V(g2),
-                                                  V(g1), V(part), V(loss), None,
-                                                  ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
-        ps = part.sum(0)
-        ctx.grads = (_critic_wgrad(g1, x, GLOBAL_DIM), ps[:256], _critic_wgrad(g2, h1), ps[256:512],
-                     _critic_wgrad(g3, h2), ps[512:640], ps[640:768].view(1, 128), ps[768:769])
-        return loss.sum().float()
+        loss, ctx.grads = critic_onepass_compute(x, coef, W1, b1, W2, b2, W3, b3, W4, b4)
+        return loss
 
     @staticmethod
     def backward(ctx, gl):
         return (None, None) + tuple(g * gl for g in ctx.grads)
+
+
+@torch.no_grad()
+def critic_onepass_compute(x, coef, W1, b1, W2, b2, W3, b3, W4, b4):
+    """_CriticOnePass's work on the current stream: (the critic loss 0-d f32, the gradients of
+    W1, b1, W2, b2, W3, b3, W4, b4)."""
+    U = x.shape[0]
+    dev = x.device
+    cw = pack_critic_weights(W1, b1, W2, b2, W3, b3, W4, b4)
+    w3t, w2t = pack_mfma(W3.detach().t()).reshape(-1), pack_mfma(W2.detach().t()).reshape(-1)
+    E = lambda *sh: torch.empty(*sh, dtype=torch.float32, device=dev)  # noqa: E731
+    h1, h2, g2, g1, g3 = E(U, 256), E(U, 256), E(U, 256), E(U, 256), E(U, 128)
+    tiles = -(-U // 32)
+    part = E(tiles, nat.CRITIC_FUSED_PW)
+    loss = torch.empty(tiles, dtype=torch.float64, device=dev)
+    V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    c = coef.contiguous()
+    nat.check(nat.lib().fjsp_a2c_critic_fused(V(x), U, V(cw), V(w3t), V(w2t), V(c), V(h1), V(h2), V(g3), V(g2),
+                                              V(g1), V(part), V(loss), None,
+                                              ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    ps = part.sum(0)
+    grads = (_critic_wgrad(g1, x, GLOBAL_DIM), ps[:256], _critic_wgrad(g2, h1), ps[256:512],
+             _critic_wgrad(g3, h2), ps[512:640], ps[640:768].view(1, 128), ps[768:769])
+    return loss.sum().float(), grads
+
+
+_SIDE = {}
+
+
+def _side_stream(device):
+    """A second stream per device (the update's critic beside its actors)."""
+    device = torch.device(device)
+    if device not in _SIDE:
+        _SIDE[device] = torch.cuda.Stream(device)
+    return _SIDE[device]
 
 
 def slab_stats(ret=None, adv=None):
@@ -332,6 +351,9 @@ critic_fused = os.environ.get("FJSP_CRITIC_FUSED", "1") != "0"
 # FJSP_CRITIC_ONEPASS=0: the forward kernel, the per-sample loss through autograd, the value head
 # and backward kernels)
 critic_onepass_on = os.environ.get("FJSP_CRITIC_ONEPASS", "1") != "0"
+# ... on a second stream beside the actors' forward / loss head / backward (FJSP_UPDATE_OVERLAP=0:
+# one stream)
+update_overlap_on = os.environ.get("FJSP_UPDATE_OVERLAP", "1") != "0"
 # its backward through the two 256-wide layers in one kernel (FJSP_CRITIC_BWD=0: GEMMs + ReLU kernels)
 critic_bwd_fused = os.environ.get("FJSP_CRITIC_BWD", "1") != "0"
 
@@ -993,7 +1015,22 @@ class A2CLosses:
         # the critic first: its GEMMs keep the GPU busy while the host issues the actors' many
         # small launches (after the grouping's host synchronisations the queue is empty)
         critic_loss = None
-        if gc is not None and feats.is_cuda and critic_fused and critic_onepass_on and gc.gsorted is not None:
+        side = None
+        if (gc is not None and feats.is_cuda and critic_fused and critic_onepass_on and gc.gsorted is not None
+                and update_overlap_on):
+            # the critic's loss and gradients on a second stream while the actors run on this one
+            # (independent until the optimiser step; the critic's parameters get their gradients
+            # directly, its loss is returned detached)
+            cur = torch.cuda.current_stream(f3.device)
+            side = _side_stream(f3.device)
+            side.wait_stream(cur)
+            n_ = critic.net
+            with torch.cuda.stream(side):
+                c_loss, c_grads = critic_onepass_compute(rows.index_select(0, gc.first[0]), critic_coef(gc, r3, count),
+                                                         n_[0].weight, n_[0].bias, n_[2].weight, n_[2].bias,
+                                                         n_[4].weight, n_[4].bias, n_[6].weight, n_[6].bias)
+            v = None
+        elif gc is not None and feats.is_cuda and critic_fused and critic_onepass_on and gc.gsorted is not None:
             critic_loss = critic_onepass(critic, rows.index_select(0, gc.first[0]), critic_coef(gc, r3, count))
             v = None
         elif gc is not None and feats.is_cuda and gc.first.shape[1] >= 65536 and critic_fused:
@@ -1026,7 +1063,17 @@ class A2CLosses:
             pm = masked_probs(probs, agent_masks(masks, midx))
             logp = categorical_log_prob(pm, acts)                    # [8, S]
             actor_losses = -(adv_n * logp).sum(dim=1) / count - entropy_coef * ent.sum(dim=1) / count
-        if critic_loss is None:
+        if side is not None:
+            cur.wait_stream(side)
+            for p, g in zip(critic.parameters(), c_grads):
+                g.record_stream(cur)               # allocated on the side stream, used on this one
+                if p.grad is None:
+                    p.grad = g
+                else:
+                    p.grad.add_(g)
+            c_loss.record_stream(cur)
+            critic_loss = c_loss
+        elif critic_loss is None:
             critic_loss = ((v.view(T, 1, n) - r3.float()) ** 2).sum() / (NA * count)
         return actor_losses, critic_loss
 
