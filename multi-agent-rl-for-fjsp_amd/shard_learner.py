@@ -193,8 +193,11 @@ def combine(feats, masks, actions, ret, adv, mean, std, world):
     adv32 = adv.float().permute(1, 0, 2).reshape(NA, S)
     advn = (adv32 - mean[:, None]) / (std[:, None] + 1e-8) if mean is not None else adv32
     sadv = _group_sums(g.perm[:NA], g.ends[:NA], advn.double())                          # [8, Umax]
-    r32 = ret.float().double()                                                           # [T, 8, n]
-    rs = torch.stack([r32.sum(1).reshape(S), (r32 * r32).sum(1).reshape(S)])             # [2, S]
+    if ret.is_cuda:
+        rs, _ = A.slab_stats(ret=ret)                                                     # [2, S], one pass
+    else:
+        r32 = ret.float().double()                                                       # [T, 8, n]
+        rs = torch.stack([r32.sum(1).reshape(S), (r32 * r32).sum(1).reshape(S)])
     cs = _group_sums(g.perm[NA:], g.ends[NA:], rs)                                       # [2, Umax]
     cnt = _counts(g.ends).to(torch.int32)                                                # [9, Umax]
 
