@@ -316,14 +316,6 @@ int fjsp_a2c_shard_keys(const uint64_t* keys, const int8_t* masks, const uint8_t
  * outputs are then not written).  Stream-ordered. */
 int fjsp_a2c_slab_stats(const double* ret, const double* adv, int32_t T, int32_t N, double* rsum, double* rsq,
                         double* part, void* stream);
-/* A critic layer's weight gradient over a long batch on the matrix cores (a2c_vec.wgrad_mfma; the
- * split-K GEMMs gW = G^T X of _update's critic backward, a2c.py:683-699; ABI 9): part f32
- * [nwg][M][N] = per-workgroup partial sums over contiguous sample runs of G[u][m] X[u][n], G f32
- * [U][ldg] (M columns used), X f32 [U][ldx] (nx columns used; N = 256 for nx = 256, 64 for
- * nx <= 64, columns >= nx zero), f32 products as three bf16 planes.  (M, nx) = (256, 256),
- * (128, 256) or (256, <= 64).  Stream-ordered. */
-int fjsp_a2c_wgrad(const float* G, int32_t ldg, int32_t M, const float* X, int32_t ldx, int32_t nx, int32_t U,
-                   int32_t nwg, float* part, void* stream);
 /* Weights into the policy / critic kernels' operand layout (a2c_vec.pack_mfma; ABI 9): W f32
  * [B][R][K] (transposed = 1: a [B][K][R] source packed as its transpose) -> out [B][R/32][K/16]
  * [3][64][8] bf16 (as floats: [.., 3, 64, 4]), element (b, t, kb, p, l, j) = plane p of the

@@ -90,7 +90,7 @@ class _LinearSplitK(torch.autograd.Function):
             gy, gb = _relu_bias_grad(gy.contiguous(), y)            # one pass (HIP kernel)
         elif ctx.relu:
             gy = torch.ops.aten.threshold_backward(gy, y, 0.0)      # relu' from the output
-        gW = _critic_wgrad(gy, x)                                   # matrix-core kernel where it fits
+        gW = _splitk_wgrad(gy, x)
         gx = None
         if ctx.needs_input_grad[0]:
             # one output (the value head): an outer product, elementwise (a K = 1 GEMM is slow)
@@ -98,35 +98,8 @@ class _LinearSplitK(torch.autograd.Function):
         return gx, gW, gy.sum(0) if gb is None else gb, None
 
 
-def wgrad_mfma(gy, x, nx=None):
-    """gy^T x[:, :nx] (a critic layer's weight gradient over a long batch of sample-major rows) on
-    the matrix cores with split-bf16 products (fjsp_a2c_wgrad), or None when the shape is not one
-    of the kernel's: gy f32 [U, M] (M = 256 or 128), x f32 [U, ld] contiguous rows, nx = 256
-    (M = 128 or 256) or <= 64 (M = 256).  Per-workgroup partial sums, added in a fixed order."""
-    U, M = gy.shape
-    nx = x.shape[1] if nx is None else nx
-    if not (wgrad_mfma_on and gy.is_cuda and gy.is_contiguous() and x.is_contiguous() and U >= 4096
-            and ((M == 256 and (nx == 256 or nx <= 64)) or (M == 128 and nx == 256))):
-        return None
-    N = 256 if nx == 256 else 64
-    nwg = min(256, -(-U // 1024))
-    part = torch.empty(nwg, M, N, dtype=torch.float32, device=gy.device)
-    V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    nat.check(nat.lib().fjsp_a2c_wgrad(V(gy), M, M, V(x), x.shape[1], nx, U, nwg, V(part),
-                                       ctypes.c_void_p(torch.cuda.current_stream(gy.device).cuda_stream)))
-    out = part.sum(0)
-    return out if nx == N else out[:, :nx].contiguous()
-
-
-wgrad_mfma_on = os.environ.get("FJSP_WGRAD_MFMA", "1") != "0"
-
-
 def _critic_wgrad(gy, x, nx=None):
-    """A critic layer's weight gradient: the matrix-core kernel where its shape fits, else the
-    split-K GEMM."""
-    w = wgrad_mfma(gy, x, nx)
-    if w is not None:
-        return w
+    """A critic layer's weight gradient gy^T x[:, :nx] (split-K GEMM)."""
     return _splitk_wgrad(gy, x if nx is None else x[:, :nx])
 
 
@@ -284,17 +257,6 @@ def critic_onepass_compute(x, coef, W1, b1, W2, b2, W3, b3, W4, b4):
     return loss.sum().float(), grads
 
 
-_SIDE = {}
-
-
-def _side_stream(device):
-    """A second stream per device (the update's critic beside its actors)."""
-    device = torch.device(device)
-    if device not in _SIDE:
-        _SIDE[device] = torch.cuda.Stream(device)
-    return _SIDE[device]
-
-
 def slab_stats(ret=None, adv=None):
     """fjsp_a2c_slab_stats over the GAE outputs f64 [T, 8, N] (GPU): (rs f64 [2, T*N] = per sample the
     sums over the agents of the f32-rounded return and of its square, or None; sums f64 [8, 2] = per
@@ -351,9 +313,7 @@ critic_fused = os.environ.get("FJSP_CRITIC_FUSED", "1") != "0"
 # FJSP_CRITIC_ONEPASS=0: the forward kernel, the per-sample loss through autograd, the value head
 # and backward kernels)
 critic_onepass_on = os.environ.get("FJSP_CRITIC_ONEPASS", "1") != "0"
-# ... on a second stream beside the actors' forward / loss head / backward (FJSP_UPDATE_OVERLAP=0:
-# one stream)
-update_overlap_on = os.environ.get("FJSP_UPDATE_OVERLAP", "1") != "0"
+
 # its backward through the two 256-wide layers in one kernel (FJSP_CRITIC_BWD=0: GEMMs + ReLU kernels)
 critic_bwd_fused = os.environ.get("FJSP_CRITIC_BWD", "1") != "0"
 
@@ -1015,22 +975,7 @@ class A2CLosses:
         # the critic first: its GEMMs keep the GPU busy while the host issues the actors' many
         # small launches (after the grouping's host synchronisations the queue is empty)
         critic_loss = None
-        side = None
-        if (gc is not None and feats.is_cuda and critic_fused and critic_onepass_on and gc.gsorted is not None
-                and update_overlap_on):
-            # the critic's loss and gradients on a second stream while the actors run on this one
-            # (independent until the optimiser step; the critic's parameters get their gradients
-            # directly, its loss is returned detached)
-            cur = torch.cuda.current_stream(f3.device)
-            side = _side_stream(f3.device)
-            side.wait_stream(cur)
-            n_ = critic.net
-            with torch.cuda.stream(side):
-                c_loss, c_grads = critic_onepass_compute(rows.index_select(0, gc.first[0]), critic_coef(gc, r3, count),
-                                                         n_[0].weight, n_[0].bias, n_[2].weight, n_[2].bias,
-                                                         n_[4].weight, n_[4].bias, n_[6].weight, n_[6].bias)
-            v = None
-        elif gc is not None and feats.is_cuda and critic_fused and critic_onepass_on and gc.gsorted is not None:
+        if gc is not None and feats.is_cuda and critic_fused and critic_onepass_on and gc.gsorted is not None:
             critic_loss = critic_onepass(critic, rows.index_select(0, gc.first[0]), critic_coef(gc, r3, count))
             v = None
         elif gc is not None and feats.is_cuda and gc.first.shape[1] >= 65536 and critic_fused:
@@ -1063,17 +1008,7 @@ class A2CLosses:
             pm = masked_probs(probs, agent_masks(masks, midx))
             logp = categorical_log_prob(pm, acts)                    # [8, S]
             actor_losses = -(adv_n * logp).sum(dim=1) / count - entropy_coef * ent.sum(dim=1) / count
-        if side is not None:
-            cur.wait_stream(side)
-            for p, g in zip(critic.parameters(), c_grads):
-                g.record_stream(cur)               # allocated on the side stream, used on this one
-                if p.grad is None:
-                    p.grad = g
-                else:
-                    p.grad.add_(g)
-            c_loss.record_stream(cur)
-            critic_loss = c_loss
-        elif critic_loss is None:
+        if critic_loss is None:
             critic_loss = ((v.view(T, 1, n) - r3.float()) ** 2).sum() / (NA * count)
         return actor_losses, critic_loss
 

@@ -1104,130 +1104,6 @@ __global__ void __launch_bounds__(256) k_group_keys(const float* __restrict__ fe
     }
 }
 
-// Weight gradients of the grouped update's critic on the matrix cores (fjsp_a2c_wgrad; the split-K
-// GEMMs gW = G^T X of a2c_vec._splitk_wgrad): C[m][n] = sum over samples u of G[u][m] X[u][n] for
-// sample-major f32 operands (G = a layer's pre-activation gradient [U][M], X = its input [U][ldx],
-// nx <= N columns used), f32 products as three bf16 planes (the policy kernel's split arithmetic,
-// six products per 16-deep block).  Workgroup b sums a contiguous run of samples into partial
-// sums part[b][M][N] (summed afterwards in a fixed order).  Per 16-sample step every thread loads
-// the 8 samples of one column of one operand (coalesced across lanes), splits them and writes
-// them as one 16-byte run of k into LDS images [plane][column][k] (double-buffered, one barrier
-// per step), which are exactly the A (G^T: row m, k = sample) and B (X: k = sample, column n)
-// operand runs of v_mfma_f32_32x32x16_bf16; the next step's loads are in flight under the MFMAs.
-// Each wave owns WM x WN output tiles of 32 x 32 (its A fragments reused across WN tiles).
-constexpr int WG_KS = 24;   // bf16 per LDS column row: 16 samples + 8 pad (12-dword stride, conflict-free)
-template <int MT, int NT>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
-k_wgrad3(const float* __restrict__ G, int ldg, const float* __restrict__ X, int ldx, int nx, int U, int chunk,
-         float* __restrict__ part) {
-    constexpr int M = 32 * MT, N = 32 * NT;
-    constexpr int WN = NT >= 4 ? 4 : NT;
-    constexpr int WM = MT * NT / 8 / WN;
-    static_assert(WM * WN * 8 == MT * NT && WM >= 1, "tiles per wave");
-    constexpr int NGRP = NT / WN;
-    constexpr int GROUPS = 2 * (M + N);            // (operand, column, k half) staging groups
-    constexpr int GPT = (GROUPS + 511) / 512;      // per thread
-    constexpr int PA = M * WG_KS, PB = N * WG_KS;  // plane sizes (bf16)
-    __shared__ __attribute__((aligned(16))) __bf16 sA[2][NP * PA];
-    __shared__ __attribute__((aligned(16))) __bf16 sB[2][NP * PB];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int mg = wave / NGRP, ng = wave % NGRP;
-    const int u_begin = blockIdx.x * chunk;
-    const int u_end = min(U, u_begin + chunk);
-    f32x16 acc[WM][WN];
-#pragma unroll
-    for (int i = 0; i < WM; i++)
-#pragma unroll
-        for (int j = 0; j < WN; j++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.0f;
-    float st[GPT][8];
-    auto load = [&](int u0) __attribute__((always_inline)) {
-#pragma unroll
-        for (int q = 0; q < GPT; q++) {
-            const int gi = tid + 512 * q;
-            const bool isA = gi < 2 * M;
-            const int gg = isA ? gi : gi - 2 * M;
-            const int cols = isA ? M : N;
-            const int c = gg % cols, kh = gg / cols;
-            const bool ok = gi < GROUPS && (isA || c < nx);
-            const float* base = isA ? G + c : X + c;
-            const int ld = isA ? ldg : ldx;
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int u = u0 + 8 * kh + j;
-                st[q][j] = (ok && u < u_end) ? base[(size_t)u * ld] : 0.0f;
-            }
-        }
-    };
-    auto store = [&](int buf) __attribute__((always_inline)) {
-#pragma unroll
-        for (int q = 0; q < GPT; q++) {
-            const int gi = tid + 512 * q;
-            if (gi >= GROUPS) continue;
-            const bool isA = gi < 2 * M;
-            const int gg = isA ? gi : gi - 2 * M;
-            const int cols = isA ? M : N;
-            const int c = gg % cols, kh = gg / cols;
-            bf16x8 ph, pm, pl;
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                __bf16 x0, x1, x2;
-                split3(st[q][j], x0, x1, x2);
-                ph[j] = x0;
-                pm[j] = x1;
-                pl[j] = x2;
-            }
-            __bf16* d = (isA ? sA[buf] : sB[buf]) + c * WG_KS + 8 * kh;
-            const int PL = isA ? PA : PB;
-            *reinterpret_cast<bf16x8*>(d) = ph;
-            *reinterpret_cast<bf16x8*>(d + PL) = pm;
-            *reinterpret_cast<bf16x8*>(d + 2 * PL) = pl;
-        }
-    };
-    if (u_begin < u_end) {
-        load(u_begin);
-        store(0);
-    }
-    __syncthreads();
-    int buf = 0;
-    for (int u0 = u_begin; u0 < u_end; u0 += 16) {
-        const bool more = u0 + 16 < u_end;
-        if (more) load(u0 + 16);
-        const __bf16* a = sA[buf] + (lane & 31) * WG_KS + 8 * (lane >> 5);
-        const __bf16* b = sB[buf] + (lane & 31) * WG_KS + 8 * (lane >> 5);
-        bf16x8 fa[WM][NP];
-#pragma unroll
-        for (int i = 0; i < WM; i++)
-#pragma unroll
-            for (int p = 0; p < NP; p++)
-                fa[i][p] = *reinterpret_cast<const bf16x8*>(a + p * PA + 32 * (mg * WM + i) * WG_KS);
-#pragma unroll
-        for (int j = 0; j < WN; j++) {
-            bf16x8 fb[NP];
-#pragma unroll
-            for (int p = 0; p < NP; p++)
-                fb[p] = *reinterpret_cast<const bf16x8*>(b + p * PB + 32 * (ng * WN + j) * WG_KS);
-#pragma unroll
-            for (int i = 0; i < WM; i++) acc[i][j] = mfma6(fa[i], fb, acc[i][j]);
-        }
-        if (more) store(buf ^ 1);
-        __syncthreads();
-        buf ^= 1;
-    }
-    // partial sums: tile (m-tile, n-tile) of this wave, C/D layout -> part[b][m][n]
-    float* out = part + (size_t)blockIdx.x * M * N;
-#pragma unroll
-    for (int i = 0; i < WM; i++)
-#pragma unroll
-        for (int j = 0; j < WN; j++) {
-            const int m0 = 32 * (mg * WM + i), n = 32 * (ng * WN + j) + (lane & 31);
-#pragma unroll
-            for (int r = 0; r < 16; r++) out[(size_t)(m0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * N + n] = acc[i][j][r];
-        }
-}
-
 // Weights into the matrix cores' operand order (a2c_vec.pack_mfma, include/fjsp.h): W f32 [B][R][K]
 // (or, transposed, the K x R source [B][K][R] read as its transpose) -> [B][R/32][K/16][3][64][8]
 // bf16, element (b, t, kb, p, l, j) = plane p of split3(W[b][32 t + (l & 31)][16 kb + 8 (l >> 5)
@@ -1668,30 +1544,6 @@ extern "C" int fjsp_a2c_group_keys(const float* feats, int32_t T, int32_t n, uin
     if (rows && ((uintptr_t)rows & 15u)) return fjsp_internal_fail("fjsp_a2c_group_keys: rows must be 16-byte aligned");
     hipLaunchKernelGGL(k_group_keys, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, feats, T, n,
                        keys, rows);
-    const hipError_t err = hipGetLastError();
-    if (err != hipSuccess) {
-        fjsp_internal_fail(hipGetErrorString(err));
-        return -2;
-    }
-    return 0;
-}
-
-extern "C" int fjsp_a2c_wgrad(const float* G, int32_t ldg, int32_t M, const float* X, int32_t ldx, int32_t nx, int32_t U,
-                              int32_t nwg, float* part, void* stream) {
-    if (U <= 0 || nwg <= 0 || nx <= 0 || ldg < M || ldx < nx)
-        return fjsp_internal_fail("fjsp_a2c_wgrad: need U > 0, nwg > 0, 0 < nx <= ldx, M <= ldg");
-    if (!G || !X || !part) return fjsp_internal_fail("fjsp_a2c_wgrad: null buffer");
-    const int chunk = ((U + nwg - 1) / nwg + 15) / 16 * 16;
-    const dim3 grid((unsigned)nwg), blk(512);
-    const hipStream_t st = (hipStream_t)stream;
-    if (M == 256 && nx == 256)
-        hipLaunchKernelGGL((k_wgrad3<8, 8>), grid, blk, 0, st, G, ldg, X, ldx, nx, U, chunk, part);
-    else if (M == 128 && nx == 256)
-        hipLaunchKernelGGL((k_wgrad3<4, 8>), grid, blk, 0, st, G, ldg, X, ldx, nx, U, chunk, part);
-    else if (M == 256 && nx <= 64)
-        hipLaunchKernelGGL((k_wgrad3<8, 2>), grid, blk, 0, st, G, ldg, X, ldx, nx, U, chunk, part);
-    else
-        return fjsp_internal_fail("fjsp_a2c_wgrad: shapes (M, nx) must be (256, 256), (128, 256) or (256, <= 64)");
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

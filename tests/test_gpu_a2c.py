@@ -627,28 +627,6 @@ def test_slab_stats_kernel_matches_torch(M):
     assert torch.allclose(sums, want, rtol=1e-12, atol=1e-9)
 
 
-@pytest.mark.parametrize("M_, nx, U", [(256, 256, 70001), (128, 256, 70001), (256, 38, 70001), (256, 256, 4100)])
-def test_wgrad_kernel_matches_float64(M, M_, nx, U):
-    """fjsp_a2c_wgrad (the critic's weight gradients on the matrix cores, split-bf16 products)
-    against float64, beside torch's f32 GEMM: relative error at most max(3x the f32 GEMM's, 2e-6);
-    a sample count that is no multiple of the 16-sample steps, a 38-column input read from 40-wide
-    rows."""
-    A = M["A"]
-    g = torch.Generator(device="cuda").manual_seed(U + nx)
-    gy = torch.randn(U, M_, device="cuda", generator=g) * (torch.rand(U, M_, device="cuda", generator=g) > 0.4)
-    ld = 40 if nx == 38 else nx
-    x = torch.rand(U, ld, device="cuda", generator=g) * 5
-    if nx == 38:
-        x[:, 38:] = 0
-    got = A.wgrad_mfma(gy, x, nx)
-    assert got is not None and got.shape == (M_, nx)
-    want = gy.double().t() @ x[:, :nx].double()
-    f32 = gy.t() @ x[:, :nx]
-    e = float((got.double() - want).norm() / want.norm())
-    et = float((f32.double() - want).norm() / want.norm())
-    assert e <= max(3 * et, 2e-6), (e, et)
-
-
 def test_critic_onepass_matches_float64(M):
     """The one-pass critic (a2c_vec._CriticOnePass: fjsp_a2c_critic_fused's forward, value
     gradient from the per-state loss coefficients, value-head and hidden-layer backward in one
