@@ -66,11 +66,16 @@ def critic_bounds(world):
     return out
 
 
+# the 16 key bits that pick a critic state's owner: the top 16 of the 59 bits RowGroups sorts by,
+# so the grouping's distinct states come out already ordered by owner rank
+DEST_SHIFT = 43
+
+
 def _critic_dest(key, world):
     if world == 1:
         return torch.zeros_like(key)
-    b = torch.tensor(critic_bounds(world), dtype=torch.int64, device=key.device)
-    return torch.searchsorted(b, (key >> 16) & 0xFFFF, right=True)
+    b = A._index_tensor(tuple(critic_bounds(world)), key.device)
+    return torch.searchsorted(b, (key >> DEST_SHIFT) & 0xFFFF, right=True)
 
 
 def _group_sums(perm, ends, vals):
@@ -192,7 +197,10 @@ def combine(feats, masks, actions, ret, adv, mean, std, world):
     # per group: count and f64 sums in sorted order
     adv32 = adv.float().permute(1, 0, 2).reshape(NA, S)
     advn = (adv32 - mean[:, None]) / (std[:, None] + 1e-8) if mean is not None else adv32
-    sadv = _group_sums(g.perm[:NA], g.ends[:NA], advn.double())                          # [8, Umax]
+    if g.gsorted is not None:   # one run-sum pass (f64 in sorted order, fjsp_a2c_run_sums)
+        sadv = A.run_sums(advn, A._index_tensor(tuple(range(NA)), dev), None, g).double()  # [8, Umax]
+    else:
+        sadv = _group_sums(g.perm[:NA], g.ends[:NA], advn.double())
     if ret.is_cuda:
         rs, _ = A.slab_stats(ret=ret)                                                     # [2, S], one pass
     else:
@@ -201,25 +209,19 @@ def combine(feats, masks, actions, ret, adv, mean, std, world):
     cs = _group_sums(g.perm[NA:], g.ends[NA:], rs)                                       # [2, Umax]
     cnt = _counts(g.ends).to(torch.int32)                                                # [9, Umax]
 
-    # actor records, agent-major, then reordered by owner rank
-    ai = torch.cat([torch.full((U[a],), a, dtype=torch.int64, device=dev) for a in range(NA)])
-    gi = torch.cat([torch.arange(U[a], device=dev) for a in range(NA)])
+    # actor records, built in owner-rank order (each agent's groups in key order)
+    agents = [a for d in range(world) for a in range(NA) if owner_of_agent(a, world) == d]
+    na_d = [sum(U[a] for a in range(NA) if owner_of_agent(a, world) == d) for d in range(world)]
+    ai = torch.cat([torch.full((U[a],), a, dtype=torch.int64, device=dev) for a in agents])
+    gi = torch.cat([torch.arange(U[a], device=dev) for a in agents])
     s1 = g.first[ai, gi]
     x = torch.gather(rows.index_select(0, s1), 1, A.gather_index(dev)[ai])               # [Ua, 13]
     word = info[ai, s1] | (ai.to(torch.int32) << 16)
     arec = torch.cat([_i32(keys[ai, s1], 2), _i32(sadv[ai, gi], 2), _i32(x, 13), word[:, None], cnt[ai, gi][:, None],
                       torch.zeros_like(word)[:, None]], dim=1)
-    offs_a = [0]
-    for a in range(NA):
-        offs_a.append(offs_a[-1] + U[a])
-    order, na_d = [], []
-    for d in range(world):
-        mine = [a for a in range(NA) if owner_of_agent(a, world) == d]
-        order += [torch.arange(offs_a[a], offs_a[a + 1], device=dev) for a in mine]
-        na_d.append(sum(U[a] for a in mine))
-    arec = arec.index_select(0, torch.cat(order)) if world > 1 else arec
 
-    # critic records, ordered by owner rank (stable)
+    # critic records: the grouping's order is ascending in the 59 sorted key bits, so ascending in
+    # the owner bits (DEST_SHIFT) too — already ordered by owner rank
     uc = U[NA]
     s1 = g.first[NA, :uc]
     ck = keys[NA].index_select(0, s1)
@@ -227,8 +229,6 @@ def combine(feats, masks, actions, ret, adv, mean, std, world):
                       torch.zeros(uc, 1, dtype=torch.int32, device=dev),
                       _i32(rows.index_select(0, s1)[:, :A.GLOBAL_DIM], A.GLOBAL_DIM)], dim=1)
     dest = _critic_dest(ck, world)
-    if world > 1:
-        crec = crec.index_select(0, torch.argsort(dest, stable=True))
     nc_d = torch.bincount(dest, minlength=world).tolist()
     counts = torch.tensor([na_d, nc_d], dtype=torch.int64).t().contiguous()
     return Combined(arec, crec, counts, bad.float().reshape(()), S)
@@ -335,11 +335,10 @@ def owner_losses(actors, critic, recv, rank, world, count, entropy_coef):
     al = torch.zeros(NA, dtype=torch.float32, device=dev)
     cl = torch.zeros((), dtype=torch.float32, device=dev)
     bad = torch.zeros((), dtype=torch.bool, device=dev)
-    agent = (arec[:, AW - 3] >> 16) & 0xFF
-    for a in range(NA):
-        if owner_of_agent(a, world) != rank:
-            continue
-        r = arec[agent == a]
+    mine = [a for a in range(NA) if owner_of_agent(a, world) == rank]
+    agent = (arec[:, AW - 3] >> 16) & 0xFF if len(mine) > 1 else None
+    for a in mine:
+        r = arec if agent is None else arec[agent == a]   # one owned agent: every record is its
         g = _regroup(r[:, 0:2].contiguous().view(torch.int64).reshape(-1))
         if g is None:
             continue

@@ -95,10 +95,15 @@ def main(world=8, n=4096, T=256, warm=1, reps=3):
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as pr:
             ret, adv = L.gae_fn(s["rewards"], s["values"], s["done"], L.gamma, L.lamb, L.use_gae)
             SL.combine(s["feats"][:T], s["masks"][:T], s["actions"], ret, adv, mean, std, world)
+            torch.cuda.synchronize()
+        print("== combine (rank %d)" % d, file=sys.stderr)
+        print(pr.key_averages().table(sort_by="self_cuda_time_total", row_limit=30), file=sys.stderr)
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as pr:
             al, cl, bad = SL.owner_losses(L.actors, L.critic, recvs[d], d, world, count, L.entropy_coef)
             (al.sum() + cl).backward()
             torch.cuda.synchronize()
-        print(pr.key_averages().table(sort_by="self_cuda_time_total", row_limit=45), file=sys.stderr)
+        print("== own (rank %d)" % d, file=sys.stderr)
+        print(pr.key_averages().table(sort_by="self_cuda_time_total", row_limit=30), file=sys.stderr)
     res["bytes_sent_to_other_ranks"] = [sum(c.bytes_by_dest()) - c.bytes_by_dest()[r] for r, c in enumerate(combs)]
     res["bytes_by_dest_rank0"] = combs[0].bytes_by_dest()
     res["gather_bytes_per_rank"] = L.exchange_bytes_per_batch() // world if L.exchange == "gather" else T * n * 258 + n * 4
