@@ -3,7 +3,7 @@
 #   bash scripts/gpu.sh <out-dir-name> <stage> [<stage> ...]
 # stages:
 #   suite             the whole -m gpu suite (one process), then smoke()
-#   tests:<expr>      pytest -m gpu -k <expr>
+#   tests:<expr>      pytest -m gpu -k <expr> (',' for ' ')
 #   bench             the driver-form bench line (N=1)
 #   bench_a2c[:args]  bench.py --workload a2c (extra args after ':' with ',' for ' ')
 #   py:<script,args>  python3 <script> <args> (',' for ' '), stdout to <stage-index>.json
@@ -32,7 +32,7 @@ for stage in "$@"; do
       timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
       rc=$?; tail -2 "$OUT/smoke.log" ;;
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$arg" > "$OUT/tests_$i.log" 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$args" > "$OUT/tests_$i.log" 2>&1
       rc=$?; tail -3 "$OUT/tests_$i.log"; grep -E "FAILED|ERROR" "$OUT/tests_$i.log" | head -5 ;;
     bench)
       timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_$i.json" 2> "$OUT/bench_$i.err"
