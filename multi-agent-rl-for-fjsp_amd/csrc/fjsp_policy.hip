@@ -619,27 +619,107 @@ struct StepArgs {
     float* feats;
     uint32_t* tile_cnt;    // [na] arrivals per tile (0 between launches)
     uint32_t* tile_act;    // [na][8][16] the tile's actions, 4 envs per dword
-    int autoreset;
+    int flags;             // STEP_AUTORESET
 };
+constexpr int STEP_AUTORESET = 1;   // reset(seed=None) an env whose episode ended
 
 // The tile's state words, [NSTATE][64] u32 after the policy's LDS (STATE_BYTES more per
 // workgroup: 2 x 77.5 KB still fit a CU): every actor workgroup of the tile copies them in with
 // LDS DMAs at its start, in the shadow of its network, so the one that runs the step reads them
 // from LDS instead of waiting a memory round trip after the hand-off.
 constexpr int STATE_BYTES = fjsp::NSTATE * 64 * 4;
-static_assert(2 * (LDS_BYTES + STATE_BYTES) <= 160 * 1024, "two workgroups per CU");
+// ... and the reward table (RLUT_SIZE doubles, the same for every tile) after them, so the step
+// tail neither copies it nor waits for it
+constexpr int LUT_BYTES = fjsp::RLUT_SIZE * 8;
+static_assert(LUT_BYTES % 256 == 0, "the reward table in whole 64-dword DMA pieces");
+static_assert(2 * (LDS_BYTES + STATE_BYTES + LUT_BYTES) <= 160 * 1024, "two workgroups per CU");
 __device__ __forceinline__ void state_prefetch(const StepArgs& St, int tile, uint32_t* s_state, int lane, int wave) {
     const int e = min(tile * TA + lane, St.S.n - 1);
     for (int i = wave; i < fjsp::NSTATE; i += NWAVE)
         __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(St.S.words + (size_t)i * St.S.n + e),
                                          (__attribute__((address_space(3))) void*)(s_state + i * 64), 4, 0, 0);
+    const uint32_t* lut = reinterpret_cast<const uint32_t*>(St.C.lut);
+    uint32_t* s_lut = s_state + fjsp::NSTATE * 64;
+    for (int i = wave; i < LUT_BYTES / 256; i += NWAVE)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(lut + i * 64 + lane),
+                                         (__attribute__((address_space(3))) void*)(s_lut + i * 64), 4, 0, 0);
 }
 
+// The step tail's outputs staged in the (then free) policy LDS as rows of the tile's 64 envs, then
+// copied out by all eight waves in 16-byte pieces: 24 store instructions for the workgroup
+// instead of 108 four- or one-byte stores on the stepping wave (the store issue was ~5 k of the
+// tail's ~16 k cycles, scripts/diag_collect_tail.py).  Rows: u32 [69][64] = a2c features 0..37,
+// state words 38..67, status 68; f64 [8][64] rewards; u8 [31][64] = masks 0..28, term, trunc.
+constexpr int STG_F32 = 0, STG_NF32 = fjsp::NFEAT + fjsp::NSTATE + 1;
+constexpr int STG_F64 = STG_F32 + STG_NF32 * 64 * 4;
+constexpr int STG_U8 = STG_F64 + NAG * 64 * 8, STG_NU8 = fjsp::NMASK + 2;
+static_assert(STG_U8 + STG_NU8 * 64 <= LDS_BYTES - 16 && STG_F64 % 16 == 0 && STG_U8 % 16 == 0, "staging rows");
+// observe() into the staging rows (StoreSink's values for the collect's two outputs); one wave
+// builds the a2c features, another the masks, from the staged state (the work of the other half
+// is dead code in each)
+template <bool FEATS, bool MASKS>
+struct TileSink {
+    uint32_t* rf;   // feature rows
+    uint8_t* rm;    // mask rows
+    int lane;
+    __device__ __forceinline__ void feat(int c, float v) { if (FEATS) rf[c * 64 + lane] = __float_as_uint(v); }
+    __device__ __forceinline__ void i32(int f, int v) { feat(fjsp::FEAT_OF_I32[f], (float)v); }
+    __device__ __forceinline__ void i8(int f, int v) { feat(fjsp::FEAT_OF_I8[f], (float)(int8_t)v); }
+    __device__ __forceinline__ void f32(int f, float v) { feat(fjsp::FEAT_OF_F32[f], v); }
+    __device__ __forceinline__ void mask(int f, int v) { if (MASKS) rm[f * 64 + lane] = (uint8_t)(int8_t)v; }
+};
+// the next observation of a staged tile from its staged post-step state: wave 1 the masks, wave 2
+// the features (and the state's status word, which observe() flags on an int8 overflow)
+__device__ __forceinline__ void tile_observe(const StepArgs& St, unsigned char* s_mem, const uint32_t* s_state, int lane,
+                                             int wave) {
+    uint32_t* rf = reinterpret_cast<uint32_t*>(s_mem + STG_F32);
+    fjsp::Env E;
+#pragma unroll
+    for (int i = 0; i < fjsp::NSTATE; i++) E.w[i] = rf[(fjsp::NFEAT + i) * 64 + lane];
+    fjsp::Cfg C = St.C;
+    C.lut = reinterpret_cast<const double*>(s_state + fjsp::NSTATE * 64);
+    if (wave == 1) {
+        TileSink<false, true> sink{rf, s_mem + STG_U8, lane};
+        fjsp::observe(E, C, sink);
+    } else {
+        TileSink<true, false> sink{rf, s_mem + STG_U8, lane};
+        fjsp::observe(E, C, sink);
+        rf[(fjsp::NFEAT + 2) * 64 + lane] = E.w[2];
+    }
+}
+static_assert(fjsp::NSTATE > 2, "the status word is state word 2 (fjsp_env.h Env::status)");
+__device__ __forceinline__ void tile_copy_out(const StepArgs& St, int tile, const unsigned char* s_mem, int tid) {
+    const size_t n = (size_t)St.S.n, e0 = (size_t)tile * TA;
+    const uint4* sf = reinterpret_cast<const uint4*>(s_mem + STG_F32);
+    for (int c = tid; c < STG_NF32 * 16; c += NTHR) {
+        const int row = c >> 4, piece = c & 15;
+        uint32_t* dst = row < fjsp::NFEAT ? (St.feats ? reinterpret_cast<uint32_t*>(St.feats) + row * n : nullptr)
+                        : row < fjsp::NFEAT + fjsp::NSTATE ? St.S.words + (row - fjsp::NFEAT) * n : St.status;
+        if (dst) *reinterpret_cast<uint4*>(dst + e0 + 4 * piece) = sf[c];
+    }
+    const uint4* sd = reinterpret_cast<const uint4*>(s_mem + STG_F64);
+    if (St.rewards) {
+        for (int c = tid; c < NAG * 32; c += NTHR)
+            *reinterpret_cast<uint4*>(St.rewards + (c >> 5) * n + e0 + 2 * (c & 31)) = sd[c];
+    }
+    const uint4* sb = reinterpret_cast<const uint4*>(s_mem + STG_U8);
+    for (int c = tid; c < STG_NU8 * 4; c += NTHR) {
+        const int row = c >> 2, piece = c & 3;
+        uint8_t* dst = row < fjsp::NMASK ? (St.next_masks ? reinterpret_cast<uint8_t*>(St.next_masks) + row * n : nullptr)
+                       : row == fjsp::NMASK ? St.term : St.trunc;
+        if (dst) *reinterpret_cast<uint4*>(dst + e0 + 16 * piece) = sb[c];
+    }
+}
+
+// STAGED: a full tile whose outputs go through the staging rows (tile_copy_out); else every lane
+// stores its own outputs (partial tiles, unaligned outputs).
+template <bool STAGED>
 __device__ __forceinline__ void tile_step(const PolicyArgs& A, const StepArgs& St, int tile, unsigned char* s_mem,
                                           const uint32_t* s_state, int lane) {
-    double* s_lut = reinterpret_cast<double*>(s_mem);
+    const double* s_lut = reinterpret_cast<const double*>(s_state + fjsp::NSTATE * 64);
     const int e = tile * TA + lane;
     const bool valid = e < A.n;
+    FJSP_DIAG(const int tid = lane;)   // diagnostic builds: the tail's phases into the workgroup's slots 2..6
     fjsp::Env E;
     int act[NAG];
     if (valid) {
@@ -651,50 +731,73 @@ __device__ __forceinline__ void tile_step(const PolicyArgs& A, const StepArgs& S
             act[a] = (int)((__hip_atomic_load(ta + a * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (8 * (lane & 3))) &
                            0xFFu);
     }
-    for (int i = lane; i < fjsp::RLUT_SIZE; i += 64) s_lut[i] = St.C.lut[i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (!valid) return;
+    PST(2, __builtin_amdgcn_s_memtime());
     fjsp::Cfg C = St.C;
     C.lut = s_lut;
     const fjsp::Tables T = fjsp::tables_of(St.S, e);
     // k_step<canon>'s step_and_emit for the outputs the collect asks for (the observation before
     // the auto-reset is not among them)
     const uint32_t n = (uint32_t)St.S.n, ue = (uint32_t)e;
+    uint32_t* rf = reinterpret_cast<uint32_t*>(s_mem + STG_F32);
+    double* rd = reinterpret_cast<double*>(s_mem + STG_F64);
+    uint8_t* rb = s_mem + STG_U8;
     uint32_t res[NAG];
     const double g8 = fjsp::env_advance<true>(E, T, C, act, nullptr, res);
-    if (St.rewards) {
+    PST(3, __builtin_amdgcn_s_memtime());
 #pragma unroll
-        for (int a = 0; a < NAG; a++) fjsp::st32(St.rewards, (uint32_t)a * n + ue, g8 + fjsp::local_reward(C, a, res[a], act[a]));
+    for (int a = 0; a < NAG; a++) {
+        const double r = g8 + fjsp::local_reward(C, a, res[a], act[a]);
+        if (STAGED) rd[a * 64 + lane] = r;
+        else if (St.rewards) fjsp::st32(St.rewards, (uint32_t)a * n + ue, r);
     }
     const int nord = E.norders();
     const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
     const int truncated = E.step() >= C.max_steps;
-    if (St.term) fjsp::st32(St.term, ue, (uint8_t)all_done);
-    if (St.trunc) fjsp::st32(St.trunc, ue, (uint8_t)truncated);
-    if (St.status) fjsp::st32(St.status, ue, E.status());
-    E.set_step(E.step() + 1);
-    if (St.autoreset && (all_done || truncated)) E = fjsp::env_reset_cold(E, T, C, St.S, e, nord);
-    if (St.next_masks || St.feats) {
-        fjsp::StoreSink nsink{nullptr, nullptr, nullptr, St.next_masks, 0u, n, ue, St.feats};
-        fjsp::observe(E, C, nsink);
+    if (STAGED) {
+        rb[fjsp::NMASK * 64 + lane] = (uint8_t)all_done;
+        rb[(fjsp::NMASK + 1) * 64 + lane] = (uint8_t)truncated;
+        rf[(STG_NF32 - 1) * 64 + lane] = E.status();
+    } else {
+        if (St.term) fjsp::st32(St.term, ue, (uint8_t)all_done);
+        if (St.trunc) fjsp::st32(St.trunc, ue, (uint8_t)truncated);
+        if (St.status) fjsp::st32(St.status, ue, E.status());
     }
-    fjsp::env_store(E, St.S.words, St.S.n, e);
+    E.set_step(E.step() + 1);
+    PST(4, __builtin_amdgcn_s_memtime());
+    if ((St.flags & STEP_AUTORESET) && (all_done || truncated)) E = fjsp::env_reset_cold(E, T, C, St.S, e, nord);
+    PST(5, __builtin_amdgcn_s_memtime());
+    if (STAGED) {   // the observation: tile_observe on waves 1 and 2
+#pragma unroll
+        for (int i = 0; i < fjsp::NSTATE; i++) rf[(fjsp::NFEAT + i) * 64 + lane] = E.w[i];
+    } else {
+        if (St.next_masks || St.feats) {
+            fjsp::StoreSink nsink{nullptr, nullptr, nullptr, St.next_masks, 0u, n, ue, St.feats};
+            fjsp::observe(E, C, nsink);
+        }
+        fjsp::env_store(E, St.S.words, St.S.n, e);
+    }
+    PST(6, __builtin_amdgcn_s_memtime());
 }
 
+// STAGED (every tile full, every output and state row 16-byte aligned): the tail's outputs go
+// through the staging rows (tile_copy_out)
+template <bool STAGED>
 __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4))) k_policy_step(PolicyArgs A, StepArgs St) {
-    __shared__ __attribute__((aligned(16))) unsigned char s_mem[LDS_BYTES + STATE_BYTES];
+    __shared__ __attribute__((aligned(16))) unsigned char s_mem[LDS_BYTES + STATE_BYTES + LUT_BYTES];
     uint32_t* s_state = reinterpret_cast<uint32_t*>(s_mem + LDS_BYTES);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.x;
+    PST(0, __builtin_amdgcn_s_memrealtime());
+    PST(1, __builtin_amdgcn_s_memtime());
     if (b < A.nc) {
         critic_tile<false>(A, 2 * A.tile0 + b, s_mem, tid, lane, wave, CriticSave{});
         return;
     }
     int role, tile;
     actor_block(A, b - A.nc, role, tile);
+    PST(13, role);
     tile += A.tile0;
     state_prefetch(St, tile, s_state, lane, wave);   // landed by actor_tile's first barrier
     int act = 0;
@@ -719,8 +822,18 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
         *s_last = last;
     }
     __syncthreads();
-    if (wave != 0 || !*s_last) return;
-    tile_step(A, St, tile, s_mem, s_state, lane);
+    if (!*s_last) return;
+    PST(14, __builtin_amdgcn_s_memtime());   // diagnostic builds: the tile's step tail
+    if (STAGED) {
+        if (wave == 0) tile_step<true>(A, St, tile, s_mem, s_state, lane);
+        __syncthreads();                      // the step's staging rows are in
+        if (wave == 1 || wave == 2) tile_observe(St, s_mem, s_state, lane, wave);
+        __syncthreads();                      // the observation's
+        tile_copy_out(St, tile, s_mem, tid);
+    } else if (wave == 0) {
+        tile_step<false>(A, St, tile, s_mem, s_state, lane);
+    }
+    PST(15, __builtin_amdgcn_s_memtime());
 }
 
 // The critic's forward over n samples for the A2C update (values + the saved hidden layers), on
@@ -1508,8 +1621,16 @@ int fjsp_internal_policy_step(const float* feats, const int8_t* masks, int32_t n
     // envs [env_begin, env_begin + env_count): whole 64-env tiles (the caller checks the range)
     PolicyArgs A{feats, masks, n, actor_w, critic_w, seed, env_gid0, step, deterministic, actions, values, nullptr,
                  values ? (env_count + TC - 1) / TC : 0, (env_count + TA - 1) / TA, env_begin / TA, policy_xmap()};
-    StepArgs St{S, C, out.rewards, out.term, out.trunc, out.status, out.next_masks, out.feats, tile_cnt, tile_act, autoreset};
-    hipLaunchKernelGGL(k_policy_step, dim3((unsigned)(A.nc + NAG * A.na)), dim3(NTHR), 0, stream, A, St);
+    // the tiles copy their outputs out in 16-byte pieces when every tile is full and every output
+    // row and state row of a tile starts 16-byte aligned (n % 64 == 0, 16-byte aligned bases)
+    const uintptr_t bases = (uintptr_t)out.rewards | (uintptr_t)out.term | (uintptr_t)out.trunc | (uintptr_t)out.status |
+                            (uintptr_t)out.next_masks | (uintptr_t)out.feats | (uintptr_t)S.words;
+    StepArgs St{S, C, out.rewards, out.term, out.trunc, out.status, out.next_masks, out.feats, tile_cnt, tile_act,
+                autoreset ? STEP_AUTORESET : 0};
+    if (n % TA == 0 && (bases & 15u) == 0)
+        hipLaunchKernelGGL(k_policy_step<true>, dim3((unsigned)(A.nc + NAG * A.na)), dim3(NTHR), 0, stream, A, St);
+    else
+        hipLaunchKernelGGL(k_policy_step<false>, dim3((unsigned)(A.nc + NAG * A.na)), dim3(NTHR), 0, stream, A, St);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

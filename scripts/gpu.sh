@@ -11,6 +11,7 @@
 #   prof_step         the step bench's kernel trace + FETCH_SIZE / WRITE_SIZE passes
 #   prof_a2c[:args]   the A2C bench's kernel trace + FETCH / WRITE / L2-hit passes
 #   pmc:<ctr,..>:<script,args>  one counter pass over a python script
+#   profenv:<VAR=VAL+..>:<script,args>  kernel trace + stats of a python script with environment variables
 # Every GPU step runs under its own time limit; the script stops at the first failure, abort,
 # segfault or time-out (nothing more runs on the GPU after one).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -59,6 +60,11 @@ for stage in "$@"; do
         timeout -s KILL 300 rocprofv3 --pmc $c -T -d "$OUT/a2c_$d" -o $d --output-format csv -- python3 bench.py $A2C > "$OUT/a2c_$d.log" 2>&1
         rc=$?; echo "a2c $c rc=$rc"; bad $rc && exit $rc
       done ;;
+    profenv)
+      # profenv:VAR=VAL[+VAR=VAL]:script,args  kernel trace + stats of one python run
+      ev="${arg%%:*}"; rest="${arg#*:}"
+      env ${ev//+/ } timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/kt_$i" -o kt --output-format csv -- python3 ${rest//,/ } > "$OUT/kt_$i.log" 2>&1
+      rc=$? ;;
     pmc)
       ctr="${arg%%:*}"; rest="${arg#*:}"
       d=$(echo "${ctr%%,*}" | tr 'A-Z' 'a-z')_$i
