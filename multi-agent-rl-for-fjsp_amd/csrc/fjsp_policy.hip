@@ -79,6 +79,9 @@ constexpr int X_BYTES = cmax(NP * XPA, NP * XPC) * 2;
 constexpr int H_BYTES = cmax(cmax(NP * HPA, NP * HPC) * 2, NWAVE * 8 * TA * 4);   // also the logit partials
 constexpr int W3_BYTES = 8 * HID * 4;
 constexpr int LDS_BYTES = X_BYTES + H_BYTES + W3_BYTES;
+// the actor's input planes end here; the station dedup's slot / input words fit in the rest of X
+constexpr int ACT_X_BYTES = NP * XPA * 2;
+static_assert(ACT_X_BYTES + (64 + 4 + 3 * 64) * 4 <= X_BYTES, "station dedup words beside the actor inputs");
 static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
 
 __constant__ int c_obs_off[NAG] = {0, 7, 20, 23, 26, 29, 32, 35};
@@ -231,13 +234,13 @@ __device__ __forceinline__ void store_rows_f32(const f32x16& acc, int row0, cons
 // The logits' partial sums of this wave's 32 rows of h2 = relu(acc + b2) (rows of the C/D
 // layout) for NA actions -> s_part[wave][j][env]: per lane its 16 rows, then the other
 // half-wave's 16 (lane ^ 32).  Actions in chunks of up to 4 (all 8 at once spilled at 128 VGPRs).
-template <int NA>
-__device__ __forceinline__ void logit_partials(const f32x16 acc[2], const Row16& b2, const float* s_w3, float* s_part,
+template <int NA, int NC>
+__device__ __forceinline__ void logit_partials(const f32x16 acc[NC], const Row16& b2, const float* s_w3, float* s_part,
                                                int wave, int lane) {
     constexpr int CH = NA < 4 ? NA : 4;
     static_assert(NA % CH == 0, "action chunks");
 #pragma unroll
-    for (int c = 0; c < 2; c++) {
+    for (int c = 0; c < NC; c++) {
         float h[16];
 #pragma unroll
         for (int r = 0; r < 16; r++) h[r] = relu(acc[c][r] + b2[r]);
@@ -323,6 +326,7 @@ struct PolicyArgs {
     int nc, na;   // critic / actor workgroups per role
     int tile0 = 0;   // first 64-env tile of the launch (k_policy_step over an env range)
     int xmap = 0;    // actor workgroup -> (role, tile) order, actor_block
+    int dedup = 1;   // the station agents' MLP once per distinct input of a tile (actor_tile)
 };
 
 // Actor workgroup j (after the critic's) -> (role, tile).  Workgroups are dealt to the 8 XCDs
@@ -433,6 +437,53 @@ __device__ __forceinline__ void critic_tile(const PolicyArgs& A, int tile, unsig
     }
 }
 
+// The actor's layers 1-3 on NC 32-env column tiles of s_x (layer 1 per K half of layer 2: one
+// 32 x 32 tile per wave and half, so only half of h1 is ever in LDS), leaving the logit partials
+// [8 waves][8 actions][TA] in s_part.
+template <int NC>
+__device__ __forceinline__ void actor_mlp(const PolicyArgs& A, int role, unsigned char* s_mem, int tid, int lane, int wave,
+                                          const bf16x8* W1, const float* B1, const bf16x8* W2, const float* B2) {
+    __bf16* s_x = reinterpret_cast<__bf16*>(s_mem);
+    __bf16* s_h = reinterpret_cast<__bf16*>(s_mem + X_BYTES);
+    float* s_part = reinterpret_cast<float*>(s_mem + X_BYTES);
+    const float* s_w3 = reinterpret_cast<const float*>(s_mem + X_BYTES + H_BYTES);
+    const int rt1 = wave & 3, ct1 = wave >> 2;   // layer-1 tile of each half
+    const bool l1 = NC == 2 || ct1 == 0;          // with one column tile, waves 4..7 have no layer-1 tile
+    WRing<1> r1;
+    if (l1) wring_start(r1, wblocks<1, 1>(W1, rt1, 0, lane));
+    Row16 b1 = load_rows(B1, 32 * rt1, lane);
+    __syncthreads();
+    PST(3, __builtin_amdgcn_s_memtime());
+    f32x16 acc[NC];
+    zero_acc<NC>(acc);
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+        f32x16 a1[1];
+        if (l1) {
+            zero_acc<1>(a1);
+            mfma_rows<1, XSA, XPA, 1>(r1, wblocks<1, 1>(W1, 4 * half + rt1, 0, lane), s_x, 32 * ct1, lane, a1);
+        }
+        WRing<HID / 32> r2;
+        wring_start(r2, wblocks<HID / 32, HID / 16>(W2, wave, 8 * half, lane));
+        if (l1) store_planes<HSA, HPA>(a1[0], 32 * rt1, 32 * ct1, b1, s_h, lane);
+        __syncthreads();
+        PST(4 + 2 * half, __builtin_amdgcn_s_memtime());
+        mfma_rows<HID / 32, HSA, HPA, NC>(r2, wblocks<HID / 32, HID / 16>(W2, wave, 8 * half, lane), s_h, 0, lane, acc);
+        if (half == 0) {                           // the second half's layer-1 weights and biases
+            if (l1) wring_start(r1, wblocks<1, 1>(W1, 4 + rt1, 0, lane));
+            b1 = load_rows(B1, 128 + 32 * rt1, lane);
+        }
+        __syncthreads();                           // every wave has read this half
+        PST(5 + 2 * half, __builtin_amdgcn_s_memtime());
+    }
+    // layer 3, the logits, straight from the accumulators
+    const Row16 b2 = load_rows(B2, 32 * wave, lane);
+    if (c_nact[role] == 8) logit_partials<8, NC>(acc, b2, s_w3, s_part, wave, lane);
+    else logit_partials<3, NC>(acc, b2, s_w3, s_part, wave, lane);
+    __syncthreads();
+    PST(8, __builtin_amdgcn_s_memtime());
+}
+
 // Actor `role` on a tile of 64 envs.  Layer 1 is computed per K half of layer 2 (rows 0..127,
 // then 128..255: one 32 x 32 tile per wave each), each half stored as the bf16 planes of layer
 // 2's input and summed into layer 2's accumulators (32 rows x 64 envs per wave), so only half of
@@ -440,7 +491,6 @@ __device__ __forceinline__ void critic_tile(const PolicyArgs& A, int tile, unsig
 __device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int tile, unsigned char* s_mem, int tid,
                                            int lane, int wave, int& act_out) {
     __bf16* s_x = reinterpret_cast<__bf16*>(s_mem);                      // inputs [NP][TA][XSA]
-    __bf16* s_h = reinterpret_cast<__bf16*>(s_mem + X_BYTES);            // an h1 half [NP][TA][HSA]
     float* s_part = reinterpret_cast<float*>(s_mem + X_BYTES);           // logit partials [8][8][TA] (after layer 2)
     float* s_w3 = reinterpret_cast<float*>(s_mem + X_BYTES + H_BYTES);   // logit weights [8][256]
     const int n = A.n, e0 = tile * TA;
@@ -483,41 +533,59 @@ __device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int ti
     }
     PST(2, __builtin_amdgcn_s_memtime());
     reinterpret_cast<float4*>(s_w3)[tid] = w3v;
-    inputs_store<TA, A_DPAD>(xv, tid, s_x);
-    const int rt1 = wave & 3, ct1 = wave >> 2;   // layer-1 tile of each half
-    WRing<1> r1;
-    wring_start(r1, wblocks<1, 1>(W1, rt1, 0, lane));
-    Row16 b1 = load_rows(B1, 32 * rt1, lane);
-    __syncthreads();
-    PST(3, __builtin_amdgcn_s_memtime());
-    f32x16 acc[2];
-    zero_acc<2>(acc);
-#pragma unroll
-    for (int half = 0; half < 2; half++) {
-        f32x16 a1[1];
-        zero_acc<1>(a1);
-        mfma_rows<1, XSA, XPA, 1>(r1, wblocks<1, 1>(W1, 4 * half + rt1, 0, lane), s_x, 32 * ct1, lane, a1);
-        WRing<HID / 32> r2;
-        wring_start(r2, wblocks<HID / 32, HID / 16>(W2, wave, 8 * half, lane));
-        store_planes<HSA, HPA>(a1[0], 32 * rt1, 32 * ct1, b1, s_h, lane);
+    // The station agents (three inputs) see a handful of distinct inputs per tile (<= 7 in every
+    // unforced tile of an A2C collect, scripts/diag_tile_distinct.py): their MLP then runs once
+    // per distinct input on ONE 32-env column tile (half the matrix-core work) and every env reads
+    // its input's logits.  A column's outputs depend only on its input (each MFMA output element
+    // sums the same 16-deep blocks in the same order), so the probabilities are bit-identical.
+    int ncol = 2;
+    uint32_t* s_slot = reinterpret_cast<uint32_t*>(s_mem + ACT_X_BYTES);   // [64] slot | leader << 8
+    if (role >= 2 && A.dedup) {
+        uint32_t* s_feat = s_slot + TA + 4;                                   // [3][64] input bits
+        if (wave < 3) s_feat[wave * TA + lane] = __float_as_uint(xv[0]);     // wave w: feature w of env lane
         __syncthreads();
-        PST(4 + 2 * half, __builtin_amdgcn_s_memtime());
-        mfma_rows<HID / 32, HSA, HPA, 2>(r2, wblocks<HID / 32, HID / 16>(W2, wave, 8 * half, lane), s_h, 0, lane, acc);
-        if (half == 0) {                           // the second half's layer-1 weights and biases
-            wring_start(r1, wblocks<1, 1>(W1, 4 + rt1, 0, lane));
-            b1 = load_rows(B1, 128 + 32 * rt1, lane);
+        if (wave == 0) {
+            const uint32_t x0 = s_feat[lane], x1 = s_feat[TA + lane], x2 = s_feat[2 * TA + lane];
+            uint64_t rem = __ballot(e0 + lane < n);
+            uint32_t slot = 0, nu = 0;
+            while (rem) {
+                const int l = __builtin_ctzll(rem);
+                const uint32_t y0 = __shfl(x0, l), y1 = __shfl(x1, l), y2 = __shfl(x2, l);
+                const uint64_t same = __ballot(x0 == y0 && x1 == y1 && x2 == y2) & rem;
+                if ((same >> lane) & 1u) slot = nu | (lane == l ? 256u : 0u);
+                rem &= ~same;
+                ++nu;
+            }
+            s_slot[lane] = slot;
+            if (lane == 0) s_slot[TA] = nu;
         }
-        __syncthreads();                           // every wave has read this half
-        PST(5 + 2 * half, __builtin_amdgcn_s_memtime());
+        __syncthreads();
+        if (s_slot[TA] <= 32) ncol = 1;
     }
-    // layer 3, the logits, straight from the accumulators
-    const Row16 b2 = load_rows(B2, 32 * wave, lane);
-    if (na == 8) logit_partials<8>(acc, b2, s_w3, s_part, wave, lane);
-    else logit_partials<3>(acc, b2, s_w3, s_part, wave, lane);
-    __syncthreads();
-    PST(8, __builtin_amdgcn_s_memtime());
+    if (ncol == 1) {
+        // the distinct inputs (each group's first env) into columns 0 .. nu - 1
+        constexpr int S = A_DPAD + 8;
+#pragma unroll
+        for (int q = 0; q < XI; q++) {
+            const int i = tid + q * NTHR, k = i / TA, c = i % TA;
+            const uint32_t sl = s_slot[c];
+            if (i < A_DPAD * TA && (sl & 256u)) {
+                __bf16 x0, x1, x2;
+                split3(xv[q], x0, x1, x2);
+                const int col = (int)(sl & 255u);
+                s_x[col * S + k] = x0;
+                s_x[XPA + col * S + k] = x1;
+                s_x[2 * XPA + col * S + k] = x2;
+            }
+        }
+        actor_mlp<1>(A, role, s_mem, tid, lane, wave, W1, B1, W2, B2);
+    } else {
+        inputs_store<TA, A_DPAD>(xv, tid, s_x);
+        actor_mlp<2>(A, role, s_mem, tid, lane, wave, W1, B1, W2, B2);
+    }
     if (tid < TA && e0 + tid < n) {
         const int e = e0 + tid;
+        const int col = ncol == 1 ? (int)(s_slot[tid] & 255u) : tid;   // this env's logit column
         float lg[8], p[8], m[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
@@ -525,7 +593,7 @@ __device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int ti
             if (j < na) {
                 v = B3[j];
 #pragma unroll
-                for (int w = 0; w < NWAVE; w++) v += s_part[(w * 8 + j) * TA + tid];
+                for (int w = 0; w < NWAVE; w++) v += s_part[(w * 8 + j) * TA + col];
             }
             lg[j] = v;
         }
@@ -1607,6 +1675,12 @@ static int policy_xmap() {
     const char* e = getenv("FJSP_POLICY_XMAP");
     return (e && e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : 0;
 }
+// the station agents' in-tile dedup (actor_tile): on unless FJSP_POLICY_DEDUP=0 (A/B runs and the
+// bit-equality test; read per launch)
+static int policy_dedup() {
+    const char* e = getenv("FJSP_POLICY_DEDUP");
+    return !(e && e[0] == '0' && !e[1]);
+}
 
 // fjsp_a2c_policy_step's launch (fjsp_hip.hip holds the handle): k_policy_step on the policy's
 // grid, the step's state / config / outputs and the tile hand-off buffers from the handle.
@@ -1620,7 +1694,7 @@ int fjsp_internal_policy_step(const float* feats, const int8_t* masks, int32_t n
         return fjsp_internal_fail("fjsp_a2c_policy_step: outputs limited to rewards, term, trunc, status, next_masks, feats");
     // envs [env_begin, env_begin + env_count): whole 64-env tiles (the caller checks the range)
     PolicyArgs A{feats, masks, n, actor_w, critic_w, seed, env_gid0, step, deterministic, actions, values, nullptr,
-                 values ? (env_count + TC - 1) / TC : 0, (env_count + TA - 1) / TA, env_begin / TA, policy_xmap()};
+                 values ? (env_count + TC - 1) / TC : 0, (env_count + TA - 1) / TA, env_begin / TA, policy_xmap(), policy_dedup()};
     // the tiles copy their outputs out in 16-byte pieces when every tile is full and every output
     // row and state row of a tile starts 16-byte aligned (n % 64 == 0, 16-byte aligned bases)
     const uintptr_t bases = (uintptr_t)out.rewards | (uintptr_t)out.term | (uintptr_t)out.trunc | (uintptr_t)out.status |
@@ -1840,7 +1914,7 @@ extern "C" int fjsp_a2c_policy(const float* feats, const int8_t* masks, int32_t 
     // workgroups: the critic on 32-env tiles (values wanted), then each actor on 64-env tiles
     // (actions wanted)
     PolicyArgs A{feats, masks, n, actor_w, critic_w, seed, env_gid0, step, deterministic, actions, values, probs,
-                 values ? (n + TC - 1) / TC : 0, actions ? (n + TA - 1) / TA : 0, 0, policy_xmap()};
+                 values ? (n + TC - 1) / TC : 0, actions ? (n + TA - 1) / TA : 0, 0, policy_xmap(), policy_dedup()};
     hipLaunchKernelGGL(k_policy, dim3((unsigned)(A.nc + NAG * A.na)), dim3(NTHR), 0, (hipStream_t)stream, A);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {

@@ -166,6 +166,34 @@ def test_policy_step_launch_equals_two_launches(M, n, T, det, graph, groups):
     assert ends >= n                                    # every env crossed an auto-reset
 
 
+@pytest.mark.parametrize("n,init", [(4096, "random"), (1000, "trained")])
+def test_station_dedup_is_bit_identical(M, n, init, monkeypatch):
+    """The station agents' MLP once per distinct input of a 64-env tile (on one 32-env column
+    tile, actor_tile) == the MLP on every env (FJSP_POLICY_DEDUP=0): every byte of the rollout
+    slabs over two batches with an update between them (the second batch acts with updated
+    weights), partial tiles, random-init and trained networks."""
+    import os
+    A, V = M["A"], M["V"]
+    keys = ("feats", "masks", "actions", "values", "rewards", "term", "trunc", "status")
+    runs = []
+    for dedup in ("0", "1"):
+        monkeypatch.setenv("FJSP_POLICY_DEDUP", dedup)
+        L = A.VecMultiAgentA2C(V.FJSPVecEnv(n), batch_size=64, seed=4)
+        if init == "trained":
+            L.load_state_dicts(A.load_npz_weights(os.path.join(os.path.dirname(__file__), "golden", "trained_policy.npz")))
+        L.reset(seeds=torch.arange(n) + 3, num_orders=25)
+        out = []
+        for _ in range(2):
+            L.collect()
+            out.append({k: L._bufs[k].clone() for k in keys})
+            L.update()
+            L.roll_over()
+        runs.append(out)
+    for b in range(2):
+        for k in keys:
+            assert torch.equal(runs[0][b][k], runs[1][b][k]), (b, k)
+
+
 def test_eager_policy_graph_rekeys_each_batch(M):
     """The PyTorch policy path (fused_policy=False) captured into the collect graph reads the
     draw key from the device: every replay draws new actions, and each batch equals the eager
