@@ -266,7 +266,10 @@ int64_t fjsp_snapshot_bytes(const fjsp_handle* h);
  * hipGraph can be re-keyed between replays), values f32 [N], optional masked
  * probabilities f32 [8][8][N] (NULL to skip).  actions == NULL: the critic's values only (masks,
  * actor_w and seed may then be NULL; e.g. the batch-end bootstrap V(s_T), a2c.py:321-332);
- * values == NULL: the actors only (critic_w may be NULL).  Stream-ordered on `stream`. */
+ * values == NULL: the actors only (critic_w may be NULL).  Stream-ordered on `stream`.
+ * A/B switches read per launch (outputs bit-identical under every setting): FJSP_POLICY_XMAP=0..3
+ * (workgroup -> XCD order), FJSP_POLICY_DEDUP=0 (the station agents' MLP on every env instead
+ * of once per distinct input of a 64-env tile). */
 #define FJSP_POLICY_ACTOR_DPAD 16
 #define FJSP_POLICY_CRITIC_DPAD 48
 #define FJSP_POLICY_ACTOR_FLOATS (3 * 256 * 16 / 2 + 256 + 3 * 256 * 256 / 2 + 256 + 8 * 256 + 16)
