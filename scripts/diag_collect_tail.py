@@ -35,7 +35,7 @@ def main(N=4096, steps=64, warm=1):
     lib.fjsp_debug_policy_stamps(buf.ctypes.data, 1)
     groups = L._collect_groups()
     st = torch.cuda.current_stream()
-    pre, tail, ev_ms, phases = [], [], [], []
+    pre, tail, ev_ms, phases, roles = [], [], [], [], []
     for t in range(steps):
         for e0, cnt in groups:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -48,6 +48,7 @@ def main(N=4096, steps=64, warm=1):
             s = buf.reshape(2048, 16).astype(np.int64)
             last = s[:, 15] > 0
             pre.append((s[last, 14] - s[last, 1]).tolist())
+            roles.extend((s[last, 13] & 255).tolist())
             tail.append((s[last, 15] - s[last, 14]).tolist())
             # the tail's phases: 14 -> 2 actions + reward table, 2 -> 3 env_advance, 3 -> 4 rewards /
             # term / trunc / status, 4 -> 5 auto-reset, 5 -> 6 observation, 6 -> 15 state store
@@ -67,6 +68,7 @@ def main(N=4096, steps=64, warm=1):
            "per_launch_max_entry_to_end_cycles_median": float(np.median(per_launch_max_end)),
            "tail_phase_cycles_mean": dict(zip(["actions_lut", "env_advance", "step_outputs", "autoreset", "observe",
                                                "state_store"], np.concatenate(phases).mean(0).tolist())),
+           "last_role_share": {name: roles.count(r) / max(1, len(roles)) for r, name in enumerate(A.AGENTS)},
            "note": "cycles = s_memtime ticks (shader clock); the entry stamp is the tail workgroup's own"}
     print(json.dumps(res), flush=True)
 
