@@ -269,7 +269,8 @@ int64_t fjsp_snapshot_bytes(const fjsp_handle* h);
  * values == NULL: the actors only (critic_w may be NULL).  Stream-ordered on `stream`.
  * A/B switches read per launch (outputs bit-identical under every setting): FJSP_POLICY_XMAP=0..3
  * (workgroup -> XCD order), FJSP_POLICY_DEDUP=0 (the station agents' MLP on every env instead
- * of once per distinct input of a 64-env tile). */
+ * of once per distinct input of a 64-env tile), FJSP_POLICY_SPLIT=0 (fjsp_a2c_policy_step: the
+ * pickup station's and the AGV's tiles on one 64-env workgroup instead of two 32-env ones). */
 #define FJSP_POLICY_ACTOR_DPAD 16
 #define FJSP_POLICY_CRITIC_DPAD 48
 #define FJSP_POLICY_ACTOR_FLOATS (3 * 256 * 16 / 2 + 256 + 3 * 256 * 256 / 2 + 256 + 8 * 256 + 16)

@@ -81,6 +81,7 @@ constexpr int W3_BYTES = 8 * HID * 4;
 constexpr int LDS_BYTES = X_BYTES + H_BYTES + W3_BYTES;
 // the actor's input planes end here; the station dedup's slot / input words fit in the rest of X
 constexpr int ACT_X_BYTES = NP * XPA * 2;
+static_assert(A_DPAD * 32 == NTHR, "a half tile's inputs: one per thread");
 static_assert(ACT_X_BYTES + (64 + 4 + 3 * 64) * 4 <= X_BYTES, "station dedup words beside the actor inputs");
 static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
 
@@ -281,11 +282,11 @@ __device__ __forceinline__ void input_kc(int i, int& k, int& c) {
     k = ROWS ? i % DPAD : i / T;
     c = ROWS ? i / DPAD : i % T;
 }
-template <int T, int DPAD, bool ROWS = false>
+template <int T, int DPAD, bool ROWS = false, int NV = XI>
 __device__ __forceinline__ void inputs_load(const float* __restrict__ feats, int n, int e0, int off, int din, int tid,
-                                            float v[XI]) {
+                                            float v[NV]) {
 #pragma unroll
-    for (int q = 0; q < XI; q++) {
+    for (int q = 0; q < NV; q++) {
         int k, c;
         const int i = tid + q * NTHR;
         input_kc<T, DPAD, ROWS>(i, k, c);
@@ -327,6 +328,7 @@ struct PolicyArgs {
     int tile0 = 0;   // first 64-env tile of the launch (k_policy_step over an env range)
     int xmap = 0;    // actor workgroup -> (role, tile) order, actor_block
     int dedup = 1;   // the station agents' MLP once per distinct input of a tile (actor_tile)
+    int split = 0;   // k_policy_step: the pickup station's and the AGV's tiles as two 32-env workgroups each
 };
 
 // Actor workgroup j (after the critic's) -> (role, tile).  Workgroups are dealt to the 8 XCDs
@@ -488,12 +490,14 @@ __device__ __forceinline__ void actor_mlp(const PolicyArgs& A, int role, unsigne
 // then 128..255: one 32 x 32 tile per wave each), each half stored as the bf16 planes of layer
 // 2's input and summed into layer 2's accumulators (32 rows x 64 envs per wave), so only half of
 // h1 is ever in LDS.
+// half >= 0: only the tile's envs 32 half .. 32 half + 31, on one column tile (the split pickup /
+// AGV workgroups of k_policy_step, PolicyArgs::split)
 __device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int tile, unsigned char* s_mem, int tid,
-                                           int lane, int wave, int& act_out) {
+                                           int lane, int wave, int& act_out, int half = -1) {
     __bf16* s_x = reinterpret_cast<__bf16*>(s_mem);                      // inputs [NP][TA][XSA]
     float* s_part = reinterpret_cast<float*>(s_mem + X_BYTES);           // logit partials [8][8][TA] (after layer 2)
     float* s_w3 = reinterpret_cast<float*>(s_mem + X_BYTES + H_BYTES);   // logit weights [8][256]
-    const int n = A.n, e0 = tile * TA;
+    const int n = A.n, e0 = tile * TA + (half < 0 ? 0 : 32 * half), ne = half < 0 ? TA : 32;
     const float* wb = A.actor_w + (size_t)role * FJSP_POLICY_ACTOR_FLOATS;
     const bf16x8* W1 = reinterpret_cast<const bf16x8*>(wb);
     const float* B1 = wb + NP * HID * A_DPAD / 2;
@@ -502,7 +506,8 @@ __device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int ti
     const float* W3 = B2 + HID;                                          // f32 [8][256]
     const float* B3 = W3 + 8 * HID;                                      // [8]
     float xv[XI];
-    inputs_load<TA, A_DPAD>(A.feats, n, e0, c_obs_off[role], c_obs_dim[role], tid, xv);
+    if (half < 0) inputs_load<TA, A_DPAD>(A.feats, n, e0, c_obs_off[role], c_obs_dim[role], tid, xv);
+    else inputs_load<32, A_DPAD, false, 1>(A.feats, n, e0, c_obs_off[role], c_obs_dim[role], tid, xv);
     const float4 w3v = reinterpret_cast<const float4*>(W3)[tid];
     const int na = c_nact[role], mo = c_mask_off[role];
     // a tile in which the agent has exactly one valid action in every env: the draw (and argmax)
@@ -512,7 +517,7 @@ __device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int ti
     // (scripts/diag_forced_actions.py)
     uint32_t mbits = 0;   // the env's valid actions (threads < TA)
     int forced = 1;
-    if (tid < TA && e0 + tid < n) {
+    if (tid < ne && e0 + tid < n) {
 #pragma unroll
         for (int j = 0; j < 8; j++)
             if (j < na && A.masks[(size_t)(mo + j) * n + e0 + tid] != 0) mbits |= 1u << j;
@@ -522,7 +527,7 @@ __device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int ti
         PST(13, role | 256);
         PST(9, __builtin_amdgcn_s_memtime());
         PST(10, __builtin_amdgcn_s_memrealtime());
-        if (tid < TA && e0 + tid < n) {
+        if (tid < ne && e0 + tid < n) {
             const int e = e0 + tid, only = __builtin_ctz(mbits | 256u);
             A.actions[(size_t)role * n + e] = (uint8_t)only;
             act_out = only;
@@ -538,9 +543,9 @@ __device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int ti
     // per distinct input on ONE 32-env column tile (half the matrix-core work) and every env reads
     // its input's logits.  A column's outputs depend only on its input (each MFMA output element
     // sums the same 16-deep blocks in the same order), so the probabilities are bit-identical.
-    int ncol = 2;
+    int ncol = half < 0 ? 2 : 1;
     uint32_t* s_slot = reinterpret_cast<uint32_t*>(s_mem + ACT_X_BYTES);   // [64] slot | leader << 8
-    if (role >= 2 && A.dedup) {
+    if (role >= 2 && half < 0 && A.dedup) {
         uint32_t* s_feat = s_slot + TA + 4;                                   // [3][64] input bits
         if (wave < 3) s_feat[wave * TA + lane] = __float_as_uint(xv[0]);     // wave w: feature w of env lane
         __syncthreads();
@@ -562,7 +567,17 @@ __device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int ti
         __syncthreads();
         if (s_slot[TA] <= 32) ncol = 1;
     }
-    if (ncol == 1) {
+    if (half >= 0) {
+        // the half's 32 envs into columns 0 .. 31 (the 64-column plane layout)
+        constexpr int S = A_DPAD + 8;
+        const int k = tid / 32, c = tid % 32;   // 16 x 32 inputs: one per thread
+        __bf16 x0, x1, x2;
+        split3(xv[0], x0, x1, x2);
+        s_x[c * S + k] = x0;
+        s_x[XPA + c * S + k] = x1;
+        s_x[2 * XPA + c * S + k] = x2;
+        actor_mlp<1>(A, role, s_mem, tid, lane, wave, W1, B1, W2, B2);
+    } else if (ncol == 1) {
         // the distinct inputs (each group's first env) into columns 0 .. nu - 1
         constexpr int S = A_DPAD + 8;
 #pragma unroll
@@ -583,9 +598,9 @@ __device__ __forceinline__ void actor_tile(const PolicyArgs& A, int role, int ti
         inputs_store<TA, A_DPAD>(xv, tid, s_x);
         actor_mlp<2>(A, role, s_mem, tid, lane, wave, W1, B1, W2, B2);
     }
-    if (tid < TA && e0 + tid < n) {
+    if (tid < ne && e0 + tid < n) {
         const int e = e0 + tid;
-        const int col = ncol == 1 ? (int)(s_slot[tid] & 255u) : tid;   // this env's logit column
+        const int col = ncol == 1 && half < 0 ? (int)(s_slot[tid] & 255u) : tid;   // this env's logit column
         float lg[8], p[8], m[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
@@ -863,20 +878,30 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
         critic_tile<false>(A, 2 * A.tile0 + b, s_mem, tid, lane, wave, CriticSave{});
         return;
     }
-    int role, tile;
-    actor_block(A, b - A.nc, role, tile);
+    int role, tile, half = -1;
+    if (A.split) {
+        // role-major with the pickup station's and the AGV's tiles as two 32-env halves each:
+        // pickup h0, pickup h1, AGV h0, AGV h1, then the six stations (a tile's blocks share an XCD)
+        const int j = b - A.nc, r = j / A.na;
+        tile = j % A.na;
+        role = r < 4 ? r >> 1 : r - 2;
+        half = r < 4 ? (r & 1) : -1;
+    } else {
+        actor_block(A, b - A.nc, role, tile);
+    }
     PST(13, role);
     tile += A.tile0;
     state_prefetch(St, tile, s_state, lane, wave);   // landed by actor_tile's first barrier
     int act = 0;
-    actor_tile(A, role, tile, s_mem, tid, lane, wave, act);
+    actor_tile(A, role, tile, s_mem, tid, lane, wave, act, half);
     if (wave == 0) {
         const uint32_t a = (uint32_t)act & 0xFFu;
         const int l4 = 4 * (lane & 15);
         const uint32_t w = (uint32_t)__shfl(a, l4) | ((uint32_t)__shfl(a, l4 + 1) << 8) |
                            ((uint32_t)__shfl(a, l4 + 2) << 16) | ((uint32_t)__shfl(a, l4 + 3) << 24);
-        if (lane < 16)
-            __hip_atomic_store((gu32*)(St.tile_act) + ((size_t)tile * NAG + role) * 16 + lane, w,
+        // the role's 16 action words (4 envs each); a half stores its 8
+        if (lane < (half < 0 ? 16 : 8))
+            __hip_atomic_store((gu32*)(St.tile_act) + ((size_t)tile * NAG + role) * 16 + 8 * max(half, 0) + lane, w,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // every wave: its action stores (wave 0) and its state DMAs into LDS have landed
@@ -885,7 +910,8 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4, 4)
     uint32_t* s_last = reinterpret_cast<uint32_t*>(s_mem + LDS_BYTES - 16);
     if (tid == 0) {
         gu32* cnt = (gu32*)(St.tile_cnt) + tile;
-        const uint32_t last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NAG - 1;
+        const uint32_t arrivals = NAG + (A.split ? 2u : 0u);
+        const uint32_t last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == arrivals - 1;
         if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *s_last = last;
     }
@@ -1681,6 +1707,13 @@ static int policy_dedup() {
     const char* e = getenv("FJSP_POLICY_DEDUP");
     return !(e && e[0] == '0' && !e[1]);
 }
+// k_policy_step's split of the pickup station's and the AGV's tiles into two 32-env workgroups
+// (half the matrix-core chain of the launch's longest workgroups): on unless FJSP_POLICY_SPLIT=0
+// (A/B runs and the bit-equality test; read per launch)
+static int policy_split() {
+    const char* e = getenv("FJSP_POLICY_SPLIT");
+    return !(e && e[0] == '0' && !e[1]);
+}
 
 // fjsp_a2c_policy_step's launch (fjsp_hip.hip holds the handle): k_policy_step on the policy's
 // grid, the step's state / config / outputs and the tile hand-off buffers from the handle.
@@ -1695,6 +1728,8 @@ int fjsp_internal_policy_step(const float* feats, const int8_t* masks, int32_t n
     // envs [env_begin, env_begin + env_count): whole 64-env tiles (the caller checks the range)
     PolicyArgs A{feats, masks, n, actor_w, critic_w, seed, env_gid0, step, deterministic, actions, values, nullptr,
                  values ? (env_count + TC - 1) / TC : 0, (env_count + TA - 1) / TA, env_begin / TA, policy_xmap(), policy_dedup()};
+    A.split = policy_split() && A.xmap == 0;
+    const int actor_blocks = (NAG + (A.split ? 2 : 0)) * A.na;
     // the tiles copy their outputs out in 16-byte pieces when every tile is full and every output
     // row and state row of a tile starts 16-byte aligned (n % 64 == 0, 16-byte aligned bases)
     const uintptr_t bases = (uintptr_t)out.rewards | (uintptr_t)out.term | (uintptr_t)out.trunc | (uintptr_t)out.status |
@@ -1702,9 +1737,9 @@ int fjsp_internal_policy_step(const float* feats, const int8_t* masks, int32_t n
     StepArgs St{S, C, out.rewards, out.term, out.trunc, out.status, out.next_masks, out.feats, tile_cnt, tile_act,
                 autoreset ? STEP_AUTORESET : 0};
     if (n % TA == 0 && (bases & 15u) == 0)
-        hipLaunchKernelGGL(k_policy_step<true>, dim3((unsigned)(A.nc + NAG * A.na)), dim3(NTHR), 0, stream, A, St);
+        hipLaunchKernelGGL(k_policy_step<true>, dim3((unsigned)(A.nc + actor_blocks)), dim3(NTHR), 0, stream, A, St);
     else
-        hipLaunchKernelGGL(k_policy_step<false>, dim3((unsigned)(A.nc + NAG * A.na)), dim3(NTHR), 0, stream, A, St);
+        hipLaunchKernelGGL(k_policy_step<false>, dim3((unsigned)(A.nc + actor_blocks)), dim3(NTHR), 0, stream, A, St);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

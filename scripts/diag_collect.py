@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """A/B of the A2C collect (diagnostic): fjsp_a2c_policy_step (policy + env step in one launch)
 against fjsp_a2c_policy + fjsp_step (two launches per vector step), 256 x N per batch, the
-captured graph replayed; alternating batches, ms per batch.  Prints JSON."""
+captured graph replayed; alternating batches, ms per batch.  Prints JSON.
+
+usage: python scripts/diag_collect.py [N] [group counts ...]"""
 import importlib
 import json
 import os
@@ -50,5 +52,6 @@ def main(n=4096, T=256, reps=8, init="random", groups=(1, 2, 4, 8)):
 
 if __name__ == "__main__":
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    groups = tuple(int(g) for g in sys.argv[2:]) or (1, 2, 4, 8)
     for init in ("random", "trained"):
-        print(json.dumps(main(n, init=init)), flush=True)
+        print(json.dumps(main(n, init=init, groups=groups)), flush=True)

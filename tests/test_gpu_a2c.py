@@ -166,18 +166,22 @@ def test_policy_step_launch_equals_two_launches(M, n, T, det, graph, groups):
     assert ends >= n                                    # every env crossed an auto-reset
 
 
+@pytest.mark.parametrize("var,values", [("FJSP_POLICY_DEDUP", ("0", "1")), ("FJSP_POLICY_SPLIT", ("0", "1"))])
 @pytest.mark.parametrize("n,init", [(4096, "random"), (1000, "trained")])
-def test_station_dedup_is_bit_identical(M, n, init, monkeypatch):
-    """The station agents' MLP once per distinct input of a 64-env tile (on one 32-env column
-    tile, actor_tile) == the MLP on every env (FJSP_POLICY_DEDUP=0): every byte of the rollout
-    slabs over two batches with an update between them (the second batch acts with updated
-    weights), partial tiles, random-init and trained networks."""
+def test_policy_launch_variants_are_bit_identical(M, n, init, var, values, monkeypatch):
+    """The policy launch's work splits change which workgroup computes what, never a value:
+    the station agents' MLP once per distinct input of a 64-env tile on one 32-env column tile
+    (FJSP_POLICY_DEDUP, on by default) == the MLP on every env; the pickup station's and the
+    AGV's tiles as two 32-env workgroups each (FJSP_POLICY_SPLIT, on by default) == one 64-env
+    workgroup.  Every
+    byte of the rollout slabs over two batches with an update between them (the second batch acts
+    with updated weights), partial tiles, random-init and trained networks."""
     import os
     A, V = M["A"], M["V"]
     keys = ("feats", "masks", "actions", "values", "rewards", "term", "trunc", "status")
     runs = []
-    for dedup in ("0", "1"):
-        monkeypatch.setenv("FJSP_POLICY_DEDUP", dedup)
+    for v in values:
+        monkeypatch.setenv(var, v)
         L = A.VecMultiAgentA2C(V.FJSPVecEnv(n), batch_size=64, seed=4)
         if init == "trained":
             L.load_state_dicts(A.load_npz_weights(os.path.join(os.path.dirname(__file__), "golden", "trained_policy.npz")))
