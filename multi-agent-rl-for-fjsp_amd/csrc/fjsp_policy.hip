@@ -82,6 +82,7 @@ constexpr int LDS_BYTES = X_BYTES + H_BYTES + W3_BYTES;
 // the actor's input planes end here; the station dedup's slot / input words fit in the rest of X
 constexpr int ACT_X_BYTES = NP * XPA * 2;
 static_assert(A_DPAD * 32 == NTHR, "a half tile's inputs: one per thread");
+static_assert(NP * HPC * 2 <= H_BYTES && NWAVE * 8 * TA * 4 <= H_BYTES, "one column tile's whole h1, then the logit partials");
 static_assert(ACT_X_BYTES + (64 + 4 + 3 * 64) * 4 <= X_BYTES, "station dedup words beside the actor inputs");
 static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
 
@@ -449,6 +450,35 @@ __device__ __forceinline__ void actor_mlp(const PolicyArgs& A, int role, unsigne
     __bf16* s_h = reinterpret_cast<__bf16*>(s_mem + X_BYTES);
     float* s_part = reinterpret_cast<float*>(s_mem + X_BYTES);
     const float* s_w3 = reinterpret_cast<const float*>(s_mem + X_BYTES + H_BYTES);
+    if constexpr (NC == 1) {
+        // one column tile: the whole h1 [NP][32][256 + 8] fits the h buffer, so layer 1 runs on
+        // all eight waves at once (row tile = wave) and layer 2 sums its 16 blocks in one pass
+        // (the same block order as the two halves: bit-identical)
+        WRing<1> r1;
+        wring_start(r1, wblocks<1, 1>(W1, wave, 0, lane));
+        const Row16 b1 = load_rows(B1, 32 * wave, lane);
+        __syncthreads();
+        PST(3, __builtin_amdgcn_s_memtime());
+        f32x16 a1[1];
+        zero_acc<1>(a1);
+        mfma_rows<1, XSA, XPA, 1>(r1, wblocks<1, 1>(W1, wave, 0, lane), s_x, 0, lane, a1);
+        WRing<HID / 16> r2;
+        wring_start(r2, wblocks<HID / 16, HID / 16>(W2, wave, 0, lane));
+        store_planes<HSC, HPC>(a1[0], 32 * wave, 0, b1, s_h, lane);
+        __syncthreads();
+        PST(4, __builtin_amdgcn_s_memtime());
+        f32x16 acc[1];
+        zero_acc<1>(acc);
+        mfma_rows<HID / 16, HSC, HPC, 1>(r2, wblocks<HID / 16, HID / 16>(W2, wave, 0, lane), s_h, 0, lane, acc);
+        const Row16 b2 = load_rows(B2, 32 * wave, lane);
+        __syncthreads();                           // every wave has read h1 (s_part overlays it)
+        PST(7, __builtin_amdgcn_s_memtime());
+        if (c_nact[role] == 8) logit_partials<8, 1>(acc, b2, s_w3, s_part, wave, lane);
+        else logit_partials<3, 1>(acc, b2, s_w3, s_part, wave, lane);
+        __syncthreads();
+        PST(8, __builtin_amdgcn_s_memtime());
+        return;
+    }
     const int rt1 = wave & 3, ct1 = wave >> 2;   // layer-1 tile of each half
     const bool l1 = NC == 2 || ct1 == 0;          // with one column tile, waves 4..7 have no layer-1 tile
     WRing<1> r1;
