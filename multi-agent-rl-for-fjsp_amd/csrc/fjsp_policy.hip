@@ -9,9 +9,13 @@
 // Grid (1-D, 512 threads = 8 wavefronts per workgroup, two workgroups per CU: 70 KB of LDS):
 //   blocks [0, nc)            the critic on tiles of 32 envs (values wanted)
 //   blocks [nc, nc + 8 na)    actor (b - nc) / na on tiles of 64 envs (actions wanted)
+// (k_policy_step, the collect's launch, adds the env step of each tile and, by default, runs the
+// pickup station's and the AGV's tiles as two 32-env workgroups each: 10 na actor blocks.)
 // The hidden activations never leave LDS, as bf16 planes (below) [3][env][k]:
-//   actor:  x [3][64][16+8]; h1 in two K halves [3][64][128+8] (rows 0..127, then 128..255:
-//           layer 2 is summed over the two halves, so one half-size buffer serves)
+//   actor:  x [3][64][16+8]; on two column tiles h1 in two K halves [3][64][128+8] (rows 0..127,
+//           then 128..255: layer 2 is summed over the two halves, so one half-size buffer
+//           serves); on one column tile (a 32-env half, or a station tile's <= 32 distinct
+//           inputs) the whole h1 [3][32][256+8]
 //   critic: x [3][32][48+8]; h1, then h2 [3][32][256+8] (in place across a barrier)
 // Every layer with K >= 16 runs on v_mfma_f32_32x32x16_bf16 with f32 operands split into three
 // bf16 planes (six plane products per 16-deep block, below).  Actor: each wave owns 32 rows of
