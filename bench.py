@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=6.0,
                     help="wall budget of each CPU baseline leg (single thread, all cores)")
     ap.add_argument("--no-step-mode", action="store_true", help="skip the one-launch-per-step measurement")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the reference-API (FJSPParallelEnv.step, one env) latency measurement")
     ap.add_argument("--workload", choices=["step", "a2c"], default="step",
                     help="step: env-step throughput (the headline metric); a2c: the batched A2C "
                          "training loop (BASELINE configs 4/5; one bench step = one A2C batch)")
@@ -138,6 +140,92 @@ def cpu_baseline(args):
                       f"{cores} threads (one per available core) {wn:.1f}s wall",
             "host": info,
             "reference_python_1core": "8.0-9.0k env-steps/s (measured in the build container, BASELINE.md)"}
+
+
+REF_PY_STEP_US = 115.0   # the reference FJSPSimulation.step, 1 core (112.9-115.6 us)
+
+
+def dropin_latency(dev, steps=2000, warm=200):
+    """The reference-API path a2c.py drives (a2c.py:294-305): one FJSPParallelEnv.step(dict) per
+    Python iteration on ONE env, then the visualiser's reads of simulation.agv.position and
+    agv.carrying_tray, the episode restarted with reset() when env.agents empties (the loop's
+    `while self.env.agents`).  Wall time per call on this host, beside the reference's ~115 us.
+    Also: the same without the agv reads, and FJSPSimulation.step alone split into its parts
+    (kernel time from the handle's events)."""
+    W = importlib.import_module("multi-agent-rl-for-fjsp_amd.FJSPParallelEnvWrapper")
+    env = W.FJSPParallelEnv()
+    env.reset(seed=0, options={"num_orders": 30})
+    rng = np.random.default_rng(0)
+    n_act = [env.action_space(a).n for a in env.possible_agents]
+    acts = [{a: int(rng.integers(0, n_act[i])) for i, a in enumerate(env.possible_agents)} for _ in range(steps)]
+    sim = env.unwrapped.simulation
+
+    def loop(agv_reads, n):
+        resets = 0
+        t0 = time.perf_counter()
+        for t in range(n):
+            env.step(acts[t])
+            if agv_reads:
+                _ = sim.agv.position
+                _ = sim.agv.carrying_tray is not None
+            if not env.agents:
+                env.reset(options={"num_orders": 30})
+                resets += 1
+        return (time.perf_counter() - t0) / n * 1e6, resets
+
+    loop(True, warm)
+    with_agv, resets = loop(True, steps)
+    no_agv, _ = loop(False, steps)
+    # the kernel alone (the handle's events around each launch), 200 steps
+    nat = importlib.import_module("multi-agent-rl-for-fjsp_amd._native")
+    k = []
+    env.reset(seed=1, options={"num_orders": 30})
+    nat.check(nat.lib().fjsp_set_option(sim._venv.handle, b"timing", 1))
+    for t in range(200):
+        env.step(acts[t])
+        k.append(sim._venv.last_kernel_ms() * 1e3)
+        if not env.agents:
+            env.reset(options={"num_orders": 30})
+    nat.check(nat.lib().fjsp_set_option(sim._venv.handle, b"timing", 0))
+    return {"dropin_n1_us_per_step": with_agv, "dropin_n1_no_agv_reads_us_per_step": no_agv,
+            "kernel_us_median": float(np.median(k)), "resets": resets, "steps": steps,
+            "reference_us_per_step": REF_PY_STEP_US,
+            "speedup_vs_reference": REF_PY_STEP_US / with_agv,
+            "note": "FJSPParallelEnv.step(dict) + a2c.py:298-305's agv.position / carrying_tray reads, one env, "
+                    "random actions, reset when env.agents empties; reference: SURVEY.md App. E (1 core, same "
+                    "container class), not re-timed on this box (the reference never travels)"}
+
+
+def host_action_step(env, dev, N, K=200):
+    """FJSPVecEnv.step with actions handed over from HOST memory each step (a CPU-side policy):
+    pinned u8[8][N] -> H2D -> k_step -> outputs in HBM, one synchronisation per step; and the
+    same with the step's lean outputs (obs, masks, rewards, term, trunc) copied back to host."""
+    vec_env = importlib.import_module("multi-agent-rl-for-fjsp_amd.vec_env")
+    nact = np.array([3, 8, 3, 3, 3, 3, 3, 3], np.int64).reshape(8, 1)
+    rng = np.random.default_rng(1)
+    host = [torch.from_numpy(((rng.integers(0, 256, (8, N)) * nact) >> 8).astype(np.uint8)).pin_memory()
+            for _ in range(K)]
+    sbuf = vec_env.Buffers(1, N, dev, infos=False)
+    back = {k: torch.empty(getattr(sbuf, k).shape, dtype=getattr(sbuf, k).dtype).pin_memory()
+            for k in ("obs_i32", "obs_i8", "obs_f32", "masks", "rewards", "term", "trunc")}
+
+    def run(copy_back):
+        t0 = time.perf_counter()
+        for t in range(K):
+            env.step(host[t], buffers=sbuf)
+            if copy_back:
+                for k, h in back.items():
+                    h.copy_(getattr(sbuf, k), non_blocking=True)
+            torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / K * 1e6
+
+    run(False)
+    a = run(False)
+    b = run(True)
+    return {"envs": N, "us_per_step": a, "value": N / (a * 1e-6), "unit": "env-steps/s",
+            "us_per_step_with_outputs_to_host": b, "value_with_outputs_to_host": N / (b * 1e-6),
+            "note": "actions from pinned host memory every step (H2D + k_step + sync); the second figure also "
+                    "copies obs/masks/rewards/term/trunc back to pinned host memory"}
 
 
 def load_pmc(workload):
@@ -419,6 +507,16 @@ def main():
                     "kernel": env.last_kernel(), "algo_bytes_per_env_step": ALGO_BYTES_STEP,
                     "achieved_GBs": ALGO_BYTES_STEP * N / (kms * 1e-3) / 1e9,
                     "note": "one launch per step, actions u8[8][N] resident in HBM (rank 0)"}
+        if rank == 0:
+            per_step["host_actions"] = host_action_step(env, dev, N)
+
+    # the reference-API path itself (FJSPParallelEnv.step with dict actions, one env)
+    dropin = None
+    if rank == 0 and world == 1 and not args.no_dropin:
+        try:
+            dropin = dropin_latency(dev)
+        except Exception as e:   # the headline metric does not depend on this leg
+            dropin = {"error": f"{type(e).__name__}: {e}"}
 
     # the same kernel at 16x the envs (65 536 on this GPU): how far the env-step approaches the
     # HBM roofline once occupancy allows (the headline stays the 4 096-env workload)
@@ -525,6 +623,8 @@ def main():
             "cpu_baseline": cpu,
             "chunk_200": chunk_200,
             "per_step_launch": per_step,
+            "dropin_n1_us_per_step": dropin.get("dropin_n1_us_per_step") if dropin else None,
+            "dropin": dropin,
             "a2c_training": a2c,
             "scale_16x_envs": scale,
             "state_bytes_per_env": env.state_bytes_per_env(),

@@ -31,6 +31,7 @@ CONFIG = {"num_trays": 1000, "tray_capacity": 5, "num_packaging_blue": 2, "num_p
           "max_episode_steps": 200}
 
 _AGENT_INDEX = {a: i for i, a in enumerate(AGENTS)}
+_CANON = list(range(8))
 _AGENT_TYPE = {"pickup_station": "PICKUP_STATION", "agv": "AGV", "small_machine": "SMALL_MACHINE",
                "big_machine": "BIG_MACHINE"}
 
@@ -47,13 +48,17 @@ def native_config(config):
 
 
 class _Packed:
-    """All per-step outputs of one env in one device slab -> one D2H copy per step."""
+    """All per-step outputs of one env in one pinned host record that the kernels write directly
+    (zero-copy: hipHostMalloc'd memory is mapped into the GPU's address space), so a step costs one
+    launch and one stream synchronisation, no copy call.  The actions are read the same way from a
+    pinned 8-byte row."""
     FIELDS = [("obs_i32", np.int32, 20), ("obs_i8", np.int8, 12), ("obs_f32", np.float32, 6),
               ("masks", np.int8, 29), ("rewards", np.float64, 8), ("term", np.uint8, 1), ("trunc", np.uint8, 1),
               ("results", np.uint32, 8), ("orders_completed", np.int32, 1), ("packaged", np.int32, 1),
               ("sim_time", np.float64, 1), ("status", np.uint32, 1)]
+    OBS = ("obs_i32", "obs_i8", "obs_f32", "masks", "status")
 
-    def __init__(self, device):
+    def __init__(self):
         off = 0
         self.layout = {}
         for name, dt, n in self.FIELDS:
@@ -61,37 +66,39 @@ class _Packed:
             self.layout[name] = (off, np.dtype(dt), n)
             off += np.dtype(dt).itemsize * n
         self.nbytes = (off + 7) & ~7
-        self.dev = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
         self.host = torch.zeros(self.nbytes, dtype=torch.uint8).pin_memory()
         self.np = self.host.numpy()
-
-    def struct(self, obs_only=False):
-        o = nat.fjsp_out()
-        base = self.dev.data_ptr()
+        self.view = {name: self.np[off: off + dt.itemsize * n].view(dt) for name, (off, dt, n) in self.layout.items()}
+        base = self.host.data_ptr()
+        self.out_full, self.out_obs = nat.fjsp_out(), nat.fjsp_out()
         for name, (off, dt, n) in self.layout.items():
-            if obs_only and name not in ("obs_i32", "obs_i8", "obs_f32", "masks", "status"):
-                continue
-            setattr(o, name, base + off)
-        return o
+            setattr(self.out_full, name, base + off)
+            if name in self.OBS:
+                setattr(self.out_obs, name, base + off)
+        self.ref_full, self.ref_obs = ctypes.byref(self.out_full), ctypes.byref(self.out_obs)
 
-    def fetch(self):
-        self.host.copy_(self.dev, non_blocking=False)
-        return {name: self.np[off: off + dt.itemsize * n].view(dt) for name, (off, dt, n) in self.layout.items()}
+    def snapshot(self):
+        """This step's record as fresh arrays (the next launch overwrites the pinned one)."""
+        c = self.np.copy()
+        return {name: c[off: off + dt.itemsize * n].view(dt) for name, (off, dt, n) in self.layout.items()}
 
 
 class _AGVView:
+    """simulation.agv as a2c.py:298-305 reads it: position and carrying_tray come from the last
+    observation (AGVAgent.get_observation fields position / carrying_tray / tray_product_count,
+    AGVAgent.py:60-64), so reading them costs no device access."""
     def __init__(self, sim):
         self._sim = sim
 
     @property
     def position(self):
-        v = self._sim._view()
-        return (v.agv_row, v.agv_col)
+        o = self._sim._last_i32
+        return (int(o[7]), int(o[8]))
 
     @property
     def carrying_tray(self):
-        v = self._sim._view()
-        return _TrayView(v.agv_tray_count) if v.agv_carrying else None
+        o = self._sim._last_i32
+        return _TrayView(int(o[10])) if o[9] else None
 
     is_moving = False   # the AGV always arrives within the step (8 / agv_speed < step_size)
 
@@ -153,9 +160,15 @@ class FJSPSimulation:
         self.config = config or CONFIG
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self._venv = FJSPVecEnv(1, device=self.device, config=native_config(self.config))
-        self._packed = _Packed(self.device)
-        self._act_host = torch.zeros(8, dtype=torch.uint8).pin_memory()
-        self._act_dev = torch.zeros(8, 1, dtype=torch.uint8, device=self.device)
+        self._h = self._venv.handle
+        self._L = nat.lib()
+        # one launch per step: no per-launch event pair (fjsp_last_kernel_ms), the facade never reads it
+        nat.check(self._L.fjsp_set_option(self._h, b"timing", 0))
+        self._packed = _Packed()
+        self._act_host = torch.zeros(8, dtype=torch.uint8).pin_memory()   # read by the kernel in place
+        self._act_np = self._act_host.numpy()
+        self._act_ptr = ctypes.c_void_p(self._act_host.data_ptr())
+        self._stream = None
         self.reward_calculator = RewardModel()
         self._pushed_weights = None
         self.agents = {a: _AgentView(a) for a in AGENTS}
@@ -166,11 +179,24 @@ class FJSPSimulation:
         self._orders_total = 0
         self._last_obs = None
         self._viewcache = None
+        self._infocache = {}
         # an empty episode (no orders, no RNG draws), like a freshly constructed reference sim
-        nat.check(nat.lib().fjsp_reset(self._venv.handle, None, None, 0, ctypes.byref(self._packed.struct(True))))
-        self._last_obs = self._obs_from(self._packed.fetch())
+        self._bind_stream()
+        nat.check(self._L.fjsp_reset(self._h, None, None, 0, self._packed.ref_obs))
+        self._wait()
+        self._take_obs(self._packed.snapshot())
 
     # ------------------------------------------------------------------ internals
+    def _bind_stream(self):
+        """Launch on torch's current stream of the device (re-read every call, as vec_env does)."""
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        if s != self._stream:
+            nat.check(self._L.fjsp_set_stream(self._h, ctypes.c_void_p(s)))
+            self._stream = s
+
+    def _wait(self):
+        nat.check(self._L.fjsp_sync(self._h))
+
     def _view(self):
         if self._viewcache is None:
             self._viewcache = self._venv.read_env(0)
@@ -180,12 +206,20 @@ class FJSPSimulation:
         w = self.reward_calculator.weights()
         if w != self._pushed_weights:
             rw = nat.fjsp_reward_weights(*w)
-            nat.check(nat.lib().fjsp_set_reward_weights(self._venv.handle, ctypes.byref(rw)))
+            nat.check(self._L.fjsp_set_reward_weights(self._h, ctypes.byref(rw)))
             self._pushed_weights = w
 
-    @staticmethod
-    def _obs_from(p):
-        return obs_dicts(p["obs_i32"], p["obs_i8"], p["obs_f32"], p["masks"])
+    def _take_obs(self, p):
+        self._last_i32 = p["obs_i32"]
+        self._last_obs = obs_dicts(p["obs_i32"], p["obs_i8"], p["obs_f32"], p["masks"])
+        return self._last_obs
+
+    def _info(self, i, a, act, word):
+        key = (i, act, word)
+        d = self._infocache.get(key)
+        if d is None:
+            d = self._infocache[key] = decode_result(a, act, word)
+        return dict(d)
 
     # ------------------------------------------------------------------ reference API
     def reset(self, seed=None, num_orders=None):
@@ -194,56 +228,58 @@ class FJSPSimulation:
             np.random.seed(seed)
         n = num_orders if num_orders is not None else 30
         st = np.random.get_state()
+        self._bind_stream()
         self._venv.mt_set(0, np.asarray(st[1], np.uint32), int(st[2]))
-        torch.cuda.current_stream(self.device).synchronize()
-        nat.check(nat.lib().fjsp_set_stream(self._venv.handle,
-                                            ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
-        nat.check(nat.lib().fjsp_reset(self._venv.handle, None, None, int(n), ctypes.byref(self._packed.struct(True))))
-        key, pos = self._venv.mt_get(0)
+        nat.check(self._L.fjsp_reset(self._h, None, None, int(n), self._packed.ref_obs))
+        key, pos = self._venv.mt_get(0)   # synchronises the stream
         np.random.set_state((st[0], key, pos, st[3], st[4]))
         self.current_step = 0
         self.total_products_packaged = 0
         self.sim_time = 0
         self._orders_total = int(n)
         self._viewcache = None
-        obs = self._obs_from(self._packed.fetch())
-        self._last_obs = obs
+        obs = self._take_obs(self._packed.snapshot())
         return obs, {a: {} for a in AGENTS}
 
     def step(self, actions):
         """FJSPSimulation.step (FJSPSimulation.py:144-242)."""
-        codes = np.full(8, 255, np.uint8)
+        codes = self._act_np
+        codes.fill(255)   # an agent absent from the dict does not act
         order = []
         for k, v in actions.items():
             i = _AGENT_INDEX.get(k)
             if i is None or i in order:
                 continue
-            codes[i] = _action_code(v)
+            codes[i] = v if (type(v) is int and 0 <= v <= 253) else _action_code(v)
             order.append(i)
-        order += [i for i in range(8) if i not in order]
+        canon = order == _CANON
+        ord_arr = None
+        if not canon:
+            order += [i for i in range(8) if i not in order]
+            canon = order == _CANON
+            ord_arr = None if canon else (ctypes.c_uint8 * 8)(*order)
         self._push_weights()
-        self._act_host.numpy()[:] = codes
-        self._act_dev.view(-1).copy_(self._act_host, non_blocking=True)
-        self._venv._sync_stream()
-        canon = order == list(range(8))
-        ord_arr = None if canon else (ctypes.c_uint8 * 8)(*order)
-        nat.check(nat.lib().fjsp_step(self._venv.handle, ctypes.c_void_p(self._act_dev.data_ptr()), ord_arr, 0,
-                                      ctypes.byref(self._packed.struct())))
-        p = self._packed.fetch()
+        self._bind_stream()
+        nat.check(self._L.fjsp_step(self._h, self._act_ptr, ord_arr, 0, self._packed.ref_full))
+        self._wait()
+        p = self._packed.snapshot()
         self._viewcache = None
-        obs = self._obs_from(p)
-        self._last_obs = obs
-        rewards = {a: float(p["rewards"][i]) for i, a in enumerate(AGENTS)}
+        obs = self._take_obs(p)
+        rw = p["rewards"].tolist()
+        rewards = dict(zip(AGENTS, rw))
         term = bool(p["term"][0])
         trunc = bool(p["trunc"][0])
         self.sim_time = float(p["sim_time"][0])
         self.total_products_packaged = int(p["packaged"][0])
         oc = int(p["orders_completed"][0])
+        res = p["results"].tolist()
         infos = {}
         for i, a in enumerate(AGENTS):
             act = actions.get(a, 0)
-            infos[a] = {"action_result": decode_result(a, act, p["results"][i]), "sim_time": self.sim_time,
-                        "orders_completed": oc, "total_products_packaged": self.total_products_packaged}
+            d = self._info(i, a, act, res[i]) if type(act) is int else decode_result(a, act, res[i])
+            d_all = {"action_result": d, "sim_time": self.sim_time, "orders_completed": oc,
+                     "total_products_packaged": self.total_products_packaged}
+            infos[a] = d_all
         self.current_step += 1
         return obs, rewards, {a: term for a in AGENTS}, {a: trunc for a in AGENTS}, infos
 

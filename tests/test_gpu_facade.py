@@ -77,6 +77,13 @@ def test_parallel_env_replays_golden(M, idx):
             assert info[a]["sim_time"] == tr.sim_time[t]
             assert info[a]["orders_completed"] == tr.orders_completed[t]
             assert info[a]["total_products_packaged"] == tr.packaged[t]
+        # a2c.py:298-305 reads: taken from the observation, equal to the device state's AGV
+        sim = env.unwrapped.simulation
+        v = sim._venv.read_env(0)
+        assert sim.agv.position == (v.agv_row, v.agv_col), (tr.name, t)
+        ct = sim.agv.carrying_tray
+        assert (ct is not None) == bool(v.agv_carrying), (tr.name, t)
+        assert (len(ct) if ct is not None else 0) == v.agv_tray_count, (tr.name, t)
         if term["agv"] or trunc["agv"]:
             assert env.agents == []
             obs, _ = env.reset(options={"num_orders": tr.num_orders})    # seed=None: numpy stream continues
