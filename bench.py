@@ -315,7 +315,29 @@ def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=
         learner.update()
         learner.roll_over()
         torch.cuda.synchronize()
-        out["update_stage_ms"] = dict(learner.exchange_timing)
+        st = dict(learner.exchange_timing)
+        if dist:
+            # every rank's stages (the same names on every rank under one exchange): the max over
+            # ranks, as the batch waits for the slowest rank at each collective
+            names = sorted(st)
+            t = torch.tensor([st[k] for k in names], device=env.device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            st = dict(zip(names, t.tolist()))
+            if exchange == "shard":
+                # per-rank record traffic of the stats batch: bytes sent to other ranks and records
+                world_ = dist.get_world_size()
+                v = torch.zeros(3, world_, device=env.device, dtype=torch.float64)
+                si = learner.shard_info
+                v[:, dist.get_rank()] = torch.tensor([si.get("bytes_sent_to_other_ranks", 0),
+                                                      si.get("actor_records_received", 0),
+                                                      si.get("critic_records_received", 0)], dtype=torch.float64)
+                dist.all_reduce(v, op=dist.ReduceOp.SUM)
+                out["shard_bytes_sent_by_rank"] = [int(x) for x in v[0].tolist()]
+                out["shard_records_received_by_rank"] = {"actor": [int(x) for x in v[1].tolist()],
+                                                         "critic": [int(x) for x in v[2].tolist()]}
+        out["update_stage_ms"] = st
+        out["update_stage_ms_note"] = ("synchronised stage timers of one extra batch, max over ranks" if dist else
+                                       "synchronised stage timers of one extra batch")
         learner.exchange_timing = None
         learner.collect()
         torch.cuda.synchronize()

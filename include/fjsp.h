@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define FJSP_ABI_VERSION 9
+#define FJSP_ABI_VERSION 10
 
 #define FJSP_NUM_AGENTS 8      /* pickup, agv, small, big, pkg_blue_1, pkg_blue_2, pkg_red, pkg_green */
 #define FJSP_OBS_I32 20        /* pickup 7 + agv 13 (position = 2) int32 observation fields */
@@ -178,7 +178,12 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
  * wave's hand-off before it gives up and flags FJSP_STATUS_SPIN_TIMEOUT / fjsp_faults); "test_stall"
  * (0..2^20, default 0; tests only: later k_step_ag and k_step_pipe<lds,2emit,predraw> launches
  * run a test build in which workgroup 0's owner wave sleeps value x ~8k cycles before its first
- * step, so that the other waves' bounded waits give up and the give-up path runs).  spin_cap and test_stall are not part of a snapshot. */
+ * step, so that the other waves' bounded waits give up and the give-up path runs).  spin_cap and test_stall are not part of a snapshot.
+ * "legacy_step" (0/1, default 0: fjsp_step in the canonical dict order launches r05's k_step<canon>
+ * instead of k_step_pf; identical results, for A/B runs).
+ * Library-wide (h may be NULL; ABI 10): "policy_xmap" (0..3, default 0), "policy_dedup" (0/1,
+ * default 1), "policy_split" (0/1, default 1) — the variants of the A2C policy launches listed at
+ * fjsp_a2c_policy; identical results.  Nothing is read from the process environment. */
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value);
 int fjsp_num_envs(const fjsp_handle* h);
 /* Bytes of device state per env (HBM footprint of the SoA state). */
@@ -267,10 +272,11 @@ int64_t fjsp_snapshot_bytes(const fjsp_handle* h);
  * probabilities f32 [8][8][N] (NULL to skip).  actions == NULL: the critic's values only (masks,
  * actor_w and seed may then be NULL; e.g. the batch-end bootstrap V(s_T), a2c.py:321-332);
  * values == NULL: the actors only (critic_w may be NULL).  Stream-ordered on `stream`.
- * A/B switches read per launch (outputs bit-identical under every setting): FJSP_POLICY_XMAP=0..3
- * (workgroup -> XCD order), FJSP_POLICY_DEDUP=0 (the station agents' MLP on every env instead
- * of once per distinct input of a 64-env tile), FJSP_POLICY_SPLIT=0 (fjsp_a2c_policy_step: the
- * pickup station's and the AGV's tiles on one 64-env workgroup instead of two 32-env ones). */
+ * Variants read per launch (fjsp_set_option(NULL, ...); outputs bit-identical under every setting):
+ * policy_xmap 0..3 (workgroup -> XCD order; 1-3 also turn the split below off), policy_dedup 0
+ * (the station agents' MLP on every env instead of once per distinct input of a 64-env tile),
+ * policy_split 0 (fjsp_a2c_policy_step: the pickup station's and the AGV's tiles on one 64-env
+ * workgroup instead of two 32-env ones). */
 #define FJSP_POLICY_ACTOR_DPAD 16
 #define FJSP_POLICY_CRITIC_DPAD 48
 #define FJSP_POLICY_ACTOR_FLOATS (3 * 256 * 16 / 2 + 256 + 3 * 256 * 256 / 2 + 256 + 8 * 256 + 16)

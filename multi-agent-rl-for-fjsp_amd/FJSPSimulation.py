@@ -169,8 +169,10 @@ class FJSPSimulation:
         self._act_np = self._act_host.numpy()
         self._act_ptr = ctypes.c_void_p(self._act_host.data_ptr())
         self._stream = None
+        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self.reward_calculator = RewardModel()
         self._pushed_weights = None
+        self._pushed_rc = None
         self.agents = {a: _AgentView(a) for a in AGENTS}
         self.agv = _AGVView(self)
         self.current_step = 0
@@ -188,8 +190,9 @@ class FJSPSimulation:
 
     # ------------------------------------------------------------------ internals
     def _bind_stream(self):
-        """Launch on torch's current stream of the device (re-read every call, as vec_env does)."""
-        s = torch.cuda.current_stream(self.device).cuda_stream
+        """Launch on torch's current stream of the device (re-read every call, as vec_env does;
+        the raw handle query is the cheap form of torch.cuda.current_stream(device).cuda_stream)."""
+        s = torch._C._cuda_getCurrentRawStream(self._dev_index)
         if s != self._stream:
             nat.check(self._L.fjsp_set_stream(self._h, ctypes.c_void_p(s)))
             self._stream = s
@@ -203,11 +206,16 @@ class FJSPSimulation:
         return self._viewcache
 
     def _push_weights(self):
-        w = self.reward_calculator.weights()
-        if w != self._pushed_weights:
-            rw = nat.fjsp_reward_weights(*w)
-            nat.check(self._L.fjsp_set_reward_weights(self._h, ctypes.byref(rw)))
-            self._pushed_weights = w
+        """The kernel's reward table follows reward_calculator's weights (read before every step,
+        like the reference's step reads them); re-uploaded only when an attribute changed."""
+        rc = self.reward_calculator
+        d = vars(rc)
+        if rc is self._pushed_rc and d == self._pushed_weights:
+            return
+        w = rc.weights()
+        rw = nat.fjsp_reward_weights(*w)
+        nat.check(self._L.fjsp_set_reward_weights(self._h, ctypes.byref(rw)))
+        self._pushed_rc, self._pushed_weights = rc, dict(d)
 
     def _take_obs(self, p):
         self._last_i32 = p["obs_i32"]

@@ -74,7 +74,7 @@ POLICY_ACTOR_DPAD, POLICY_CRITIC_DPAD = 16, 48
 POLICY_ACTOR_FLOATS = 3 * 256 * 16 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 8 * 256 + 16
 POLICY_CRITIC_FLOATS = 3 * 256 * 48 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 3 * 128 * 256 // 2 + 128 + 128 + 16
 CRITIC_FUSED_PW = 2 * 256 + 2 * 128 + 4   # floats per tile of fjsp_a2c_critic_fused's partial sums
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lib = None
 

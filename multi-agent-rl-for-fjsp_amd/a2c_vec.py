@@ -306,16 +306,16 @@ def critic_onepass(critic, x, coef):
                                 n[4].bias, n[6].weight, n[6].bias)
 
 
-# the grouped update's critic through the fused forward kernel (FJSP_CRITIC_FUSED=0: PyTorch GEMMs,
-# for A/B runs)
-critic_fused = os.environ.get("FJSP_CRITIC_FUSED", "1") != "0"
+# Implementation switches of the grouped update (module attributes, set from Python by the A/B
+# scripts and the tests; every setting computes the same losses and gradients):
+# the critic through the fused forward kernel (False: PyTorch GEMMs)
+critic_fused = True
 # ... and its loss, forward and backward in one pass per distinct state (fjsp_a2c_critic_fused;
-# FJSP_CRITIC_ONEPASS=0: the forward kernel, the per-sample loss through autograd, the value head
-# and backward kernels)
-critic_onepass_on = os.environ.get("FJSP_CRITIC_ONEPASS", "1") != "0"
+# False: the forward kernel, the per-sample loss through autograd, the value head and backward kernels)
+critic_onepass_on = True
 
-# its backward through the two 256-wide layers in one kernel (FJSP_CRITIC_BWD=0: GEMMs + ReLU kernels)
-critic_bwd_fused = os.environ.get("FJSP_CRITIC_BWD", "1") != "0"
+# its backward through the two 256-wide layers in one kernel (False: GEMMs + ReLU kernels)
+critic_bwd_fused = True
 
 
 def feature_rows(f3):
@@ -615,14 +615,16 @@ def group_keys(feats, rows=None):
                       row_keys(feats.permute(1, 0, 2).reshape(GLOBAL_DIM, T * N))[None]])
 
 
+group_buckets = True   # False: exact group counts (A/B)
+
+
 def bucket(u):
     """A group count rounded up to a coarse bucket (1/16 to 1/8 of the count: ≤ 12.5 % more
     columns, ~6 % on average), so that the update's shapes (and the library kernels chosen for
     them) repeat from batch to batch.  Padding groups own no samples: computed, never gathered,
-    zero gradient.  FJSP_GROUP_BUCKETS=0: exact counts."""
-    import os
+    zero gradient.  group_buckets = False: exact counts."""
     u = int(u)
-    if os.environ.get("FJSP_GROUP_BUCKETS", "1") == "0" or u <= 64:
+    if not group_buckets or u <= 64:
         return u
     step = 1 << max(5, u.bit_length() - 4)
     return -(-u // step) * step
@@ -1064,7 +1066,7 @@ def pack_mfma(W):
     return pack_mfma_torch(W)
 
 
-pack_kernel_on = os.environ.get("FJSP_PACK_KERNEL", "1") != "0"
+pack_kernel_on = True   # False: the weight packing in torch ops (A/B)
 
 
 def pack_mfma_torch(W):
@@ -1485,9 +1487,15 @@ class VecMultiAgentA2C:
             b = self._bufs
             T = self.batch_size
             info = {}
+            stage = None
+            if self.exchange_timing is not None:   # the bench's stats batch: every stage synchronised
+                clock = [self._mark("shard_gae", t0)]
+
+                def stage(name):
+                    clock[0] = self._mark("shard_" + name, clock[0])
             al, cl = SL.update_sharded(self.actors, self.critic, self.optim_actor, self.optim_critic, b["feats"][:T],
                                        b["masks"][:T], b["actions"], ret, adv, self.gidx, self.midx, self.entropy_coef,
-                                       self.max_grad_norm, self.group, self.dedup, self.grad_probe, info)
+                                       self.max_grad_norm, self.group, self.dedup, self.grad_probe, info, stage)
             self.shard_info = info
             self._mark("learn", t0)
         else:
@@ -1561,8 +1569,8 @@ class VecMultiAgentA2C:
     def exchange_bytes_per_batch(self):
         """Bytes one rank sends per batch: exchange="gather" the transition slab; "shard" the
         records the last batch sent to other ranks (measured: the combiner's output varies)."""
-        if self.exchange == "shard":
-            return self.shard_info.get("bytes_sent_to_other_ranks")
+        if self.exchange == "shard":   # 0 before the first update has measured it
+            return self.shard_info.get("bytes_sent_to_other_ranks", 0)
         T, N = self.batch_size, self.N
         per_env_step = GLOBAL_DIM * 4 + 29 + NA + NA * 8 + 4 + 1
         return T * N * per_env_step + N * 4

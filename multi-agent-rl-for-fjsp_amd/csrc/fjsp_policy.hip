@@ -30,6 +30,7 @@
 // reference's greedy actions on its trained policy.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "../../include/fjsp.h"
 #include "fjsp_stamps.h"
@@ -1729,24 +1730,29 @@ __global__ void __launch_bounds__(256) k_value_head_grad(const float* __restrict
 
 int fjsp_internal_fail(const char* msg);
 
-// actor_block's order for the policy launches: FJSP_POLICY_XMAP=0..3 (A/B runs; read per launch,
-// so a captured graph keeps the order it was captured with), default 0
-static int policy_xmap() {
-    const char* e = getenv("FJSP_POLICY_XMAP");
-    return (e && e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : 0;
-}
-// the station agents' in-tile dedup (actor_tile): on unless FJSP_POLICY_DEDUP=0 (A/B runs and the
-// bit-equality test; read per launch)
-static int policy_dedup() {
-    const char* e = getenv("FJSP_POLICY_DEDUP");
-    return !(e && e[0] == '0' && !e[1]);
-}
-// k_policy_step's split of the pickup station's and the AGV's tiles into two 32-env workgroups
-// (half the matrix-core chain of the launch's longest workgroups): on unless FJSP_POLICY_SPLIT=0
-// (A/B runs and the bit-equality test; read per launch)
-static int policy_split() {
-    const char* e = getenv("FJSP_POLICY_SPLIT");
-    return !(e && e[0] == '0' && !e[1]);
+// Library-wide variants of the policy launches, set with fjsp_set_option(NULL or any handle,
+// "policy_xmap" | "policy_dedup" | "policy_split", v) (A/B runs and the bit-identity tests; read
+// per launch, so a captured graph keeps the variant it was captured with).  Every setting gives
+// byte-identical outputs.
+//   policy_xmap 0..3: actor_block's workgroup -> XCD order (0, the default: none).  Orders 1-3
+//     lay the launch out per XCD and so run without the split below.
+//   policy_dedup 0/1: the station agents' MLP once per distinct input of a 64-env tile (1, default)
+//     or on every env.
+//   policy_split 0/1: k_policy_step's pickup-station and AGV tiles as two 32-env workgroups each
+//     (1, default: half the matrix-core chain of the launch's longest workgroups) or one.
+static int g_policy_xmap = 0, g_policy_dedup = 1, g_policy_split = 1;
+static int policy_xmap() { return g_policy_xmap; }
+static int policy_dedup() { return g_policy_dedup; }
+static int policy_split() { return g_policy_split; }
+extern "C" int fjsp_internal_policy_option(const char* name, int64_t value) {
+    if (!strcmp(name, "policy_xmap")) {
+        if (value < 0 || value > 3) return fjsp_internal_fail("policy_xmap must be in 0..3");
+        g_policy_xmap = (int)value;
+        return 0;
+    }
+    if (!strcmp(name, "policy_dedup")) { g_policy_dedup = value != 0; return 0; }
+    if (!strcmp(name, "policy_split")) { g_policy_split = value != 0; return 0; }
+    return fjsp_internal_fail("unknown option");
 }
 
 // fjsp_a2c_policy_step's launch (fjsp_hip.hip holds the handle): k_policy_step on the policy's

@@ -108,18 +108,27 @@ def _verify_rows(rows, rep, cols):
 
 class Combined:
     """One rank's records, ordered by destination rank: actor [Ra, AW] and critic [Rc, CW] int32,
-    counts [world, 2] (actor, critic records per destination), bad = 0-d float tensor (1: a hash
+    counts [world, 2] int64 on the records' device (actor, critic records per destination; the
+    host copy comes with the exchange's one synchronisation), bad = 0-d float tensor (1: a hash
     collision or a non-binary mask; the batch must fall back)."""
 
     def __init__(self, actor, critic, counts, bad, samples):
         self.actor, self.critic, self.counts, self.bad, self.samples = actor, critic, counts, bad, samples
+        self._host = None
+
+    @property
+    def counts_host(self):
+        """[world, 2] int64 on the host (synchronises unless exchange() already fetched it)."""
+        if self._host is None:
+            self._host = self.counts.cpu()
+        return self._host
 
     def flat(self):
         """The send buffer (int32 words, per destination: its actor records, then its critic
         records) and the split sizes in words."""
         pieces, splits = [], []
         a0 = c0 = 0
-        for na, nc in self.counts.tolist():
+        for na, nc in self.counts_host.tolist():
             pieces += [self.actor[a0:a0 + na].reshape(-1), self.critic[c0:c0 + nc].reshape(-1)]
             splits.append(AW * na + CW * nc)
             a0 += na
@@ -127,7 +136,7 @@ class Combined:
         return torch.cat(pieces), splits
 
     def bytes_by_dest(self):
-        return [4 * (AW * na + CW * nc) for na, nc in self.counts.tolist()]
+        return [4 * (AW * na + CW * nc) for na, nc in self.counts_host.tolist()]
 
 
 def shard_info_words(masks, actions):
@@ -229,8 +238,14 @@ def combine(feats, masks, actions, ret, adv, mean, std, world):
                       torch.zeros(uc, 1, dtype=torch.int32, device=dev),
                       _i32(rows.index_select(0, s1)[:, :A.GLOBAL_DIM], A.GLOBAL_DIM)], dim=1)
     dest = _critic_dest(ck, world)
-    nc_d = torch.bincount(dest, minlength=world).tolist()
-    counts = torch.tensor([na_d, nc_d], dtype=torch.int64).t().contiguous()
+    # the records must leave in owner order for the all_to_all's contiguous splits: RowGroups sorts
+    # the 59 key bits whose top 16 (DEST_SHIFT) pick the owner, so dest is non-decreasing; a break
+    # of that invariant would mis-route records silently, so it raises the collision flag (fallback)
+    if uc > 1:
+        bad = bad | (dest[1:] < dest[:-1]).any()
+    counts = torch.empty(world, 2, dtype=torch.int64, device=dev)
+    counts[:, 0].copy_(torch.tensor(na_d, dtype=torch.int64), non_blocking=True)
+    counts[:, 1] = torch.bincount(dest, minlength=world)            # on the device: no host sync here
     return Combined(arec, crec, counts, bad.float().reshape(()), S)
 
 
@@ -246,8 +261,11 @@ def exchange(comb, group):
     cnt_in = comb.counts.to(cdev)
     cnt_out = torch.empty_like(cnt_in)
     dist.all_to_all_single(cnt_out, cnt_in, group=group)
+    # the update's one count synchronisation: what this rank sends and receives, to the host together
+    both = torch.stack([cnt_in, cnt_out]).cpu()
+    comb._host = both[0]
+    rc = both[1].tolist()
     buf, splits = comb.flat()
-    rc = cnt_out.cpu().tolist()
     osplits = [AW * na + CW * nc for na, nc in rc]
     src = buf.cpu() if gloo else buf
     out = torch.empty(sum(osplits), dtype=torch.int32, device=cdev)
@@ -275,10 +293,11 @@ def emulate(combs):
     for d in range(world):
         acts, crits = [], []
         for c in combs:
-            a0 = int(c.counts[:d, 0].sum())
-            c0 = int(c.counts[:d, 1].sum())
-            acts.append(c.actor[a0:a0 + int(c.counts[d, 0])])
-            crits.append(c.critic[c0:c0 + int(c.counts[d, 1])])
+            ch = c.counts_host
+            a0 = int(ch[:d, 0].sum())
+            c0 = int(ch[:d, 1].sum())
+            acts.append(c.actor[a0:a0 + int(ch[d, 0])])
+            crits.append(c.critic[c0:c0 + int(ch[d, 1])])
         out.append((torch.cat(acts), torch.cat(crits)))
     return out
 
@@ -430,33 +449,45 @@ def reduce_grads(actors, critic, al, cl, bad, group):
 
 
 def update_sharded(actors, critic, optim_actor, optim_critic, feats, masks, actions, ret, adv, gidx, midx,
-                   entropy_coef, max_grad_norm, group, dedup=True, grad_probe=None, info=None):
+                   entropy_coef, max_grad_norm, group, dedup=True, grad_probe=None, info=None, stage=None):
     """One _update (a2c.py:647-703) over every rank's transitions with the learner sharded by
     network (module docstring).  Collective calls, in order: the advantage statistics
     (all_reduce), the record counts and the records (all_to_all), the gradients + losses + flag
-    (all_reduce).  info (dict): filled with this rank's record counts and bytes sent.  Returns
-    (actor losses [8], critic loss) as Python floats."""
+    (all_reduce).  Host synchronisations: the advantage count, the record counts (one, for both
+    directions) and the reduced losses + flag (one).  info (dict): filled with this rank's record
+    counts and bytes sent.  stage (callable(name) or None): called at the end of each stage
+    (adv_stats, combine, exchange, own, all_reduce, clip_adam) by the bench's synchronised stage
+    timer.  Returns (actor losses [8], critic loss) as Python floats."""
     import torch.distributed as dist
+    mark = stage if stage is not None else (lambda name: None)
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     count, mean, std = D.adv_stats_slab(adv, group)
     norm = count > 1
+    mark("adv_stats")
     comb = combine(feats, masks, actions, ret, adv, mean if norm else None, std if norm else None, world)
+    mark("combine")
     recv, sent = exchange(comb, group)
+    mark("exchange")
     optim_actor.zero_grad(set_to_none=True)
     optim_critic.zero_grad(set_to_none=True)
     al, cl, bad = owner_losses(actors, critic, recv, rank, world, count, entropy_coef)
     bad = torch.maximum(bad, comb.bad)
     if al.requires_grad or cl.requires_grad:
         (al.sum() + cl).backward()
+    mark("own")
     al, cl, bad = reduce_grads(actors, critic, al, cl, bad, group)
+    tail = torch.cat([al.float(), cl.float().reshape(1), bad.float().reshape(1)]).cpu().tolist()   # one sync
+    mark("all_reduce")
     if info is not None:
-        info.update({"actor_records_sent": int(comb.counts[:, 0].sum()), "critic_records_sent": int(comb.counts[:, 1].sum()),
+        ch = comb.counts_host
+        info.update({"actor_records_sent": int(ch[:, 0].sum()), "critic_records_sent": int(ch[:, 1].sum()),
                      "actor_records_received": int(recv[0].shape[0]), "critic_records_received": int(recv[1].shape[0]),
                      "samples": comb.samples, "bytes_sent_to_other_ranks": sent,
-                     "bytes_by_dest": comb.bytes_by_dest(), "fallback": bool(bad > 0)})
-    if float(bad) > 0:
-        # a hash collision somewhere (or a non-binary mask): the all-reduce exchange's update,
-        # which checks its own grouping and falls back to the dense update if needed
+                     "bytes_by_dest": comb.bytes_by_dest(), "fallback": tail[NA + 1] > 0})
+    if tail[NA + 1] > 0:
+        # a hash collision somewhere (or a non-binary mask, or records out of owner order): the
+        # all-reduce exchange's update, which checks its own grouping and falls back to the dense
+        # update if needed
         al2, cl2 = A.update_core(actors, critic, optim_actor, optim_critic, feats, masks, actions, ret, adv, gidx,
                                  midx, entropy_coef, max_grad_norm, group, dedup, grad_probe)
         return al2.cpu().tolist(), float(cl2.cpu()[0])
@@ -466,4 +497,5 @@ def update_sharded(actors, critic, optim_actor, optim_critic, feats, masks, acti
     torch.nn.utils.clip_grad_norm_(critic.parameters(), max_grad_norm)
     optim_actor.step()
     optim_critic.step()
-    return al.cpu().tolist(), float(cl.cpu())
+    mark("clip_adam")
+    return tail[:NA], tail[NA]

@@ -74,24 +74,27 @@ def decode_result(agent, action, word):
     return d
 
 
+_I32, _I8, _F32 = np.dtype(np.int32), np.dtype(np.int8), np.dtype(np.float32)
+
+
 def obs_dicts(i32, i8, f32, mask):
-    """One env's SoA observation columns -> the reference's dict of numpy arrays."""
+    """One env's SoA observation columns -> the reference's dict of numpy arrays (fresh arrays:
+    the values are taken as Python numbers once, each agent's action mask is its own slice of
+    one fresh copy of the 29 mask bytes)."""
+    a, b, c, m = i32.tolist(), i8.tolist(), f32.tolist(), np.array(mask, dtype=_I8)
+    arr = np.array
     obs = {}
-    p = {k: np.array(int(i32[i]), dtype=np.int32) for i, k in enumerate(PICKUP_FIELDS)}
-    p["action_mask"] = np.asarray(mask[0:3], dtype=np.int8).copy()
+    p = {k: arr(a[i], _I32) for i, k in enumerate(PICKUP_FIELDS)}
+    p["action_mask"] = m[0:3]
     obs["pickup_station"] = p
-    a = {"position": np.array([int(i32[7]), int(i32[8])], dtype=np.int32)}
+    g = {"position": arr(a[7:9], _I32)}
     for j, k in enumerate(AGV_FIELDS[1:]):
-        a[k] = np.array(int(i32[9 + j]), dtype=np.int32)
-    a["action_mask"] = np.asarray(mask[3:11], dtype=np.int8).copy()
-    obs["agv"] = a
+        g[k] = arr(a[9 + j], _I32)
+    g["action_mask"] = m[3:11]
+    obs["agv"] = g
     for s, name in enumerate(AGENTS[2:]):
-        obs[name] = {
-            "is_busy": np.array(int(i8[2 * s]), dtype=np.int8),
-            "processing_progress": np.array(f32[s], dtype=np.float32),
-            "queue_length": np.array(int(i8[2 * s + 1]), dtype=np.int8),
-            "action_mask": np.asarray(mask[11 + 3 * s: 14 + 3 * s], dtype=np.int8).copy(),
-        }
+        obs[name] = {"is_busy": arr(b[2 * s], _I8), "processing_progress": arr(c[s], _F32),
+                     "queue_length": arr(b[2 * s + 1], _I8), "action_mask": m[11 + 3 * s: 14 + 3 * s]}
     return obs
 
 

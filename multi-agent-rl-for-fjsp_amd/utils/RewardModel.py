@@ -31,7 +31,7 @@ class RewardModel:
 
     def weights(self):
         """Weights in fjsp_reward_weights order (include/fjsp.h)."""
-        return tuple(float(getattr(self, f.name)) for f in fields(self))
+        return tuple(float(getattr(self, n)) for n in _WEIGHT_NAMES)
 
     # (weight, result key, only-when-action-0) terms per agent kind, in the reference's order
     _TERMS = {
@@ -68,3 +68,6 @@ class RewardModel:
 
     def combine_rewards(self, global_reward, local_rewards, num_agents):
         return {a: global_reward / num_agents + r for a, r in local_rewards.items()}
+
+
+_WEIGHT_NAMES = tuple(f.name for f in fields(RewardModel))   # dataclass field order = fjsp_reward_weights order

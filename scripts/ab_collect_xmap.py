@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B of the collect's actor-workgroup order (FJSP_POLICY_XMAP, csrc/fjsp_policy.hip actor_block):
+"""A/B of the collect's actor-workgroup order (option policy_xmap, csrc/fjsp_policy.hip actor_block):
 one learner per order, each captured with its order, replayed in alternation (256 x N per batch,
 ms per batch), and the rollout slabs compared byte for byte across orders after every batch (the
 order changes which workgroup computes what, never a value).
@@ -22,7 +22,7 @@ V = importlib.import_module("multi-agent-rl-for-fjsp_amd.vec_env")
 def main(n=4096, reps=10, orders=(0, 1, 2), init="random", T=256):
     learners = {}
     for x in orders:
-        os.environ["FJSP_POLICY_XMAP"] = str(x)
+        A.nat.check(A.nat.lib().fjsp_set_option(None, b"policy_xmap", x))   # library-wide, read per launch
         L = A.VecMultiAgentA2C(V.FJSPVecEnv(n), batch_size=T, seed=3)
         if init == "trained":
             L.load_state_dicts(A.load_npz_weights(os.path.join(REPO, "tests", "golden", "trained_policy.npz")))

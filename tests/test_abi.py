@@ -20,7 +20,7 @@ def test_library_exports_every_symbol():
     L = G.native.lib()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.fjsp_abi_version() == G.native.ABI_VERSION == 9
+    assert L.fjsp_abi_version() == G.native.ABI_VERSION == 10
 
 
 def test_config_validation_without_gpu():
@@ -109,3 +109,19 @@ def test_update_kernels_validate_arguments_without_gpu():
     assert L.fjsp_a2c_slab_stats(a, a, 0, 4, a, a, a, None) != 0
     assert L.fjsp_a2c_shard_keys(a, a, a, 0, 4, a, a, a, None) != 0
     assert L.fjsp_a2c_shard_keys(a, None, a, 4, 4, a, a, a, None) != 0
+
+
+def test_library_wide_policy_options_without_gpu():
+    """ABI 10: the policy launches' variants are library-wide options (fjsp_set_option with a null
+    handle), validated; nothing else is settable without a handle, and nothing is read from the
+    process environment."""
+    L = G.native.lib()
+    for name, v in ((b"policy_xmap", 2), (b"policy_xmap", 0), (b"policy_dedup", 0), (b"policy_dedup", 1),
+                    (b"policy_split", 0), (b"policy_split", 1)):
+        assert L.fjsp_set_option(None, name, v) == 0, name
+    assert L.fjsp_set_option(None, b"policy_xmap", 4) != 0
+    assert L.fjsp_set_option(None, b"policy_bogus", 1) != 0
+    assert L.fjsp_set_option(None, b"pipeline", 1) != 0 and b"null handle" in L.fjsp_last_error()
+    data = open(G.native.LIB_PATH, "rb").read()
+    for var in (b"FJSP_POLICY_XMAP", b"FJSP_FUSED_LDS", b"FJSP_AGENTS", b"FJSP_PREDRAW"):
+        assert var not in data, var

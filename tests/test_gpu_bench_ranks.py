@@ -53,3 +53,8 @@ def test_bench_gpus2_a2c_shard():
     # the records sent to the other rank, plus the 2.7 MB gradient all_reduce: far below the slab
     assert 0 < a["exchange_bytes_per_rank_per_batch"] < 256 * 4096 * 258
     assert a["n_gpus"] == 2 and a["value"] > 0
+    # the stats batch's stages, max over ranks, and every rank's record traffic
+    stages = ("gae", "adv_stats", "combine", "exchange", "own", "all_reduce", "clip_adam")
+    assert set(a["update_stage_ms"]) == {"learn"} | {"shard_" + k for k in stages}
+    assert len(a["shard_bytes_sent_by_rank"]) == 2 and all(b > 0 for b in a["shard_bytes_sent_by_rank"])
+    assert all(len(v) == 2 for v in a["shard_records_received_by_rank"].values())

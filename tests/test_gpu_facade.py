@@ -187,6 +187,10 @@ def test_reward_weights_follow_reward_model(M):
     sim.reset(seed=1, num_orders=3)
     prev_orders = prev_pk = 0
     for t in range(400):
+        if t == 150:   # a weight changed mid-episode is used from the next step on
+            rm.AGV_MOVE_PENALTY = -0.77
+        if t == 250:   # a replaced reward_calculator object too
+            sim.reward_calculator = rm = type(rm)(ORDER_COMPLETE_REWARD=55.5, AGV_DELIVERY_REWARD=3.25)
         acts = O.actions(4, 1, t, None)
         actions = {a: int(acts[i]) for i, a in enumerate(spec.AGENTS)}
         obs, rew, term, trunc, info = sim.step(actions)

@@ -87,6 +87,9 @@ def _learner(exchange, n=256, T=64):
     return L
 
 
+SHARD_STAGES = ("gae", "adv_stats", "combine", "exchange", "own", "all_reduce", "clip_adam")
+
+
 @pytest.mark.timeout(300)
 def test_rccl_learner_exchanges_equal_single_learner(R):
     """The three exchanges through RCCL with one rank: "gather" is the single learner's update on
@@ -104,7 +107,13 @@ def test_rccl_learner_exchanges_equal_single_learner(R):
             finally:
                 D.FORCE_ACTIVE = True
         else:
+            if ex == "shard":
+                L.exchange_timing = {}   # the bench's synchronised stage timers
             L.update()
+            if ex == "shard":
+                assert set(L.exchange_timing) == {"learn"} | {"shard_" + k for k in SHARD_STAGES}, L.exchange_timing
+                assert all(v >= 0 for v in L.exchange_timing.values())
+                L.exchange_timing = None
         p = torch.cat([q.detach().reshape(-1) for q in list(L.actors.parameters()) + list(L.critic.parameters())])
         res[ex] = (grads[0], p, L.critic_loss_history[-1], [h[-1] for h in L.actor_loss_history.values()],
                    dict(L.shard_info), L._bufs["rewards"].clone())
