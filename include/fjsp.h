@@ -179,8 +179,6 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
  * (0..2^20, default 0; tests only: later k_step_ag and k_step_pipe<lds,2emit,predraw> launches
  * run a test build in which workgroup 0's owner wave sleeps value x ~8k cycles before its first
  * step, so that the other waves' bounded waits give up and the give-up path runs).  spin_cap and test_stall are not part of a snapshot.
- * "legacy_step" (0/1, default 0: fjsp_step in the canonical dict order launches r05's k_step<canon>
- * instead of k_step_pf; identical results, for A/B runs).
  * Library-wide (h may be NULL; ABI 10): "policy_xmap" (0..3, default 0), "policy_dedup" (0/1,
  * default 1), "policy_split" (0/1, default 1) — the variants of the A2C policy launches listed at
  * fjsp_a2c_policy; identical results.  Nothing is read from the process environment. */

@@ -343,16 +343,14 @@ constexpr uint32_t R_EXEC = 0x80u;
 // hand the tray to ready_trays when the order ends / the tray is full) and SIGNAL are
 // conditions; the only memory operations are the next order's word (when an order starts)
 // and the single tray push.
-// pre_ow: the next order's word read ahead (k_step's prefetch round; nothing writes the order
-// table before the pickup station in dict order), or null to read it here.
-FJSP_DEV uint32_t pickup_execute(Env& E, const Tables& T, const Cfg& C, int action, const uint32_t* pre_ow = nullptr) {
+FJSP_DEV uint32_t pickup_execute(Env& E, const Tables& T, const Cfg& C, int action) {
     const int co = E.cur_order(), no = E.next_order();
     const bool more = no < E.norders();
     const bool has_orders = more || co >= 0;
     const bool a1 = action == 1;
     // order (PickupStationAgent.py:210-215)
     const bool start = a1 && co < 0 && more;
-    if (start) E.set_cur_info(pre_ow ? *pre_ow : T.orders[no * T.stride]);
+    if (start) E.set_cur_info(T.orders[no * T.stride]);
     E.set_next_order(no + (start ? 1 : 0));
     const int co1 = start ? no : co;
     const int idx1 = start ? 0 : E.cur_idx();
@@ -709,20 +707,14 @@ FJSP_DEV void machine_grant(Env& E, const Cfg& C, int slot, int code, int step) 
     else E.set_m_prog(M, 1);
 }
 // AT: the order words are shared with another wave (k_step_ag) -> atomic OR, no read.
-// PF (k_step's prefetch round): pf->g[m] = the granted slot's code, pf->w[m] = the completing
-// product's order word, both read at the top of the step (nothing writes either before the run).
-struct MachPF {
-    int g[2];
-    uint32_t w[2];
-};
 template <bool AT = false>
-FJSP_DEV void machines_run(Env& E, const Tables& T, const Cfg& C, int s0, int s1, const MachPF* pf = nullptr) {
+FJSP_DEV void machines_run(Env& E, const Tables& T, const Cfg& C, int s0, int s1) {
     const int step = E.step();
     const bool due0 = E.m_busy(0) && E.m_next(0) == step, due1 = E.m_busy(1) && E.m_next(1) == step;
     const int c0 = E.m_code(0), c1 = E.m_code(1);
     const int o0 = tc_order(c0), o1 = tc_order(c1);
-    const int g0 = pf ? pf->g[0] : T.scode[(s0 >= 0 ? s0 : 0) * T.stride];
-    const int g1 = pf ? pf->g[1] : T.scode[(s1 >= 0 ? s1 : 0) * T.stride];
+    const int g0 = T.scode[(s0 >= 0 ? s0 : 0) * T.stride];
+    const int g1 = T.scode[(s1 >= 0 ? s1 : 0) * T.stride];
     const uint32_t b0 = 1u << (tc_start(c0) + E.m_k(0)), b1 = 1u << (tc_start(c1) + E.m_k(1));
     // product.is_processed = True
     if constexpr (AT) {
@@ -730,8 +722,8 @@ FJSP_DEV void machines_run(Env& E, const Tables& T, const Cfg& C, int s0, int s1
         if (due1) order_or(&T.orders[o1 * T.stride], b1);
     } else {
         // independent loads (addresses clamped to valid entries when unused)
-        const uint32_t w0 = pf ? pf->w[0] : T.orders[(due0 ? o0 : 0) * T.stride];
-        const uint32_t w1 = pf ? pf->w[1] : T.orders[(due1 ? o1 : 0) * T.stride];
+        const uint32_t w0 = T.orders[(due0 ? o0 : 0) * T.stride];
+        const uint32_t w1 = T.orders[(due1 ? o1 : 0) * T.stride];
         if (due0) T.orders[o0 * T.stride] = w0 | b0;
         if (due1) T.orders[o1 * T.stride] = ((due0 && o0 == o1) ? (w0 | b0) : w1) | b1;
     }
@@ -749,11 +741,11 @@ FJSP_DEV void machines_run(Env& E, const Tables& T, const Cfg& C, int s0, int s1
 // `due` = the in-flight head run completes now (pack_due: the four stations' head checks are
 // issued as one batch of independent loads).
 template <int S>
-FJSP_DEV bool pack_due(const Env& E, const Tables& T, int step, const uint16_t* pre_cs = nullptr) {
+FJSP_DEV bool pack_due(const Env& E, const Tables& T, int step) {
     constexpr int L = L_PKG + S;
     const int h = E.lh(L);
     const bool inflight = E.ll(L) > 0 && h != E.p_qfirst(S);
-    const uint16_t cs = pre_cs ? *pre_cs : T.scstep[(inflight ? h : 0) * T.stride];   // slot 0 always exists
+    const uint16_t cs = T.scstep[(inflight ? h : 0) * T.stride];   // slot 0 always exists
     return inflight && cs == (uint16_t)step;
 }
 template <int S, bool AT = false>
@@ -1128,92 +1120,6 @@ FJSP_DEV double env_advance(Env& E, const Tables& T, const Cfg& C, const int* ac
     E.set_ncompleted(E.ncompleted() + orders_done);
     FJSP_STAMP(E, 2);
     // 3. calculate_global_reward; combine_rewards divides it by len(self.agents)
-    return global_reward8(C, orders_done, E.total_packaged() - products_before);
-}
-
-// env_advance<CANON = true> with the step's first-level table reads issued as ONE batch right
-// after the state words arrive (the one-launch-per-step k_step, whose single step has no
-// pipeline to hide its dependent reads in).  Read ahead, on the state at the top of the step:
-//   the next order's word (pickup START), the AGV's PICKUP source front (agv_pre: its successor
-//   and code, then the code's order word), each machine queue front's successor and code (START
-//   pops it; the run grants it), each machine's completing product's order word, each
-//   packaging station's in-flight head's completion step.
-// Why each stays valid until it is used (dict order: pickup, AGV, machines, packaging, run):
-//   * the pickup station is the first writer of anything, and it never writes the order table;
-//   * a list front only changes by a pop: the AGV pops only its own source, the machines only
-//     their queues, packaging completions only in the run; pushes append.  A machine queue empty
-//     at the top can only receive the AGV's drop, whose code the AGV word holds; a queue of one
-//     gets the drop as the front's successor = its tail (k_step_ag's nk rule);
-//   * a machine's completing order word is written first by machines_run itself (the packaging
-//     completions that also write order words run after it);
-//   * the in-flight head of a packaging list and its completion step do not change before the
-//     run: a drop appends behind the queued runs (a list that was empty only gets a queued run),
-//     and the step's grants are written after pack_due.
-// agv_fin + agv_pack_drop at the AGV's turn equal agv_execute<false> (the packaging stations'
-// actions, after the AGV in dict order, do not change the in-flight counts the routing reads).
-FJSP_DEV double env_advance_pf(Env& E, const Tables& T, const Cfg& C, const int* act, uint32_t* res) {
-    const int products_before = E.total_packaged();
-    // ---- the read-ahead round
-    const uint32_t pre_ow = T.orders[(E.next_order() < MAX_ORDERS ? E.next_order() : 0) * T.stride];
-    int qh[2], ql[2];
-    uint32_t qn[2], qc[2], mw[2];
-#pragma unroll
-    for (int m = 0; m < 2; m++) {
-        const int LQ = m == 0 ? L_M0Q : L_M1Q;
-        ql[m] = E.ll(LQ);
-        qh[m] = ql[m] > 0 ? E.lh(LQ) : 0;
-        qn[m] = T.snext[qh[m] * T.stride];
-        qc[m] = T.scode[qh[m] * T.stride];
-        mw[m] = T.orders[tc_order(E.m_code(m)) * T.stride];
-    }
-    uint16_t pcs[4];
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-        const int L = L_PKG + s, h = E.lh(L);
-        pcs[s] = T.scstep[((E.ll(L) > 0 && h != E.p_qfirst(s)) ? h : 0) * T.stride];
-    }
-    const int a1 = act[1];
-    const AgvPre pre = agv_pre(E, T, C, a1 == 255 ? 0 : a1);
-    // ---- 1. actions in dict order (FJSPSimulation.py:172-174)
-    int move_to = 0, m_start[2] = {-1, -1}, p_started[4] = {0, 0, 0, 0};
-    res[0] = act[0] != 255 ? pickup_execute(E, T, C, act[0], &pre_ow) : 0u;
-    res[1] = 0u;
-    if (a1 != 255) {
-        uint32_t pend = 0;
-        res[1] = agv_fin(E, T, pre, &move_to, &pend);
-        if (pend) agv_pack_drop(E, T, C, pend);
-    }
-    MachPF pf;
-#pragma unroll
-    for (int m = 0; m < 2; m++) {
-        const int LQ = m == 0 ? L_M0Q : L_M1Q;
-        const int nk = ql[m] >= 2 ? (int)qn[m] : E.lt(LQ);
-        res[2 + m] = 0u;
-        if (act[2 + m] != 255)
-            res[2 + m] = m == 0 ? machine_execute<0>(E, T, act[2], &m_start[0], nk)
-                                : machine_execute<1>(E, T, act[3], &m_start[1], nk);
-        // the granted slot: the front at the top, or the AGV's drop into an empty queue
-        pf.g[m] = ql[m] > 0 ? (int)qc[m] : pre.code;
-        pf.w[m] = mw[m];
-    }
-    res[4] = act[4] != 255 ? pack_execute<0>(E, act[4], &p_started[0]) : 0u;
-    res[5] = act[5] != 255 ? pack_execute<1>(E, act[5], &p_started[1]) : 0u;
-    res[6] = act[6] != 255 ? pack_execute<2>(E, act[6], &p_started[2]) : 0u;
-    res[7] = act[7] != 255 ? pack_execute<3>(E, act[7], &p_started[3]) : 0u;
-    FJSP_STAMP(E, 1);
-    // ---- 2. env.run(until=now+step_size) in closed form
-    if (move_to) E.set_loc(move_to);
-    machines_run(E, T, C, m_start[0], m_start[1], &pf);
-    int orders_done = 0;
-    const int step = E.step();
-    const bool due0 = pack_due<0>(E, T, step, &pcs[0]), due1 = pack_due<1>(E, T, step, &pcs[1]);
-    const bool due2 = pack_due<2>(E, T, step, &pcs[2]), due3 = pack_due<3>(E, T, step, &pcs[3]);
-    pack_run<0>(E, T, C, p_started[0], due0, &orders_done);
-    pack_run<1>(E, T, C, p_started[1], due1, &orders_done);
-    pack_run<2>(E, T, C, p_started[2], due2, &orders_done);
-    pack_run<3>(E, T, C, p_started[3], due3, &orders_done);
-    E.set_ncompleted(E.ncompleted() + orders_done);
-    FJSP_STAMP(E, 2);
     return global_reward8(C, orders_done, E.total_packaged() - products_before);
 }
 

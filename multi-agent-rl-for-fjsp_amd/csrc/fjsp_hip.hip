@@ -267,104 +267,6 @@ __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t
     )
 }
 
-// The one-launch-per-step kernel of the canonical dict order (fjsp_step without agent_order: the
-// facade, FJSPVecEnv.step).  A single step has no pipeline to hide its dependent reads or its
-// ~85 output stores in (stamps, profiles/r06/kstep_stamps_r05code.json: of 16.1 k cycles per wave,
-// 4.6 k action phase, 1.8 k run, 3.6 k observe + 0.6 k rewards of stores), so:
-//   * env_advance_pf: the step's first-level table reads go out as one batch on the state words;
-//   * STAGED (N % 64 == 0, 16-byte aligned lean outputs): obs, masks, rewards, term, trunc and
-//     status are written into an LDS tile and leave as whole 16-byte rows (~15 stores per wave
-//     instead of ~85, which overran the wave's 63 outstanding stores and waited on their acks).
-// The optional outputs (results, infos, post-reset observation, a2c features) are stored directly.
-template <bool STAGED>
-__global__ void __launch_bounds__(BLOCK) k_step_pf(DevState S, Cfg C, const uint8_t* __restrict__ actions, int autoreset,
-                                                   fjsp_out out) {
-    FJSP_DIAG(
-    const uint64_t t_entry = __builtin_amdgcn_s_memtime();
-    )
-    struct NoTile { int unused; };
-    __shared__ typename std::conditional<STAGED, StageTile, NoTile>::type s_tile;
-    __shared__ double s_lut[RLUT_SIZE];
-    const int lane = threadIdx.x;
-    const int e = blockIdx.x * BLOCK + lane;
-    const bool valid = e < S.n;
-    Env E;
-    int act[NA];
-    if (valid) {
-        env_load(E, S.words, S.n, e);
-#pragma unroll
-        for (int a = 0; a < NA; a++) act[a] = actions[a * S.n + e];
-    }
-    for (int i = lane; i < RLUT_SIZE; i += BLOCK) s_lut[i] = C.lut[i];
-    __syncthreads();
-    C.lut = s_lut;
-    if (!valid) return;   // STAGED launches only whole 64-env blocks: every lane reaches its barriers
-    FJSP_DIAG(
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (int i = 0; i < 8; i++) E.st_acc[i] = 0;
-    E.st_t0 = __builtin_amdgcn_s_memtime();
-    E.st_acc[0] = E.st_t0 - t_entry;
-    )
-    const Tables T = tables_of(S, e);
-    const uint32_t n = (uint32_t)S.n, ue = (uint32_t)e;
-    uint32_t res[NA];
-    const double g8 = env_advance_pf(E, T, C, act, res);
-#pragma unroll
-    for (int a = 0; a < NA; a++) {
-        const double r = g8 + local_reward(C, a, res[a], act[a]);
-        if constexpr (STAGED) s_tile.rew[a * BLOCK + lane] = r;
-        else if (out.rewards) st32(out.rewards, (uint32_t)a * n + ue, r);
-    }
-    if (out.results) {
-#pragma unroll
-        for (int a = 0; a < NA; a++) st32(out.results, (uint32_t)a * n + ue, res[a]);
-    }
-    FJSP_STAMP(E, 3);
-    const int nord = E.norders();
-    if constexpr (STAGED) {
-        StageSink sink{&s_tile, lane};
-        observe(E, C, sink);
-    } else {
-        StoreSink sink{out.obs_i32, out.obs_i8, out.obs_f32, out.masks, 0u, n, ue};
-        observe(E, C, sink);
-    }
-    FJSP_STAMP(E, 4);
-    const int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;
-    const int truncated = E.step() >= C.max_steps;
-    if constexpr (STAGED) {
-        s_tile.term[lane] = (uint8_t)all_done;
-        s_tile.trunc[lane] = (uint8_t)truncated;
-        s_tile.status[lane] = E.status();
-    } else {
-        if (out.term) st32(out.term, ue, (uint8_t)all_done);
-        if (out.trunc) st32(out.trunc, ue, (uint8_t)truncated);
-        if (out.status) st32(out.status, ue, E.status());
-    }
-    if (out.orders_completed) st32(out.orders_completed, ue, E.ncompleted());
-    if (out.packaged) st32(out.packaged, ue, E.total_packaged());
-    if (out.sim_time) st32(out.sim_time, ue, (double)(E.step() + 1) * (double)C.step_size);
-    if constexpr (STAGED) {
-        __syncthreads();
-        copy_out(s_tile, out, 0u, (size_t)S.n, blockIdx.x, lane);
-    }
-    FJSP_STAMP(E, 5);
-    E.set_step(E.step() + 1);
-    if (autoreset && (all_done || truncated))
-        E = env_reset_cold(E, T, C, S, e, nord);   // reset(seed=None) continues the MT stream
-    if (out.next_i32 || out.next_i8 || out.next_f32 || out.next_masks || out.feats) {
-        StoreSink nsink{out.next_i32, out.next_i8, out.next_f32, out.next_masks, 0u, n, ue, out.feats};
-        observe(E, C, nsink);
-    }
-    FJSP_STAMP(E, 6);
-    env_store(E, S.words, S.n, e);
-    FJSP_DIAG(
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    FJSP_STAMP_AT(E, 7);
-    if (lane == 0)
-        for (int i = 0; i < 8; i++) atomicAdd((unsigned long long*)&g_stamps[i], (unsigned long long)E.st_acc[i]);
-    )
-}
-
 // The env's order table and used tray-slot prefix into LDS tables (one lane per env): the
 // loads of eight rows are issued together and waited for once (a load-then-store loop per row
 // waits out one HBM round trip per row, ~30 us per launch at 30 orders and a few dozen slots).
@@ -1994,15 +1896,13 @@ struct fjsp_handle {
     int timed;
     double* lut_dev;
     double lut_host[RLUT_SIZE];
-    int use_lds;     // fused kernel variant (FJSP_FUSED_LDS env var / fjsp_set_option)
-    int use_staged;  // LDS-staged wide output stores (FJSP_STAGED env var / fjsp_set_option)
+    int use_lds;     // fused kernel variant (fjsp_set_option "fused_lds")
+    int use_staged;  // LDS-staged wide output stores (fjsp_set_option "staged_stores")
     int timing;      // hipEvent bracketing of step launches (off while graph-capturing)
-    int use_pipe;    // two-wave pipelined k_step_many for lean outputs (FJSP_PIPE / fjsp_set_option)
-    int use_pg;      // pre-draw wave in the pipelined kernel (FJSP_PREDRAW / fjsp_set_option "predraw")
-    int use_ag;      // agent-group pipeline k_step_ag for uniform-random actions (FJSP_AGENTS / "agents")
-    int legacy_step; // fjsp_step in canonical order launches r05's k_step<canon> (option "legacy_step", A/B)
-    int step_staged; // k_step_pf stages its lean outputs in LDS (option "step_staged", A/B; measured slower)
-    int ag_epw;      // k_step_ag envs per workgroup: 64 / 32 / 16, 0 = auto (FJSP_AG_EPW / "ag_envs")
+    int use_pipe;    // two-wave pipelined k_step_many for lean outputs (fjsp_set_option "pipeline")
+    int use_pg;      // pre-draw wave in the pipelined kernel (fjsp_set_option "predraw")
+    int use_ag;      // agent-group pipeline k_step_ag for uniform-random actions (fjsp_set_option "agents")
+    int ag_epw;      // k_step_ag envs per workgroup: 64 / 32 / 16, 0 = auto (fjsp_set_option "ag_envs")
     const char* last_kernel;   // name of the last step kernel launched (fjsp_last_kernel)
     uint32_t env_id_base;      // global id of env 0 (fjsp_set_option "env_id_base")
     // fjsp_a2c_policy_step's tile hand-off: [ntiles] arrival counters (zero between launches),
@@ -2228,8 +2128,6 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
         h->ag_epw = (int)value;
         return 0;
     }
-    if (!strcmp(name, "legacy_step")) { h->legacy_step = value != 0; return 0; }   // A/B: k_step<canon> (r05)
-    if (!strcmp(name, "step_staged")) { h->step_staged = value != 0; return 0; }   // A/B: k_step_pf<staged>
     if (!strcmp(name, "timing")) { h->timing = value != 0; if (!h->timing) h->timed = 0; return 0; }
     if (!strcmp(name, "spin_cap")) {
         if (value < 256 || value > 0x7FFFFFFFll) return fail("spin_cap must be in 256..2^31-1");
@@ -2302,18 +2200,7 @@ int fjsp_step(fjsp_handle* h, const uint8_t* actions, const uint8_t* agent_order
     DeviceGuard g(h->device);
     dim3 grid((h->n + BLOCK - 1) / BLOCK);
     if (h->timing) HIPCHK(hipEventRecord(h->ev0, h->stream));
-    const fjsp_out o = out ? *out : kNoOut;
-    // LDS-staged lean outputs need whole 64-env blocks and 16-byte aligned rows
-    auto al16 = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
-    const bool staged = h->step_staged && h->n % BLOCK == 0 && al16(o.obs_i32) && al16(o.obs_i8) && al16(o.obs_f32) && al16(o.masks) &&
-                        al16(o.rewards) && al16(o.term) && al16(o.trunc) && al16(o.status);
-    if (canon && !h->legacy_step) {
-        h->last_kernel = staged ? "k_step_pf<staged>" : "k_step_pf";
-        if (staged)
-            hipLaunchKernelGGL(k_step_pf<true>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, autoreset, o);
-        else
-            hipLaunchKernelGGL(k_step_pf<false>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, autoreset, o);
-    } else if (canon) {
+    if (canon) {
         h->last_kernel = "k_step<canon>";
         hipLaunchKernelGGL(k_step<true>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, packed, autoreset,
                            out ? *out : kNoOut);

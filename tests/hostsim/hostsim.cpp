@@ -13,7 +13,6 @@ struct HS {
     int n; Cfg C;
     Env* E; uint32_t* orders; uint16_t* scode; uint8_t* snext; uint16_t* scstep;
     uint32_t (*mt)[624]; int* mti;
-    int pf;   // 1: env_advance_pf (k_step_pf's read-ahead step) instead of env_advance
 };
 static uint32_t mt_next_(uint32_t* s, int& mti) {
     if (mti >= 624) {
@@ -53,7 +52,6 @@ void* hs_create(const int32_t* c, int n) {
     h->mti = (int*)calloc(n, sizeof(int));
     return h;
 }
-void hs_set_pf(void* p, int pf) { ((HS*)p)->pf = pf; }
 void hs_destroy(void* p) {
     HS* h = (HS*)p; free((void*)h->C.lut); free(h->E); free(h->orders); free(h->scode); free(h->snext); free(h->scstep); free(h->mt); free(h->mti); free(h);
 }
@@ -93,12 +91,7 @@ void hs_step(void* p, const uint8_t* actions, int autoreset, int32_t* i32, int8_
     for (int e = 0; e < h->n; e++) {
         Env& E = h->E[e]; Tables T = tabs(h, e);
         int act[8]; for (int a = 0; a < 8; a++) act[a] = actions[8 * e + a];
-        if (h->pf) {
-            const double g8 = env_advance_pf(E, T, h->C, act, res + 8 * e);
-            for (int a = 0; a < 8; a++) rew[8 * e + a] = g8 + local_reward(h->C, a, res[8 * e + a], act[a]);
-        } else {
-            env_step<true>(E, T, h->C, act, nullptr, res + 8 * e, rew + 8 * e);
-        }
+        env_step<true>(E, T, h->C, act, nullptr, res + 8 * e, rew + 8 * e);
         obs_out(h, e, i32, i8, f32, mk);
         const int nord = E.norders();
         int all_done = E.ncompleted() == nord && nord > 0 && E.next_order() == nord;

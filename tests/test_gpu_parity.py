@@ -115,39 +115,6 @@ def test_step_vs_fused(G):
         masks = r["next_masks"][0]
 
 
-@pytest.mark.parametrize("n,infos,staged", [(4096, False, 0), (4096, False, 1), (4096, True, 1), (100, True, 1),
-                                            (1, True, 0)])
-def test_step_pf_equals_legacy_step(G, n, infos, staged):
-    """k_step_pf (read-ahead table reads; LDS-staged lean outputs when N % 64 == 0) byte-equal to
-    r05's k_step<canon> (option legacy_step): random, absent (255) and out-of-range actions in
-    the canonical dict order, every output and the final state snapshot, auto-reset included."""
-    steps = 260 if n > 1 else 450
-    rng = np.random.default_rng(n + 7 * infos)
-    envs = [G.make_env(n), G.make_env(n)]
-    G.native.check(G.native.lib().fjsp_set_option(envs[1].handle, b"legacy_step", 1))
-    G.native.check(G.native.lib().fjsp_set_option(envs[0].handle, b"step_staged", staged))
-    bufs = [G.vec_env.Buffers(1, n, envs[0].device, infos=infos, next_obs=infos, feats=infos) for _ in envs]
-    for env in envs:
-        env.reset(seeds=torch.arange(n), num_orders=30)
-    nact = np.array([3, 8, 3, 3, 3, 3, 3, 3]).reshape(8, 1)
-    for t in range(steps):
-        acts = (rng.integers(0, 256, (8, n)) * nact >> 8).astype(np.uint8)
-        acts[rng.random((8, n)) < 0.05] = 255
-        weird = rng.random((8, n)) < 0.02
-        acts[weird] = rng.integers(3, 255, size=weird.sum())
-        a = torch.from_numpy(acts).cuda()
-        for env, b in zip(envs, bufs):
-            env.step(a, buffers=b)
-        if t == 0:
-            assert envs[0].last_kernel() == ("k_step_pf<staged>" if n % 64 == 0 and staged else "k_step_pf")
-            assert envs[1].last_kernel() == "k_step<canon>"
-        for k in G.native.OUT_FIELDS:
-            x, y = getattr(bufs[0], k, None), getattr(bufs[1], k, None)
-            if x is not None:
-                assert x.cpu().numpy().tobytes() == y.cpu().numpy().tobytes(), (t, k)
-    assert torch.equal(envs[0].snapshot(), envs[1].snapshot())
-
-
 def test_agent_order_and_absent_agents(G):
     """Non-canonical dict order and missing agents against the oracle (FJSPSimulation.py:172-205)."""
     n, steps = 64, 200

@@ -31,15 +31,13 @@ def L():
     lib.hs_reset.argtypes = [Pt, Pt, ctypes.c_int, Pt, Pt, Pt, Pt]
     lib.hs_step.argtypes = [Pt, Pt, ctypes.c_int] + [Pt] * 13
     lib.hs_heuristic.argtypes = [Pt, Pt]
-    lib.hs_set_pf.argtypes = [Pt, ctypes.c_int]
     return lib
 
 
 class HS:
-    def __init__(self, L, n, cfg, pf=0):
+    def __init__(self, L, n, cfg):
         self.L, self.n = L, n
         self.h = L.hs_create(O.cfg_array(**cfg), n)
-        L.hs_set_pf(self.h, pf)   # 1: the one-launch step's read-ahead variant (env_advance_pf)
         z = np.zeros
         self.i32, self.i8, self.f32, self.mk = z((n, 20), np.int32), z((n, 12), np.int8), z((n, 6), np.float32), z((n, 29), np.int8)
         self.rew, self.term, self.trunc = z((n, 8)), z(n, np.uint8), z(n, np.uint8)
@@ -74,9 +72,8 @@ class HS:
     (1, {"tray_capacity": 3, "max_episode_steps": 50}, 3, 32, 500),
     (1, {"packaging_capacity": 2, "num_trays": 40}, 20, 32, 600),
 ])
-@pytest.mark.parametrize("pf", [0, 1], ids=["advance", "advance_pf"])
-def test_closed_form_vs_oracle(L, policy, cfg, norders, n, steps, pf):
-    hs = HS(L, n, cfg, pf)
+def test_closed_form_vs_oracle(L, policy, cfg, norders, n, steps):
+    hs = HS(L, n, cfg)
     seeds = np.arange(n, dtype=np.uint32) + 100
     hs.reset(seeds, norders)
     rec, rst, _ = O.rollout(n, steps, seeds=seeds, gid0=0, num_orders=norders, policy=policy,
@@ -99,10 +96,9 @@ def test_closed_form_vs_oracle(L, policy, cfg, norders, n, steps, pf):
         masks = hs.rmk.copy()
 
 
-@pytest.mark.parametrize("pf", [0, 1], ids=["advance", "advance_pf"])
 @pytest.mark.parametrize("tr", P.load_traces() + P.load_scenarios(), ids=lambda t: t.name)
-def test_closed_form_vs_golden(L, tr, pf):
-    hs = HS(L, 1, tr.cfg, pf)
+def test_closed_form_vs_golden(L, tr):
+    hs = HS(L, 1, tr.cfg)
     hs.reset([tr.seed], tr.num_orders)
     assert P.bits_equal(hs.i32[0], tr.init_i32)
     for t in range(tr.steps):
@@ -142,8 +138,7 @@ def test_heuristic_vs_oracle_rollout(L):
     assert done > 0   # the heuristic finishes small episodes
 
 
-@pytest.mark.parametrize("pf", [0, 1], ids=["advance", "advance_pf"])
-def test_property_random_configs_and_actions(L, pf):
+def test_property_random_configs_and_actions(L):
     """Property test (hypothesis): the kernel's state machine equals the oracle's event heap on
     random valid configurations and arbitrary action streams, including out-of-range actions."""
     hyp = pytest.importorskip("hypothesis")
@@ -158,7 +153,7 @@ def test_property_random_configs_and_actions(L, pf):
         cfg = {"tray_capacity": tray_cap, "mask_tray_capacity": tray_cap, "storage_capacity": storage,
                "num_trays": trays, "step_size": step, "pt_small": 6 * step, "pt_big": 12 * step,
                "pt_packaging": 3 * step}
-        hs = HS(L, 1, cfg, pf)
+        hs = HS(L, 1, cfg)
         hs.reset([seed], norders)
         o = O.OracleEnv(**cfg)
         o.reset(seed=seed, num_orders=norders)
