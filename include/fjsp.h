@@ -384,15 +384,18 @@ int fjsp_a2c_group_verify(const float* rows, int32_t T, int32_t n, const int64_t
  * group's first sample and run end.  fjsp_a2c_group_sort: one radix sort of every row's 59 key
  * bits with the row id above them (flat / sorted uint64 [R * S], pos / spos uint32 [R * S]), the
  * run starts (runs uint32 [R * S]) and their inclusive scan (scan), and the group count of each
- * row, counts int64 [R]; temp: fjsp_a2c_group_temp_bytes(R * S) bytes.  After the caller has read
+ * row, counts int64 [R]; temp: fjsp_a2c_group_temp_bytes(R * S) bytes.  lowcard (ABI 10): bit r
+ * set = row r is expected to hold at most 64 distinct keys (the station agents' rows) and is
+ * grouped by a stable counting sort instead (same outputs); a row that turns out to hold more
+ * reports counts[r] = -1 and the caller groups again with that bit clear.  After the caller has read
  * counts and chosen umax >= every count, fjsp_a2c_group_runs: starts (scratch) / first / ends int64
  * [R][umax] (padding groups: start and end S, first = the row's last sorted sample), perm int64
  * [R][S] (sample of each sorted position), inv int64 [R][S] (group of each sample), rep int64
  * [R][S] (first sample of each sample's group).  Stream-ordered. */
 int fjsp_a2c_group_temp_bytes(int64_t count, uint64_t* bytes);
-int fjsp_a2c_group_sort(const uint64_t* keys, int32_t R, int64_t S, void* temp, uint64_t temp_bytes, uint64_t* flat,
-                        uint64_t* sorted, uint32_t* pos, uint32_t* spos, uint32_t* runs, uint32_t* scan, int64_t* counts,
-                        void* stream);
+int fjsp_a2c_group_sort(const uint64_t* keys, int32_t R, int64_t S, uint32_t lowcard, void* temp, uint64_t temp_bytes,
+                        uint64_t* flat, uint64_t* sorted, uint32_t* pos, uint32_t* spos, uint32_t* runs, uint32_t* scan,
+                        int64_t* counts, void* stream);
 int fjsp_a2c_group_runs(const uint32_t* spos, const uint32_t* scan, int32_t R, int64_t S, int64_t umax, int64_t* starts,
                         int64_t* perm, int64_t* inv, int64_t* rep, int64_t* first, int64_t* ends, int32_t* gsorted,
                         void* stream);

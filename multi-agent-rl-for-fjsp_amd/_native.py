@@ -165,7 +165,7 @@ def lib():
         "fjsp_gae_shared": (I, [P, P, P, I, I, I, D, D, P, P, P]),
         "fjsp_a2c_policy_step": (I, [P, P, P, P, P, P, U32, U32, I, P, P, I, ctypes.POINTER(fjsp_out), I, I, P]),
         "fjsp_a2c_group_temp_bytes": (I, [ctypes.c_int64, ctypes.POINTER(U64)]),
-        "fjsp_a2c_group_sort": (I, [P, I, ctypes.c_int64, P, U64, P, P, P, P, P, P, P, P]),
+        "fjsp_a2c_group_sort": (I, [P, I, ctypes.c_int64, ctypes.c_uint32, P, U64, P, P, P, P, P, P, P, P]),
         "fjsp_a2c_group_runs": (I, [P, P, I, ctypes.c_int64, ctypes.c_int64, P, P, P, P, P, P, P, P]),
         "fjsp_a2c_run_sums_bytes": (I, [I, ctypes.c_int64, ctypes.POINTER(U64)]),
         "fjsp_a2c_run_sums": (I, [P, I, P, P, P, P, ctypes.c_int64, ctypes.c_int64, P, U64, P, P]),

@@ -107,7 +107,7 @@ def _splitk_wgrad(gy, x):
     """gy^T x over a long batch B: c chunks of B // c rows as strided views (no padded copies)
     in one batched GEMM, summed; the B - c * (B // c) tail apart."""
     B = x.shape[0]
-    c = max(1, min(64, B // 8192))
+    c = max(1, min(128, B // 8192))   # 128 chunks: 7 % faster than 64 at U = 698 k (profiles/r06/a2c/ab_wgrad_split.json)
     bc = B // c
     xc = x[:c * bc].reshape(c, bc, -1)
     gc = gy[:c * bc].reshape(c, bc, -1)
@@ -218,25 +218,36 @@ class _CriticGrouped(torch.autograd.Function):
 class _CriticOnePass(torch.autograd.Function):
     """The grouped update's critic loss and its gradients in one kernel pass over the distinct
     global states (fjsp_a2c_critic_fused: forward, value gradient from the per-state loss
-    coefficients, value head and the two 256-wide layers' backward; a2c.py:683-699, 713-722), then
-    the three split-K weight gradients.  x f32 [U, 40] (sample-major rows), coef f64 [U, 3] =
-    (a, b, c) with state u's loss a/2 V^2 + b V + c (critic_coef) -> the critic loss (0-d f32);
-    backward returns the gradients the forward computed, scaled by the loss's gradient."""
+    coefficients, value head and the two 256-wide layers' backward; a2c.py:683-699, 713-722); the
+    three split-K weight gradients in backward (a loss-only call pays for none of them).  x f32
+    [U, 40] (sample-major rows), coef f64 [U, 3] = (a, b, c) with state u's loss a/2 V^2 + b V + c
+    (critic_coef) -> the critic loss (0-d f32); backward returns the gradients, scaled by the
+    loss's gradient."""
 
     @staticmethod
     def forward(ctx, x, coef, W1, b1, W2, b2, W3, b3, W4, b4):
-        loss, ctx.grads = critic_onepass_compute(x, coef, W1, b1, W2, b2, W3, b3, W4, b4)
+        loss, ctx.parts = critic_onepass_compute(x, coef, W1, b1, W2, b2, W3, b3, W4, b4)
         return loss
 
     @staticmethod
     def backward(ctx, gl):
-        return (None, None) + tuple(g * gl for g in ctx.grads)
+        grads = critic_onepass_grads(*ctx.parts)
+        ctx.parts = None
+        return (None, None) + tuple(g * gl for g in grads)
+
+
+@torch.no_grad()
+def critic_onepass_grads(x, h1, h2, g1, g2, g3, ps):
+    """The critic's gradients W1, b1, W2, b2, W3, b3, W4, b4 from fjsp_a2c_critic_fused's outputs."""
+    return (_critic_wgrad(g1, x, GLOBAL_DIM), ps[:256], _critic_wgrad(g2, h1), ps[256:512],
+            _critic_wgrad(g3, h2), ps[512:640], ps[640:768].view(1, 128), ps[768:769])
 
 
 @torch.no_grad()
 def critic_onepass_compute(x, coef, W1, b1, W2, b2, W3, b3, W4, b4):
-    """_CriticOnePass's work on the current stream: (the critic loss 0-d f32, the gradients of
-    W1, b1, W2, b2, W3, b3, W4, b4)."""
+    """_CriticOnePass's kernel pass on the current stream: (the critic loss 0-d f32, the inputs of
+    critic_onepass_grads: x and the per-state activations / activation gradients the kernel wrote,
+    and the per-tile bias / value-head partial sums summed)."""
     U = x.shape[0]
     dev = x.device
     cw = pack_critic_weights(W1, b1, W2, b2, W3, b3, W4, b4)
@@ -251,10 +262,7 @@ def critic_onepass_compute(x, coef, W1, b1, W2, b2, W3, b3, W4, b4):
     nat.check(nat.lib().fjsp_a2c_critic_fused(V(x), U, V(cw), V(w3t), V(w2t), V(c), V(h1), V(h2), V(g3), V(g2),
                                               V(g1), V(part), V(loss), None,
                                               ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
-    ps = part.sum(0)
-    grads = (_critic_wgrad(g1, x, GLOBAL_DIM), ps[:256], _critic_wgrad(g2, h1), ps[256:512],
-             _critic_wgrad(g3, h2), ps[512:640], ps[640:768].view(1, 128), ps[768:769])
-    return loss.sum().float(), grads
+    return loss.sum().float(), (x, h1, h2, g1, g2, g3, part.sum(0))
 
 
 def slab_stats(ret=None, adv=None):
@@ -630,6 +638,11 @@ def bucket(u):
     return -(-u // step) * step
 
 
+# the station agents' rows of a grouping of the 8 actor inputs (+ the critic's): 3 input features
+# each, a few dozen distinct inputs per batch (batch_stats), grouped by the counting sort
+STATION_ROWS = tuple(range(2, NA))
+
+
 class RowGroups:
     """Distinct values of each row of keys int64 [R, S] (one flat sort for all rows):
     U[r] groups in row r; inv [R, S] = each sample's group, first [R, Umax] = a representative
@@ -637,12 +650,14 @@ class RowGroups:
     sample's group, perm [R, S] / ends [R, Umax] = the samples sorted by group and the end of
     each group's run (padding: S)."""
 
-    def __init__(self, keys):
+    def __init__(self, keys, lowcard=()):
+        """lowcard: rows expected to hold few distinct keys (<= 64: the station agents' rows),
+        grouped on the GPU by a counting sort instead of the radix sort (same result)."""
         R, S = keys.shape
         assert R <= 16, "the row id lives in bits 59..62 of the sort key"
         dev = keys.device
         if keys.is_cuda and R * S < 2 ** 31:
-            self._init_device(keys)
+            self._init_device(keys, sum(1 << r for r in lowcard if r < R))
             return
         # one flat sort for all rows: the row in bits 59..62 above 59 bits of the key (the
         # grouping is verified by the caller, so a shorter key only risks a dense fallback)
@@ -666,7 +681,7 @@ class RowGroups:
         self.perm = perm
         self.gsorted = None   # the run sums' kernel input (device path only)
 
-    def _init_device(self, keys):
+    def _init_device(self, keys, lowcard=0):
         """The same grouping by the library's kernels (fjsp_a2c_group_sort / _runs: one radix sort
         with 32-bit sample positions, one scan, one scatter pass; the torch path below does a 64-bit
         payload sort, a blocked prefix sum, a binary search per group and three gathers)."""
@@ -684,10 +699,15 @@ class RowGroups:
         flat, srt = E(RS, torch.int64), E(RS, torch.int64)
         pos, spos, runs, scan = (E(RS, torch.int32) for _ in range(4))
         counts = E(R, torch.int64)
-        nat.check(L.fjsp_a2c_group_sort(V(k), R, S, V(temp), tb.value, V(flat), V(srt), V(pos), V(spos), V(runs),
-                                        V(scan), V(counts), st))
+        nat.check(L.fjsp_a2c_group_sort(V(k), R, S, lowcard, V(temp), tb.value, V(flat), V(srt), V(pos), V(spos),
+                                        V(runs), V(scan), V(counts), st))
+        U = counts.tolist()                                       # the one host sync
+        if min(U) < 0:   # a lowcard row held more than 64 distinct keys: the radix sort for every row
+            nat.check(L.fjsp_a2c_group_sort(V(k), R, S, 0, V(temp), tb.value, V(flat), V(srt), V(pos), V(spos),
+                                            V(runs), V(scan), V(counts), st))
+            U = counts.tolist()
         del temp, flat, srt, pos, runs
-        self.U = counts.tolist()                                  # the one host sync
+        self.U = U
         umax = bucket(max(self.U))
         starts, first, ends = (E((R, umax), torch.int64) for _ in range(3))
         perm, inv, rep = (E((R, S), torch.int64) for _ in range(3))
@@ -946,7 +966,7 @@ class A2CLosses:
         elif dedup:
             f3 = f3.contiguous()
             rows = torch.empty(S, GROUP_ROW, dtype=torch.float32, device=f3.device) if f3.is_cuda else None
-            gr = RowGroups(group_keys(f3, rows))                    # 8 actor rows + the critic's
+            gr = RowGroups(group_keys(f3, rows), STATION_ROWS)      # 8 actor rows + the critic's
             ga, gc = gr.rows(0, NA), gr.rows(NA, NA + 1)
             x = gv = None
             if not feats.is_cuda:

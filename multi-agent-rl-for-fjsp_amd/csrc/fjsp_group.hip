@@ -236,6 +236,199 @@ __global__ void __launch_bounds__(RS_T) k_run_carry(int64_t nch, int64_t umax, c
     }
 }
 
+// ---- the low-cardinality rows (lowcard mask): a stable counting sort instead of the radix sort.
+// The station agents' rows of the A2C grouping hold <= ~30 distinct keys per 10^6 samples; a
+// radix sort pays 8 passes over them (8 bits per pass of 63 key bits).  Per such row: the distinct
+// keys in a 256-slot open-addressing table (LC_CAP = 64 at most, else the row is reported as
+// overflowing: counts[r] = -1, and the caller groups again without the mask), their ranks in key
+// order, per 1 024-sample chunk the samples of each rank (one wave per chunk), one exclusive scan
+// over (row, rank, chunk), and a stable scatter: a wave takes its chunk's samples in order, 64 at
+// a time, and each sample's position is its rank's running offset + the lanes before it with the
+// same rank (six ballots).  The output is the radix sort's exactly: per row the (row-tagged) keys
+// ascending, equal keys in sample order.
+constexpr int LC_CAP = 64, LC_SLOTS = 256, LC_CH = 1024;
+struct RowList {   // row ids, by value in the kernel arguments
+    int32_t r[16];
+};
+constexpr uint64_t LC_EMPTY = ~0ull;   // never a masked key (bit 63 is clear)
+
+__device__ __forceinline__ int lc_hash(uint64_t k) { return (int)((k * 0x9E3779B97F4A7C15ull) >> 56); }
+
+// insert k into a 256-slot table (LDS or global); returns true if it was new; *over on overflow
+template <bool SHARED>
+__device__ __forceinline__ bool lc_insert(uint64_t* tbl, uint64_t k, bool* full) {
+    int h = lc_hash(k);
+    for (int probe = 0; probe < LC_SLOTS; probe++, h = (h + 1) & (LC_SLOTS - 1)) {
+        uint64_t cur = tbl[h];
+        if (cur == k) return false;
+        if (cur == LC_EMPTY) {
+            const uint64_t old = SHARED ? atomicCAS((unsigned long long*)&tbl[h], (unsigned long long)LC_EMPTY,
+                                                    (unsigned long long)k)
+                                        : atomicCAS((unsigned long long*)&tbl[h], (unsigned long long)LC_EMPTY,
+                                                    (unsigned long long)k);
+            if (old == LC_EMPTY) return true;
+            if (old == k) return false;
+        }
+    }
+    *full = true;
+    return false;
+}
+
+__device__ __forceinline__ int lc_find(const uint64_t* tbl, uint64_t k) {   // slot of a key known to be there
+    int h = lc_hash(k);
+    for (int probe = 0; probe < LC_SLOTS; probe++, h = (h + 1) & (LC_SLOTS - 1))
+        if (tbl[h] == k) return h;
+    return -1;
+}
+
+// grid (chunks, low rows), 256 threads: the chunk's distinct keys, then into the row's global table
+// (gtbl [nl][256], gcnt [nl], over [nl]; rows[i] = the i-th low row)
+__global__ void __launch_bounds__(256) k_lc_distinct(const uint64_t* __restrict__ keys, RowList rows,
+                                                     int64_t S, uint64_t* __restrict__ gtbl, uint32_t* __restrict__ gcnt,
+                                                     uint32_t* __restrict__ over) {
+    __shared__ uint64_t t[LC_SLOTS];
+    __shared__ uint32_t n;
+    __shared__ bool full;
+    const int li = (int)blockIdx.y, tid = (int)threadIdx.x;
+    const int64_t r = rows.r[li], c0 = (int64_t)blockIdx.x * LC_CH;
+    t[tid] = LC_EMPTY;
+    if (tid == 0) { n = 0; full = false; }
+    __syncthreads();
+    for (int i = tid; i < LC_CH; i += 256) {
+        const int64_t s = c0 + i;
+        if (s >= S) break;
+        const uint64_t k = keys[r * S + s] & KEY_MASK;
+        bool f = false;
+        if (lc_insert<true>(t, k, &f)) atomicAdd(&n, 1u);
+        if (f) full = true;
+    }
+    __syncthreads();
+    if (full || n > (uint32_t)LC_CAP) {
+        if (tid == 0) atomicOr(&over[li], 1u);
+        return;
+    }
+    const uint64_t k = t[tid];
+    if (k != LC_EMPTY) {
+        bool f = false;
+        if (lc_insert<false>(gtbl + (int64_t)li * LC_SLOTS, k, &f)) {
+            if (atomicAdd(&gcnt[li], 1u) + 1u > (uint32_t)LC_CAP) atomicOr(&over[li], 1u);
+        }
+        if (f) atomicOr(&over[li], 1u);
+    }
+}
+
+// one workgroup of 256 per low row: rank of every used slot in ascending key order (grank [nl][256])
+__global__ void __launch_bounds__(256) k_lc_rank(const uint64_t* __restrict__ gtbl, const uint32_t* __restrict__ over,
+                                                 uint8_t* __restrict__ grank) {
+    __shared__ uint64_t t[LC_SLOTS];
+    const int li = (int)blockIdx.x, tid = (int)threadIdx.x;
+    if (over[li]) return;
+    const uint64_t k = gtbl[(int64_t)li * LC_SLOTS + tid];
+    t[tid] = k;
+    __syncthreads();
+    int rank = 0;
+    for (int j = 0; j < LC_SLOTS; j++) rank += (t[j] != LC_EMPTY && t[j] < k) ? 1 : 0;
+    grank[(int64_t)li * LC_SLOTS + tid] = k == LC_EMPTY ? (uint8_t)255 : (uint8_t)rank;
+}
+
+// one wave per (chunk, low row): samples per rank, hist [nl][LC_CAP][nch]
+// (an overflowed row counts its chunk's samples as rank 0, so every row's counts still sum to S and
+// the scan's offsets of the other rows stay in their rows; its samples are not scattered)
+__global__ void __launch_bounds__(64) k_lc_hist(const uint64_t* __restrict__ keys, RowList rows,
+                                                int64_t S, int64_t nch, const uint64_t* __restrict__ gtbl,
+                                                const uint8_t* __restrict__ grank, const uint32_t* __restrict__ over,
+                                                uint32_t* __restrict__ hist) {
+    __shared__ uint64_t t[LC_SLOTS];
+    __shared__ uint8_t rk[LC_SLOTS];
+    __shared__ uint32_t h[LC_CAP];
+    const int li = (int)blockIdx.y, lane = (int)threadIdx.x;
+    const int64_t r = rows.r[li], c = blockIdx.x;
+    if (over[li]) {
+        const int64_t len = S - c * LC_CH < LC_CH ? S - c * LC_CH : LC_CH;
+        hist[((int64_t)li * LC_CAP + lane) * nch + c] = lane == 0 ? (uint32_t)len : 0u;
+        return;
+    }
+    for (int j = lane; j < LC_SLOTS; j += 64) {
+        t[j] = gtbl[(int64_t)li * LC_SLOTS + j];
+        rk[j] = grank[(int64_t)li * LC_SLOTS + j];
+    }
+    h[lane] = 0;
+    __syncthreads();
+    for (int i = lane; i < LC_CH; i += 64) {
+        const int64_t s = c * LC_CH + i;
+        if (s >= S) break;
+        const int q = rk[lc_find(t, keys[r * S + s] & KEY_MASK)];
+        atomicAdd(&h[q], 1u);
+    }
+    __syncthreads();
+    hist[((int64_t)li * LC_CAP + lane) * nch + c] = h[lane];
+}
+
+// one wave per (chunk, low row): the stable scatter into the row's part of sorted / spos
+__global__ void __launch_bounds__(64) k_lc_scatter(const uint64_t* __restrict__ keys, RowList rows,
+                                                   int64_t S, int64_t nch, const uint64_t* __restrict__ gtbl,
+                                                   const uint8_t* __restrict__ grank, const uint32_t* __restrict__ over,
+                                                   const uint32_t* __restrict__ offs, uint64_t* __restrict__ sorted,
+                                                   uint32_t* __restrict__ spos) {
+    __shared__ uint64_t t[LC_SLOTS];
+    __shared__ uint8_t rk[LC_SLOTS];
+    __shared__ uint32_t base[LC_CAP];
+    const int li = (int)blockIdx.y, lane = (int)threadIdx.x;
+    if (over[li]) return;
+    const int64_t r = rows.r[li], c = blockIdx.x;
+    for (int j = lane; j < LC_SLOTS; j += 64) {
+        t[j] = gtbl[(int64_t)li * LC_SLOTS + j];
+        rk[j] = grank[(int64_t)li * LC_SLOTS + j];
+    }
+    // offs: the exclusive scan over [nl][LC_CAP][nch]; row li's samples start at li * S there
+    base[lane] = offs[((int64_t)li * LC_CAP + lane) * nch + c] - (uint32_t)(li * S);
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int i0 = 0; i0 < LC_CH; i0 += 64) {
+        const int64_t s = c * LC_CH + i0 + lane;
+        const bool ok = s < S;
+        uint64_t k = 0;
+        int q = 0;
+        if (ok) {
+            k = keys[r * S + s] & KEY_MASK;
+            q = rk[lc_find(t, k)];
+        }
+        uint64_t peers = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 6; b++) {
+            const uint64_t m = __ballot((q >> b) & 1);
+            peers &= ((q >> b) & 1) ? m : ~m;
+        }
+        const uint32_t my = base[q] + (uint32_t)__popcll(peers & lt);
+        __builtin_amdgcn_wave_barrier();
+        if (ok && (peers >> lane) == 1ull) base[q] += (uint32_t)__popcll(peers);   // the group's last lane
+        __builtin_amdgcn_wave_barrier();
+        if (ok) {
+            const int64_t d = r * S + my;
+            sorted[d] = k | ((uint64_t)r << 59);
+            spos[d] = (uint32_t)(r * S + s);
+        }
+    }
+}
+
+// flat / pos for the high-cardinality rows only, compacted (hrows[i] = the i-th such row)
+__global__ void __launch_bounds__(256) k_group_flat_rows(const uint64_t* __restrict__ keys, RowList hrows,
+                                                         int64_t S, int64_t HS, uint64_t* __restrict__ flat,
+                                                         uint32_t* __restrict__ pos) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= HS) return;
+    const int64_t hi = i / S, s = i - hi * S;
+    const uint64_t r = (uint64_t)hrows.r[hi];
+    flat[i] = (keys[r * S + s] & KEY_MASK) | (r << 59);
+    pos[i] = (uint32_t)(r * S + s);
+}
+
+// counts[r] = -1 for a low row that overflowed LC_CAP (the caller groups again without the mask)
+__global__ void k_lc_flag(RowList rows, int32_t nl, const uint32_t* __restrict__ over, int64_t* __restrict__ counts) {
+    const int i = (int)threadIdx.x;
+    if (i < nl && over[i]) counts[rows.r[i]] = -1;
+}
+
 int launch_error() {
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
@@ -252,19 +445,22 @@ unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
 extern "C" int fjsp_a2c_group_temp_bytes(int64_t count, uint64_t* bytes) {
     if (count <= 0 || count >= (1ll << 31)) return fjsp_internal_fail("fjsp_a2c_group_temp_bytes: count must be in (0, 2^31)");
     if (!bytes) return fjsp_internal_fail("fjsp_a2c_group_temp_bytes: null pointer");
-    size_t a = 0, b = 0;
+    size_t a = 0, b = 0, c = 0;
     if (rocprim::radix_sort_pairs(nullptr, a, (const uint64_t*)nullptr, (uint64_t*)nullptr, (const uint32_t*)nullptr,
                                   (uint32_t*)nullptr, (uint32_t)count, 0u, 63u) != hipSuccess ||
         rocprim::inclusive_scan(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)count,
+                                rocprim::plus<uint32_t>()) != hipSuccess ||
+        rocprim::exclusive_scan(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)count,
                                 rocprim::plus<uint32_t>()) != hipSuccess)
         return fjsp_internal_fail("fjsp_a2c_group_temp_bytes: rocprim size query failed");
-    *bytes = (uint64_t)(a > b ? a : b);
+    a = a > b ? a : b;
+    *bytes = (uint64_t)(a > c ? a : c);
     return 0;
 }
 
-extern "C" int fjsp_a2c_group_sort(const uint64_t* keys, int32_t R, int64_t S, void* temp, uint64_t temp_bytes,
-                                   uint64_t* flat, uint64_t* sorted, uint32_t* pos, uint32_t* spos, uint32_t* runs,
-                                   uint32_t* scan, int64_t* counts, void* stream) {
+extern "C" int fjsp_a2c_group_sort(const uint64_t* keys, int32_t R, int64_t S, uint32_t lowcard, void* temp,
+                                   uint64_t temp_bytes, uint64_t* flat, uint64_t* sorted, uint32_t* pos, uint32_t* spos,
+                                   uint32_t* runs, uint32_t* scan, int64_t* counts, void* stream) {
     const int64_t RS = (int64_t)R * S;
     if (R <= 0 || R > 16 || S <= 0 || RS >= (1ll << 31))
         return fjsp_internal_fail("fjsp_a2c_group_sort: need 0 < R <= 16, S > 0, R * S < 2^31");
@@ -274,12 +470,86 @@ extern "C" int fjsp_a2c_group_sort(const uint64_t* keys, int32_t R, int64_t S, v
     if (int rc = fjsp_a2c_group_temp_bytes(RS, &need)) return rc;
     if (temp_bytes < need) return fjsp_internal_fail("fjsp_a2c_group_sort: temp buffer too small");
     const hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_group_flat, dim3(blocks(RS)), dim3(256), 0, st, keys, S, RS, flat, pos);
-    if (int rc = launch_error()) return rc;
+    // the counting path's rows, and its scratch: the per-(row, rank, chunk) counts and their scan
+    // in runs / scan (free until the run starts), the tables at the end of pos (the radix sort's
+    // input uses only its first (R - nl) * S words)
+    RowList lrl{}, hrl{};
+    int32_t* lrows = lrl.r;
+    int32_t* hrows = hrl.r;
+    int nl = 0, nh = 0;
+    for (int r = 0; r < R; r++) {
+        if ((lowcard >> r) & 1u) lrows[nl++] = r;
+        else hrows[nh++] = r;
+    }
+    const int64_t nch = (S + LC_CH - 1) / LC_CH;
+    const size_t tbl_bytes = (size_t)nl * LC_SLOTS * 8 + 32 * 4 + (size_t)nl * LC_SLOTS + 64;
+    if (nl > 0 && ((int64_t)nl * LC_CAP * nch > RS || tbl_bytes > (size_t)nl * (size_t)S * 4)) {
+        for (int i = 0; i < nl; i++) hrows[nh++] = lrows[i];   // too small for the scratch: radix sort them all
+        nl = 0;
+        for (int a = 0; a < nh; a++)   // keep ascending row order
+            for (int b = a + 1; b < nh; b++)
+                if (hrows[b] < hrows[a]) { const int32_t x = hrows[a]; hrows[a] = hrows[b]; hrows[b] = x; }
+    }
     size_t tb = (size_t)temp_bytes;
-    // stable LSD radix sort over the 63 key bits (row id 59..62 above 59 hash bits)
-    if (rocprim::radix_sort_pairs(temp, tb, flat, sorted, pos, spos, (uint32_t)RS, 0u, 63u, st) != hipSuccess)
-        return fjsp_internal_fail("fjsp_a2c_group_sort: radix sort failed");
+    if (nl == 0) {
+        hipLaunchKernelGGL(k_group_flat, dim3(blocks(RS)), dim3(256), 0, st, keys, S, RS, flat, pos);
+        if (int rc = launch_error()) return rc;
+        // stable LSD radix sort over the 63 key bits (row id 59..62 above 59 hash bits)
+        if (rocprim::radix_sort_pairs(temp, tb, flat, sorted, pos, spos, (uint32_t)RS, 0u, 63u, st) != hipSuccess)
+            return fjsp_internal_fail("fjsp_a2c_group_sort: radix sort failed");
+    } else {
+        // small device arrays (row lists, tables) at the end of pos
+        char* ex = (char*)(pos + RS) - tbl_bytes;
+        ex = (char*)(((uintptr_t)ex) & ~(uintptr_t)63);
+        uint64_t* gtbl = (uint64_t*)ex;
+        uint32_t* gcnt = (uint32_t*)(gtbl + (size_t)nl * LC_SLOTS);   // [16] counts, then [16] overflow flags
+        uint32_t* over = gcnt + 16;
+        uint8_t* grank = (uint8_t*)(over + 16);
+        if (hipMemsetAsync(gtbl, 0xFF, (size_t)nl * LC_SLOTS * 8, st) != hipSuccess ||
+            hipMemsetAsync(gcnt, 0, 32 * 4, st) != hipSuccess)
+            return fjsp_internal_fail("fjsp_a2c_group_sort: scratch set-up failed");
+        if (nh > 0) {
+            const int64_t HS = (int64_t)nh * S;
+            hipLaunchKernelGGL(k_group_flat_rows, dim3(blocks(HS)), dim3(256), 0, st, keys, hrl, S, HS, flat, pos);
+            if (int rc = launch_error()) return rc;
+            if (rocprim::radix_sort_pairs(temp, tb, flat, sorted, pos, spos, (uint32_t)HS, 0u, 63u, st) != hipSuccess)
+                return fjsp_internal_fail("fjsp_a2c_group_sort: radix sort failed");
+            // the i-th high row's sorted block to its own row (last first: blocks only move up)
+            for (int i = nh - 1; i >= 0; i--) {
+                if (hrows[i] == i) continue;
+                if (hipMemcpyAsync(sorted + (int64_t)hrows[i] * S, sorted + (int64_t)i * S, 8 * (size_t)S,
+                                   hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                    hipMemcpyAsync(spos + (int64_t)hrows[i] * S, spos + (int64_t)i * S, 4 * (size_t)S,
+                                   hipMemcpyDeviceToDevice, st) != hipSuccess)
+                    return fjsp_internal_fail("fjsp_a2c_group_sort: block move failed");
+            }
+        }
+        hipLaunchKernelGGL(k_lc_distinct, dim3((unsigned)nch, (unsigned)nl), dim3(256), 0, st, keys, lrl, S, gtbl, gcnt,
+                           over);
+        if (int rc = launch_error()) return rc;
+        hipLaunchKernelGGL(k_lc_rank, dim3((unsigned)nl), dim3(256), 0, st, gtbl, over, grank);
+        if (int rc = launch_error()) return rc;
+        hipLaunchKernelGGL(k_lc_hist, dim3((unsigned)nch, (unsigned)nl), dim3(64), 0, st, keys, lrl, S, nch, gtbl, grank,
+                           over, runs);
+        if (int rc = launch_error()) return rc;
+        const size_t nhist = (size_t)nl * LC_CAP * (size_t)nch;
+        tb = (size_t)temp_bytes;
+        if (rocprim::exclusive_scan(temp, tb, runs, scan, 0u, nhist, rocprim::plus<uint32_t>(), st) != hipSuccess)
+            return fjsp_internal_fail("fjsp_a2c_group_sort: count scan failed");
+        hipLaunchKernelGGL(k_lc_scatter, dim3((unsigned)nch, (unsigned)nl), dim3(64), 0, st, keys, lrl, S, nch, gtbl,
+                           grank, over, scan, sorted, spos);
+        if (int rc = launch_error()) return rc;
+        // k_lc_flag below reads over after the counts
+        hipLaunchKernelGGL(k_group_new, dim3(blocks(RS)), dim3(256), 0, st, sorted, S, RS, runs);
+        if (int rc = launch_error()) return rc;
+        tb = (size_t)temp_bytes;
+        if (rocprim::inclusive_scan(temp, tb, runs, scan, (size_t)RS, rocprim::plus<uint32_t>(), st) != hipSuccess)
+            return fjsp_internal_fail("fjsp_a2c_group_sort: scan failed");
+        hipLaunchKernelGGL(k_group_counts, dim3(1), dim3(64), 0, st, scan, R, S, counts);
+        if (int rc = launch_error()) return rc;
+        hipLaunchKernelGGL(k_lc_flag, dim3(1), dim3(64), 0, st, lrl, nl, over, counts);
+        return launch_error();
+    }
     hipLaunchKernelGGL(k_group_new, dim3(blocks(RS)), dim3(256), 0, st, sorted, S, RS, runs);
     if (int rc = launch_error()) return rc;
     tb = (size_t)temp_bytes;

@@ -792,8 +792,10 @@ __device__ __forceinline__ void tile_observe(const StepArgs& St, unsigned char* 
                                              int wave) {
     uint32_t* rf = reinterpret_cast<uint32_t*>(s_mem + STG_F32);
     fjsp::Env E;
+    // the mask wave never reads the status word (observe() only ORs flags into it) and does not
+    // load it: wave 2 rewrites that staged word below, with no barrier between the two waves
 #pragma unroll
-    for (int i = 0; i < fjsp::NSTATE; i++) E.w[i] = rf[(fjsp::NFEAT + i) * 64 + lane];
+    for (int i = 0; i < fjsp::NSTATE; i++) E.w[i] = (wave == 1 && i == 2) ? 0u : rf[(fjsp::NFEAT + i) * 64 + lane];
     fjsp::Cfg C = St.C;
     C.lut = reinterpret_cast<const double*>(s_state + fjsp::NSTATE * 64);
     if (wave == 1) {

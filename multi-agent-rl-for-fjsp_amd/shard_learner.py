@@ -185,7 +185,7 @@ def combine(feats, masks, actions, ret, adv, mean, std, world):
         bad = (~((m == 0) | (m == 1))).any()
         info = shard_info_words(m, actions)
         tk = torch.cat([A._fmix64(keys[:NA] ^ A._fmix64(info.to(torch.int64) * _MIX + 1)), keys[NA:]])
-    g = A.RowGroups(tk)                                                                  # 8 + 1 rows
+    g = A.RowGroups(tk, A.STATION_ROWS)                                                  # 8 + 1 rows
     U = g.U
     # every sample equals its group's representative: the input bitwise, the mask bits and action
     if rows.is_cuda:

@@ -61,10 +61,10 @@ def test_grouping_entries_validate_arguments_without_gpu():
     cnt = ctypes.c_uint64()
     assert L.fjsp_a2c_group_temp_bytes(0, ctypes.byref(cnt)) != 0
     assert L.fjsp_a2c_group_temp_bytes(1 << 31, ctypes.byref(cnt)) != 0
-    assert L.fjsp_a2c_group_sort(one, 17, 100, one, 1 << 20, one, one, one, one, one, one, one, None) != 0
+    assert L.fjsp_a2c_group_sort(one, 17, 100, 0, one, 1 << 20, one, one, one, one, one, one, one, None) != 0
     assert b"R <= 16" in L.fjsp_last_error()
-    assert L.fjsp_a2c_group_sort(one, 9, 1 << 28, one, 1 << 20, one, one, one, one, one, one, one, None) != 0
-    assert L.fjsp_a2c_group_sort(None, 9, 100, one, 1 << 20, one, one, one, one, one, one, one, None) != 0
+    assert L.fjsp_a2c_group_sort(one, 9, 1 << 28, 0, one, 1 << 20, one, one, one, one, one, one, one, None) != 0
+    assert L.fjsp_a2c_group_sort(None, 9, 100, 0, one, 1 << 20, one, one, one, one, one, one, one, None) != 0
     assert b"null" in L.fjsp_last_error()
     assert L.fjsp_a2c_group_runs(one, one, 9, 100, 0, one, one, one, one, one, one, one, None) != 0
     assert L.fjsp_a2c_run_sums_bytes(0, 100, ctypes.byref(cnt)) != 0

@@ -208,6 +208,37 @@ def test_policy_launch_variants_are_bit_identical(M, n, init, var, values):
                 assert torch.equal(runs[0][b][k], r[b][k]), (b, k)
 
 
+def test_collect_graphs_interleaved_with_allocations(M):
+    """Two learners' captured collects (each graph in its own private pool) replayed in turn, with
+    an update, a recapture (deterministic toggled) and allocation churn between the replays, equal
+    their eager twins byte for byte: nothing allocated after a capture may land in a live graph's
+    memory (the aliasing that made r04's shared-pool update graphs diverge)."""
+    A, V = M["A"], M["V"]
+    n, T = 320, 24
+    keys = ("feats", "masks", "actions", "values", "rewards", "term", "trunc", "status")
+    L = {}
+    for name, seed in (("a", 5), ("b", 6)):
+        for graph in (True, False):
+            x = A.VecMultiAgentA2C(V.FJSPVecEnv(n), batch_size=T, seed=seed, use_graph=graph)
+            x.reset(seeds=torch.arange(n) + seed, num_orders=25)
+            L[name, graph] = x
+    junk = []
+    for it in range(5):
+        det = it == 3                                   # batch 3 recaptures (deterministic), 4 again
+        for name in ("a", "b"):
+            for graph in (True, False):
+                L[name, graph].collect(deterministic=det)
+            junk.append(torch.randn(1 << 20, device="cuda") * it)   # churn between the replays
+            if len(junk) > 3:
+                junk.pop(0)
+            for k in keys:
+                assert torch.equal(L[name, True]._bufs[k], L[name, False]._bufs[k]), (it, name, k)
+            for graph in (True, False):
+                L[name, graph].update()
+                L[name, graph].roll_over()
+        torch.cuda.empty_cache()
+
+
 def test_eager_policy_graph_rekeys_each_batch(M):
     """The PyTorch policy path (fused_policy=False) captured into the collect graph reads the
     draw key from the device: every replay draws new actions, and each batch equals the eager
@@ -778,11 +809,14 @@ def test_prefix_at_equals_full_prefix_sum_on_gpu(M):
         assert torch.equal(torch.gather(A._prefix_sum(w.double()), -1, idx), A._prefix_at(w, idx))
 
 
-def test_row_groups_kernels_equal_stable_sort(M):
+@pytest.mark.parametrize("lowcard", [(), (2, 3, 4, 5, 6, 7), (0, 1, 4, 5, 6), (4,), tuple(range(9))])
+def test_row_groups_kernels_equal_stable_sort(M, lowcard):
     """RowGroups on the GPU (fjsp_a2c_group_sort / _runs) equals the grouping by a stable sort of
     each row's 59 key bits computed here in numpy: group counts, the sorted order (equal keys in
     sample order), each sample's group and representative, each group's first sample and run end
-    (padding groups: end S, first = the row's last sorted sample)."""
+    (padding groups: end S, first = the row's last sorted sample).  lowcard: rows grouped by the
+    counting sort (<= 64 distinct keys; rows 2, 3, 7 and 8 hold more, so those requests fall back
+    to the radix sort for the whole grouping)."""
     import numpy as np
     A = M["A"]
     R, S = 9, 50001
@@ -790,7 +824,7 @@ def test_row_groups_kernels_equal_stable_sort(M):
     card = [3, 28, 1225, 40000, 1, 7, 2, 50001, 600]
     base = torch.stack([torch.randint(0, c, (S,), generator=g) for c in card])
     keys = base * -7046029254386353131 + torch.arange(R)[:, None] * 977   # int64 wrap: keys over all 64 bits
-    G = A.RowGroups(keys.cuda())
+    G = A.RowGroups(keys.cuda(), lowcard)
     k = keys.numpy()
     rows = np.arange(R, dtype=np.int64)[:, None]
     flat = (k & ((1 << 59) - 1)) | (rows << 59)
@@ -815,6 +849,24 @@ def test_row_groups_kernels_equal_stable_sort(M):
     rep = first[rows, inv]
     for name, want in (("perm", perm), ("inv", inv), ("rep", rep), ("first", first), ("ends", ends)):
         assert np.array_equal(getattr(G, name).cpu().numpy(), want), name
+
+
+@pytest.mark.parametrize("S", [1, 63, 1024, 1025, 1048576])
+def test_row_groups_counting_sort_equals_radix(M, S):
+    """The station rows' counting sort (lowcard) at the A2C batch's size: every output of the
+    grouping equal to the radix sort's, with rows of 1, 2, 30 and 64 distinct keys (the counting
+    path's limit), a skewed row and partial 1 024-sample chunks."""
+    A = M["A"]
+    g = torch.Generator().manual_seed(11)
+    cols = [torch.zeros(S, dtype=torch.int64), torch.randint(0, 2, (S,), generator=g),
+            torch.randint(0, 30, (S,), generator=g), torch.randint(0, 64, (S,), generator=g),
+            (torch.rand(S, generator=g) ** 8 * 40).long(), torch.randint(0, 5000, (S,), generator=g)]
+    keys = (torch.stack(cols) * -7046029254386353131 + 12345).cuda()
+    a = A.RowGroups(keys, (0, 1, 2, 3, 4))
+    b = A.RowGroups(keys)
+    assert a.U == b.U
+    for name in ("perm", "inv", "rep", "first", "ends", "gsorted"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
 
 
 @pytest.mark.parametrize("S", [1, 1023, 50001, 300000, 1300000])
