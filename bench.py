@@ -150,8 +150,8 @@ def dropin_latency(dev, steps=2000, warm=200):
     Python iteration on ONE env, then the visualiser's reads of simulation.agv.position and
     agv.carrying_tray, the episode restarted with reset() when env.agents empties (the loop's
     `while self.env.agents`).  Wall time per call on this host, beside the reference's ~115 us.
-    Also: the same without the agv reads, and FJSPSimulation.step alone split into its parts
-    (kernel time from the handle's events)."""
+    Also: the same without the agv reads, the same through one launch + one synchronisation per
+    step instead of the step server, and one server request alone."""
     W = importlib.import_module("multi-agent-rl-for-fjsp_amd.FJSPParallelEnvWrapper")
     env = W.FJSPParallelEnv()
     env.reset(seed=0, options={"num_orders": 30})
@@ -176,23 +176,32 @@ def dropin_latency(dev, steps=2000, warm=200):
     loop(True, warm)
     with_agv, resets = loop(True, steps)
     no_agv, _ = loop(False, steps)
-    # the kernel alone (the handle's events around each launch), 200 steps
+    # the same loop through one launch + one synchronisation per step (the step server off)
+    sim.use_server = False
+    loop(True, warm)
+    launch_path, _ = loop(True, steps)
+    sim.use_server = True
+    # the device part alone: one server request (doorbell + wait) on the facade's record
+    L, h = sim._L, sim._h
     nat = importlib.import_module("multi-agent-rl-for-fjsp_amd._native")
-    k = []
     env.reset(seed=1, options={"num_orders": 30})
-    nat.check(nat.lib().fjsp_set_option(sim._venv.handle, b"timing", 1))
-    for t in range(200):
-        env.step(acts[t])
-        k.append(sim._venv.last_kernel_ms() * 1e3)
-        if not env.agents:
-            env.reset(options={"num_orders": 30})
-    nat.check(nat.lib().fjsp_set_option(sim._venv.handle, b"timing", 0))
+    nat.check(L.fjsp_server_start(h, sim._act_ptr, 0, sim._packed.ref_full))
+    for _ in range(100):
+        nat.check(L.fjsp_server_step(h))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        nat.check(L.fjsp_server_step(h))
+    server_us = (time.perf_counter() - t0) / steps * 1e6
+    nat.check(L.fjsp_server_stop(h))
     return {"dropin_n1_us_per_step": with_agv, "dropin_n1_no_agv_reads_us_per_step": no_agv,
-            "kernel_us_median": float(np.median(k)), "resets": resets, "steps": steps,
+            "dropin_n1_launch_path_us_per_step": launch_path, "server_request_us": server_us,
+            "resets": resets, "steps": steps,
             "reference_us_per_step": REF_PY_STEP_US,
             "speedup_vs_reference": REF_PY_STEP_US / with_agv,
             "note": "FJSPParallelEnv.step(dict) + a2c.py:298-305's agv.position / carrying_tray reads, one env, "
-                    "random actions, reset when env.agents empties; reference: SURVEY.md App. E (1 core, same "
+                    "random actions, reset when env.agents empties; the step server carries the canonical-order "
+                    "steps (launch_path: one fjsp_step launch + one synchronisation per step instead); "
+                    "server_request_us: one fjsp_server_step alone; reference: SURVEY.md App. E (1 core, same "
                     "container class), not re-timed on this box (the reference never travels)"}
 
 
@@ -222,10 +231,25 @@ def host_action_step(env, dev, N, K=200):
     run(False)
     a = run(False)
     b = run(True)
+    # the same through the step server: the actions rewritten in one pinned buffer before every
+    # step, one doorbell per step, no launch and no stream synchronisation
+    srv = torch.zeros(8, N, dtype=torch.uint8).pin_memory()
+    env.server_start(srv, autoreset=True, buffers=sbuf)
+    for t in range(20):
+        srv.copy_(host[t])
+        env.server_step()
+    t0 = time.perf_counter()
+    for t in range(K):
+        srv.copy_(host[t])
+        env.server_step()
+    c = (time.perf_counter() - t0) / K * 1e6
+    env.server_stop()
     return {"envs": N, "us_per_step": a, "value": N / (a * 1e-6), "unit": "env-steps/s",
             "us_per_step_with_outputs_to_host": b, "value_with_outputs_to_host": N / (b * 1e-6),
+            "server_us_per_step": c, "server_value": N / (c * 1e-6),
             "note": "actions from pinned host memory every step (H2D + k_step + sync); the second figure also "
-                    "copies obs/masks/rewards/term/trunc back to pinned host memory"}
+                    "copies obs/masks/rewards/term/trunc back to pinned host memory; server_*: the same steps "
+                    "through the step server (fjsp_server_step: resident kernel, host doorbell)"}
 
 
 def load_pmc(workload):

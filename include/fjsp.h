@@ -201,6 +201,23 @@ int fjsp_reset(fjsp_handle* h, const uint32_t* seeds, const uint8_t* env_mask, i
 int fjsp_step(fjsp_handle* h, const uint8_t* actions, const uint8_t* agent_order, int32_t autoreset,
               const fjsp_out* out);
 
+/* Step server (ABI 10; FJSPSimulation.step / FJSPParallelEnv.step called once per Python
+ * iteration, a2c.py:294): a persistent kernel keeps the handle's envs resident (state words in
+ * registers, reward table in LDS, tables warm in L2) and runs one fjsp_step in the canonical dict
+ * order per fjsp_server_step, signalled through a doorbell word in host memory — no launch and no
+ * stream synchronisation per step.  fjsp_server_start(h, actions, autoreset, out): actions =
+ * u8[8][N] the caller rewrites before every fjsp_server_step (pinned host memory, or device memory
+ * whose writes are complete), out = the outputs of every step (pinned host memory or device
+ * memory; T = 1); N <= 16384.  fjsp_server_step: one step of every env, returns when every output
+ * of it is visible to the host.  Any other call on the handle (reset, fjsp_step, read_env,
+ * snapshot, set_reward_weights, ...) first stops the server (its state is written back); the next
+ * fjsp_server_step relaunches it with the same actions / outputs, as it does after 2 ms without a
+ * request (the kernel itself leaves after 5 ms idle, so a device-wide synchronisation issued
+ * between steps waits at most that long).  fjsp_server_stop: leave now. */
+int fjsp_server_start(fjsp_handle* h, const uint8_t* actions, int32_t autoreset, const fjsp_out* out);
+int fjsp_server_step(fjsp_handle* h);
+int fjsp_server_stop(fjsp_handle* h);
+
 /* K fused steps with on-device synthetic actions from the counter RNG
  *   h = fmix64(action_seed ^ fmix64(((uint64)(env_gid0 + e) << 32) | (step0 + k)))
  * (spec: oracle/fjsp_oracle.c oracle_actions).  Outputs are [K][F][N] trajectories. */

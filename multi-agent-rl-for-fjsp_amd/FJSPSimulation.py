@@ -182,6 +182,11 @@ class FJSPSimulation:
         self._last_obs = None
         self._viewcache = None
         self._infocache = {}
+        # the step server (fjsp_server_*): a resident kernel stepping this env on a host doorbell;
+        # configured at the first canonical-order step, relaunched by the library after any other
+        # call on the handle (reset, read_env, a reward-weight upload, a non-canonical step)
+        self.use_server = True
+        self._srv_on = False
         # an empty episode (no orders, no RNG draws), like a freshly constructed reference sim
         self._bind_stream()
         nat.check(self._L.fjsp_reset(self._h, None, None, 0, self._packed.ref_obs))
@@ -268,8 +273,14 @@ class FJSPSimulation:
             ord_arr = None if canon else (ctypes.c_uint8 * 8)(*order)
         self._push_weights()
         self._bind_stream()
-        nat.check(self._L.fjsp_step(self._h, self._act_ptr, ord_arr, 0, self._packed.ref_full))
-        self._wait()
+        if canon and self.use_server:
+            if not self._srv_on:
+                nat.check(self._L.fjsp_server_start(self._h, self._act_ptr, 0, self._packed.ref_full))
+                self._srv_on = True
+            nat.check(self._L.fjsp_server_step(self._h))   # returns with the record written
+        else:
+            nat.check(self._L.fjsp_step(self._h, self._act_ptr, ord_arr, 0, self._packed.ref_full))
+            self._wait()
         p = self._packed.snapshot()
         self._viewcache = None
         obs = self._take_obs(p)

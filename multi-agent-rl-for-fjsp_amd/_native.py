@@ -69,7 +69,8 @@ EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_c
            "fjsp_a2c_relu_bias_grad", "fjsp_a2c_value_head_grad", "fjsp_faults", "fjsp_a2c_critic_forward",
            "fjsp_a2c_critic_backward", "fjsp_gae_shared",
            "fjsp_a2c_policy_step", "fjsp_a2c_group_temp_bytes", "fjsp_a2c_group_sort", "fjsp_a2c_group_runs",
-           "fjsp_a2c_run_sums_bytes", "fjsp_a2c_run_sums", "fjsp_a2c_critic_fused", "fjsp_a2c_shard_keys", "fjsp_a2c_record_head", "fjsp_a2c_pack_mfma", "fjsp_a2c_slab_stats"]
+           "fjsp_a2c_run_sums_bytes", "fjsp_a2c_run_sums", "fjsp_a2c_critic_fused", "fjsp_a2c_shard_keys", "fjsp_a2c_record_head", "fjsp_a2c_pack_mfma", "fjsp_a2c_slab_stats",
+           "fjsp_server_start", "fjsp_server_step", "fjsp_server_stop"]
 POLICY_ACTOR_DPAD, POLICY_CRITIC_DPAD = 16, 48
 POLICY_ACTOR_FLOATS = 3 * 256 * 16 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 8 * 256 + 16
 POLICY_CRITIC_FLOATS = 3 * 256 * 48 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 3 * 128 * 256 // 2 + 128 + 128 + 16
@@ -164,6 +165,9 @@ def lib():
         "fjsp_a2c_critic_backward": (I, [P, P, P, I, P, P, P, P, P, P, P]),
         "fjsp_gae_shared": (I, [P, P, P, I, I, I, D, D, P, P, P]),
         "fjsp_a2c_policy_step": (I, [P, P, P, P, P, P, U32, U32, I, P, P, I, ctypes.POINTER(fjsp_out), I, I, P]),
+        "fjsp_server_start": (I, [P, P, I, ctypes.POINTER(fjsp_out)]),
+        "fjsp_server_step": (I, [P]),
+        "fjsp_server_stop": (I, [P]),
         "fjsp_a2c_group_temp_bytes": (I, [ctypes.c_int64, ctypes.POINTER(U64)]),
         "fjsp_a2c_group_sort": (I, [P, I, ctypes.c_int64, ctypes.c_uint32, P, U64, P, P, P, P, P, P, P, P]),
         "fjsp_a2c_group_runs": (I, [P, P, I, ctypes.c_int64, ctypes.c_int64, P, P, P, P, P, P, P, P]),

@@ -18,6 +18,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <chrono>
 #include <string>
 #include <type_traits>
 
@@ -265,6 +266,96 @@ __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t
     if (threadIdx.x == 0)
         for (int i = 0; i < 8; i++) atomicAdd((unsigned long long*)&g_stamps[i], (unsigned long long)E.st_acc[i]);
     )
+}
+
+// ---------------------------------------------------------------- step server (fjsp_server_*)
+// The one-launch-per-step path pays a launch, a cold chip and a stream synchronisation per step
+// (k_step: 6.8 us of kernel time for ONE env, the facade 18.8 us of launch + sync).  The server is
+// a persistent k_step: each workgroup keeps its 64 envs' state words in registers and the reward
+// table in LDS, and steps them whenever the host bumps a doorbell word in host memory; the host
+// waits for every workgroup's done word.  No launch, no stream operation per step; the tables stay
+// warm in L2.  Control block: host memory (hipHostMalloc, coherent, mapped), one per handle.
+constexpr int SRV_MAX_WG = 256;   // 16 384 envs
+struct alignas(64) ServerCtl {
+    uint32_t seq;                  // host: the step requested (monotonic)
+    uint32_t stop;                 // host: leave now (the state words are written back)
+    uint32_t pad[14];
+    uint32_t done[SRV_MAX_WG];     // kernel: the last seq each workgroup completed
+    uint32_t exited[SRV_MAX_WG];   // kernel: the epoch of the launch that left
+};
+
+// Exit conditions every wave reaches: the stop word, or idle_ticks of the 100 MHz clock without a
+// new request (the host relaunches well before that: fjsp_server_step's restart_ms); a step itself
+// is bounded straight-line code.  Only lane 0 of workgroup 0 polls the host's words (system-scope
+// loads over the bus); it relays each request (and a stop) through two device words, relay[0] =
+// the request, relay[1] = stop, which the other workgroups' lane 0 poll in L2 (both set by the host
+// before the launch: relay[0] = start_seq, relay[1] = 0).
+__global__ void __launch_bounds__(BLOCK) k_step_server(DevState S, Cfg C, ServerCtl* ctl, uint32_t* relay,
+                                                       const uint8_t* actions, int autoreset, fjsp_out out,
+                                                       uint32_t start_seq, uint32_t epoch, uint64_t idle_ticks) {
+    __shared__ double s_lut[RLUT_SIZE];
+    const int lane = threadIdx.x;
+    const int e = blockIdx.x * BLOCK + lane;
+    const bool valid = e < S.n;
+    Env E;
+    if (valid) env_load(E, S.words, S.n, e);
+    for (int i = lane; i < RLUT_SIZE; i += BLOCK) s_lut[i] = C.lut[i];
+    __syncthreads();
+    C.lut = s_lut;
+    const Tables T = tables_of(S, valid ? e : 0);
+    uint32_t last = start_seq;
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        uint32_t sq = last, quit = 0;
+        if (lane == 0 && blockIdx.x == 0) {
+            for (;;) {
+                sq = __hip_atomic_load(&ctl->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (sq != last) {
+                    __hip_atomic_store(&relay[0], sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                if (__hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                    __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+                    __hip_atomic_store(&relay[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    quit = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        } else if (lane == 0) {
+            for (;;) {
+                sq = __hip_atomic_load(&relay[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if (sq != last) break;
+                // the relay's stop, or this workgroup's own idle bound (a backstop: workgroup 0
+                // relays every stop and timeout)
+                if (__hip_atomic_load(&relay[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+                    __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks + idle_ticks / 2) {
+                    quit = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        sq = (uint32_t)__shfl((int)sq, 0);
+        quit = (uint32_t)__shfl((int)quit, 0);
+        if (quit) break;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // every lane: the request's actions are visible
+        last = sq;
+        if (valid) {
+            int act[NA];
+#pragma unroll
+            for (int a = 0; a < NA; a++) act[a] = actions[a * S.n + e];
+            step_and_emit<true>(E, T, C, S, e, act, nullptr, autoreset, out, 0);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this lane's outputs reach host / device memory
+        __syncthreads();
+        if (lane == 0) __hip_atomic_store(&ctl->done[blockIdx.x], sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        t0 = __builtin_amdgcn_s_memrealtime();
+    }
+    if (valid) env_store(E, S.words, S.n, e);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __syncthreads();
+    if (lane == 0) __hip_atomic_store(&ctl->exited[blockIdx.x], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The env's order table and used tray-slot prefix into LDS tables (one lane per env): the
@@ -1910,6 +2001,16 @@ struct fjsp_handle {
     uint32_t* tiles;
     int ntiles;
     int test_stall;   // option "test_stall" (tests): launch the STALL builds of the multi-wave kernels
+    // step server (fjsp_server_*): the persistent k_step_server, its control block in host memory
+    ServerCtl* srv;
+    uint32_t* srv_relay;      // device words: workgroup 0 relays each request / stop to the others
+    hipStream_t srv_stream;   // its own stream: nothing on h->stream queues behind the resident kernel
+    hipEvent_t srv_ev;        // h->stream's work before a (re)launch
+    int srv_configured, srv_running, srv_autoreset, srv_nwg;
+    const uint8_t* srv_actions;
+    fjsp_out srv_out;
+    uint32_t srv_epoch;
+    std::chrono::steady_clock::time_point srv_last;   // the last request (idle relaunch)
 };
 
 static thread_local std::string g_err;
@@ -1953,6 +2054,25 @@ struct DeviceGuard {
 
 extern "C" {
 
+static int server_stop(fjsp_handle* h) {
+    if (!h->srv_running) return 0;
+    DeviceGuard g(h->device);
+    __atomic_store_n(&h->srv->stop, 1u, __ATOMIC_RELEASE);
+    const hipError_t e = hipStreamSynchronize(h->srv_stream);   // bounded: every poll reads stop
+    h->srv_running = 0;
+    __atomic_store_n(&h->srv->stop, 0u, __ATOMIC_RELEASE);
+    if (e != hipSuccess) return hip_fail("step server stop", e);
+    return 0;
+}
+// every other entry point that touches the envs' state stops a resident server first (its state
+// words live in the kernel's registers until it leaves)
+#define SERVER_QUIESCE(h)                                 \
+    do {                                                  \
+        if ((h) && (h)->srv_running) {                    \
+            if (int rc_ = server_stop(h)) return rc_;     \
+        }                                                 \
+    } while (0)
+
 int fjsp_abi_version(void) { return FJSP_ABI_VERSION; }
 const char* fjsp_last_error(void) { return g_err.c_str(); }
 
@@ -1982,6 +2102,7 @@ int fjsp_default_reward_weights(fjsp_reward_weights* w) {
 
 int fjsp_set_reward_weights(fjsp_handle* h, const fjsp_reward_weights* w) {
     if (!h || !w) return fail("null argument");
+    SERVER_QUIESCE(h);
     DeviceGuard g(h->device);
     build_reward_lut(reinterpret_cast<const double*>(w), h->cfg.step_size, h->lut_host);
     // stream-ordered: launches queued before this call keep the old table contents
@@ -2101,6 +2222,11 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
 int fjsp_destroy(fjsp_handle* h) {
     if (!h) return 0;
     DeviceGuard g(h->device);
+    (void)server_stop(h);
+    if (h->srv_ev) (void)hipEventDestroy(h->srv_ev);
+    if (h->srv_stream) (void)hipStreamDestroy(h->srv_stream);
+    if (h->srv) (void)hipHostFree(h->srv);
+    if (h->srv_relay) (void)hipFree(h->srv_relay);
     (void)hipStreamSynchronize(h->stream);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -2118,6 +2244,7 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
     // library-wide options (h may be null): the A2C policy launches' variants
     if (!strncmp(name, "policy_", 7)) return fjsp_internal_policy_option(name, value);
     if (!h) return fail("null handle (only the policy_* options are library-wide)");
+    SERVER_QUIESCE(h);
     if (!strcmp(name, "fused_lds")) { h->use_lds = value < 0 ? -1 : value != 0; return 0; }
     if (!strcmp(name, "staged_stores")) { h->use_staged = value != 0; return 0; }
     if (!strcmp(name, "pipeline")) { h->use_pipe = value != 0; return 0; }
@@ -2172,6 +2299,7 @@ static const fjsp_out kNoOut = {};
 
 int fjsp_reset(fjsp_handle* h, const uint32_t* seeds, const uint8_t* env_mask, int32_t num_orders, const fjsp_out* out) {
     if (!h) return fail("null handle");
+    SERVER_QUIESCE(h);
     if (num_orders < 0 || num_orders > MAX_ORDERS) return fail("num_orders must be in 0..64");
     DeviceGuard g(h->device);
     dim3 grid((h->n + BLOCK - 1) / BLOCK);
@@ -2184,6 +2312,7 @@ int fjsp_reset(fjsp_handle* h, const uint32_t* seeds, const uint8_t* env_mask, i
 
 int fjsp_step(fjsp_handle* h, const uint8_t* actions, const uint8_t* agent_order, int32_t autoreset, const fjsp_out* out) {
     if (!h) return fail("null handle");
+    SERVER_QUIESCE(h);
     if (!actions) return fail("null actions");
     if (!h->has_reset) return fail("fjsp_step before fjsp_reset");
     bool canon = true;
@@ -2217,11 +2346,102 @@ int fjsp_step(fjsp_handle* h, const uint8_t* actions, const uint8_t* agent_order
     return 0;
 }
 
+// ---- the step server (include/fjsp.h fjsp_server_*)
+// The resident kernel leaves after 5 ms without a request (the host relaunches it after 2 ms idle,
+// ~30 us): a process-wide hipDeviceSynchronize (torch.cuda.synchronize) issued between steps waits
+// for the resident kernel, i.e. at most that long.
+static constexpr uint64_t SRV_IDLE_TICKS = 500000ull;     // 5 ms of the 100 MHz clock
+static constexpr int SRV_RESTART_US = 2000;
+static constexpr int SRV_WAIT_MS = 2000;                  // a request not done by then is an error
+
+static int server_launch(fjsp_handle* h) {
+    DeviceGuard g(h->device);
+    HIPCHK(hipEventRecord(h->srv_ev, h->stream));            // the state as h->stream leaves it
+    HIPCHK(hipStreamWaitEvent(h->srv_stream, h->srv_ev, 0));
+    h->srv_epoch++;
+    const uint32_t seq = __atomic_load_n(&h->srv->seq, __ATOMIC_ACQUIRE);
+    for (int w = 0; w < h->srv_nwg; w++) {
+        __atomic_store_n(&h->srv->done[w], seq, __ATOMIC_RELAXED);
+        __atomic_store_n(&h->srv->exited[w], 0u, __ATOMIC_RELAXED);
+    }
+    __atomic_store_n(&h->srv->stop, 0u, __ATOMIC_RELEASE);
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->srv_relay, (int)seq, 1, h->srv_stream));
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(h->srv_relay + 1), 0, 1, h->srv_stream));
+    hipLaunchKernelGGL(k_step_server, dim3(h->srv_nwg), dim3(BLOCK), 0, h->srv_stream, h->S, h->dcfg, h->srv,
+                       h->srv_relay, h->srv_actions, h->srv_autoreset, h->srv_out, seq, h->srv_epoch, SRV_IDLE_TICKS);
+    HIPCHK(hipGetLastError());
+    h->srv_running = 1;
+    h->srv_last = std::chrono::steady_clock::now();
+    h->last_kernel = "k_step_server";
+    return 0;
+}
+
+int fjsp_server_start(fjsp_handle* h, const uint8_t* actions, int32_t autoreset, const fjsp_out* out) {
+    if (!h) return fail("null handle");
+    if (!actions) return fail("null actions");
+    if (!h->has_reset) return fail("fjsp_server_start before fjsp_reset");
+    if (h->n > SRV_MAX_WG * BLOCK) return fail("fjsp_server_start: at most 16384 envs per handle");
+    SERVER_QUIESCE(h);
+    DeviceGuard g(h->device);
+    if (!h->srv) {
+        void* p = nullptr;
+        HIPCHK(hipHostMalloc(&p, sizeof(ServerCtl), hipHostMallocCoherent | hipHostMallocMapped));
+        memset(p, 0, sizeof(ServerCtl));
+        h->srv = (ServerCtl*)p;
+        HIPCHK(hipMalloc(&h->srv_relay, 64));
+        HIPCHK(hipStreamCreateWithFlags(&h->srv_stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&h->srv_ev, hipEventDisableTiming));
+    }
+    h->srv_actions = actions;
+    h->srv_out = out ? *out : kNoOut;
+    h->srv_autoreset = autoreset != 0;
+    h->srv_nwg = (h->n + BLOCK - 1) / BLOCK;
+    h->srv_configured = 1;
+    return server_launch(h);
+}
+
+int fjsp_server_step(fjsp_handle* h) {
+    if (!h) return fail("null handle");
+    if (!h->srv_configured) return fail("fjsp_server_step before fjsp_server_start");
+    const auto now = std::chrono::steady_clock::now();
+    if (h->srv_running &&
+        std::chrono::duration_cast<std::chrono::microseconds>(now - h->srv_last).count() > SRV_RESTART_US) {
+        if (int rc = server_stop(h)) return rc;   // idle: relaunch before the kernel's own timeout
+    }
+    if (!h->srv_running) {
+        if (int rc = server_launch(h)) return rc;
+    }
+    const uint32_t seq = __atomic_load_n(&h->srv->seq, __ATOMIC_RELAXED) + 1u;
+    __atomic_store_n(&h->srv->seq, seq, __ATOMIC_RELEASE);   // after the caller's action bytes
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int w = 0; w < h->srv_nwg; w++) {
+        for (uint32_t it = 0; __atomic_load_n(&h->srv->done[w], __ATOMIC_ACQUIRE) != seq; it++) {
+            if ((it & 1023u) == 1023u) {
+                const bool left = __atomic_load_n(&h->srv->exited[w], __ATOMIC_ACQUIRE) == h->srv_epoch;
+                const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                                    std::chrono::steady_clock::now() - t0).count();
+                if (left || ms > SRV_WAIT_MS) {
+                    (void)server_stop(h);
+                    return fail(left ? "step server left before the request" : "step server request timed out");
+                }
+            }
+        }
+    }
+    h->srv_last = std::chrono::steady_clock::now();
+    return 0;
+}
+
+int fjsp_server_stop(fjsp_handle* h) {
+    if (!h) return fail("null handle");
+    return server_stop(h);
+}
+
 int fjsp_a2c_policy_step(fjsp_handle* h, const float* feats, const int8_t* masks, const float* actor_w,
                          const float* critic_w, const uint64_t* seed, uint32_t env_gid0, uint32_t step,
                          int32_t deterministic, uint8_t* actions, float* values, int32_t autoreset, const fjsp_out* out,
                          int32_t env_begin, int32_t env_count, void* stream) {
     if (!h) return fail("null handle");
+    SERVER_QUIESCE(h);
     if (!h->has_reset) return fail("fjsp_a2c_policy_step before fjsp_reset");
     if (!feats || !masks || !actor_w || !seed || !actions || (values && !critic_w))
         return fail("fjsp_a2c_policy_step: null buffer");
@@ -2250,6 +2470,7 @@ int fjsp_a2c_policy_step(fjsp_handle* h, const float* feats, const int8_t* masks
 int fjsp_step_many(fjsp_handle* h, int32_t K, uint64_t action_seed, uint32_t env_gid0, uint32_t step0,
                    int32_t action_mode, int32_t autoreset, const fjsp_out* traj) {
     if (!h) return fail("null handle");
+    SERVER_QUIESCE(h);
     if (K < 0) return fail("K must be >= 0");
     if (action_mode != FJSP_ACTIONS_UNMASKED && action_mode != FJSP_ACTIONS_MASKED && action_mode != FJSP_ACTIONS_HEURISTIC)
         return fail("bad action_mode");
@@ -2467,6 +2688,7 @@ extern "C" int fjsp_debug_pgstamps(unsigned long long* out) {   // out[8]: pre-d
 
 int fjsp_pack_a2c(fjsp_handle* h, float* feats, int8_t* masks) {
     if (!h) return fail("null handle");
+    SERVER_QUIESCE(h);
     if (!h->has_reset) return fail("fjsp_pack_a2c before fjsp_reset");
     if (!feats && !masks) return 0;
     DeviceGuard g(h->device);
@@ -2489,6 +2711,7 @@ int64_t fjsp_snapshot_bytes(const fjsp_handle* h) { return h ? (int64_t)h->bytes
 
 int fjsp_snapshot(fjsp_handle* h, void* dst) {
     if (!h || !dst) return fail("null argument");
+    SERVER_QUIESCE(h);
     if (!h->has_reset) return fail("fjsp_snapshot before fjsp_reset");
     DeviceGuard g(h->device);
     HIPCHK(hipMemcpyAsync(dst, h->base, h->bytes, hipMemcpyDefault, h->stream));
@@ -2497,6 +2720,7 @@ int fjsp_snapshot(fjsp_handle* h, void* dst) {
 
 int fjsp_restore(fjsp_handle* h, const void* src) {
     if (!h || !src) return fail("null argument");
+    SERVER_QUIESCE(h);
     DeviceGuard g(h->device);
     // everything but the aux words (fault word, spin_cap, test options): those stay the handle's
     const size_t state = (size_t)NWORDS * h->n * 4, rest = (size_t)((char*)h->S.orders - (char*)h->base);
@@ -2512,6 +2736,7 @@ const char* fjsp_last_kernel(const fjsp_handle* h) {
 
 int fjsp_faults(fjsp_handle* h, uint32_t* out, int32_t clear) {
     if (!h || !out) return fail("null argument");
+    SERVER_QUIESCE(h);
     DeviceGuard g(h->device);
     HIPCHK(hipStreamSynchronize(h->stream));
     uint32_t* w = h->S.words + (size_t)NWORDS * h->n + AUX_FAULT;
@@ -2522,6 +2747,7 @@ int fjsp_faults(fjsp_handle* h, uint32_t* out, int32_t clear) {
 
 int fjsp_sync(fjsp_handle* h) {
     if (!h) return fail("null handle");
+    SERVER_QUIESCE(h);
     DeviceGuard g(h->device);
     HIPCHK(hipStreamSynchronize(h->stream));
     return 0;
@@ -2539,6 +2765,7 @@ int fjsp_last_kernel_ms(fjsp_handle* h, float* ms) {
 // MT19937 state exchange in numpy's (key[624], pos) convention (np.random.get_state()[1:3]).
 int fjsp_mt_get(fjsp_handle* h, int32_t env, uint32_t* key, int32_t* pos) {
     if (!h || !key || !pos) return fail("null argument");
+    SERVER_QUIESCE(h);
     if (env < 0 || env >= h->n) return fail("env index out of range");
     DeviceGuard g(h->device);
     HIPCHK(hipStreamSynchronize(h->stream));
@@ -2559,6 +2786,7 @@ int fjsp_mt_get(fjsp_handle* h, int32_t env, uint32_t* key, int32_t* pos) {
 
 int fjsp_mt_set(fjsp_handle* h, int32_t env, const uint32_t* key, int32_t pos) {
     if (!h || !key) return fail("null argument");
+    SERVER_QUIESCE(h);
     if (env < 0 || env >= h->n) return fail("env index out of range");
     if (pos < 0 || pos > MT_N) return fail("pos must be in 0..624");
     DeviceGuard g(h->device);
@@ -2573,6 +2801,7 @@ int fjsp_mt_set(fjsp_handle* h, int32_t env, const uint32_t* key, int32_t pos) {
 
 int fjsp_read_env(fjsp_handle* h, int32_t env, fjsp_env_view* v) {
     if (!h || !v) return fail("null argument");
+    SERVER_QUIESCE(h);
     if (env < 0 || env >= h->n) return fail("env index out of range");
     DeviceGuard g(h->device);
     HIPCHK(hipStreamSynchronize(h->stream));

@@ -163,6 +163,30 @@ class FJSPVecEnv:
         nat.check(nat.lib().fjsp_step(self._h, _ptr(a), order, int(bool(autoreset)), ctypes.byref(out)))
         return buffers
 
+    def server_start(self, actions, autoreset=True, buffers=None):
+        """Start the step server (fjsp_server_start): a resident kernel that steps every env once
+        per server_step() on a host doorbell, no launch or stream synchronisation per step.
+        actions: u8 [8, N] the caller rewrites before every server_step (pinned host memory, or a
+        device tensor whose writes are complete); outputs go to `buffers` (T = 1)."""
+        if actions.dtype != torch.uint8 or not actions.is_contiguous() or tuple(actions.shape) != (NA, self.num_envs):
+            raise ValueError(f"actions must be a contiguous uint8 [8, {self.num_envs}] tensor")
+        if actions.device.type == "cpu" and not actions.is_pinned():
+            raise ValueError("host actions must be in pinned memory (the kernel reads them in place)")
+        self._sync_stream()
+        b = buffers or Buffers(1, self.num_envs, self.device, infos=False)
+        self._srv_keep = (actions, b, b.struct())          # the kernel reads / writes these every step
+        nat.check(nat.lib().fjsp_server_start(self._h, _ptr(actions), int(bool(autoreset)),
+                                              ctypes.byref(self._srv_keep[2])))
+        return b
+
+    def server_step(self):
+        """One step of every env on the running (or relaunched) step server; returns when the
+        step's outputs are written."""
+        nat.check(nat.lib().fjsp_server_step(self._h))
+
+    def server_stop(self):
+        nat.check(nat.lib().fjsp_server_stop(self._h))
+
     def rollout(self, K, action_seed=0, step0=0, masked=False, autoreset=True, buffers=None, infos=False,
                 policy=None):
         """K fused steps with on-device actions; returns [K, F, N] trajectories.

@@ -115,6 +115,47 @@ def test_step_vs_fused(G):
         masks = r["next_masks"][0]
 
 
+@pytest.mark.parametrize("n", [1, 100, 4096])
+def test_step_server_equals_step(G, n):
+    """The step server (fjsp_server_*: a resident kernel stepped through a host doorbell) ==
+    fjsp_step launch by launch: random, absent and out-of-range actions from pinned host memory,
+    auto-resets, every output of every step; other calls on the handle in between (read_env,
+    snapshot: the server leaves and is relaunched), a pause past the idle relaunch, the final state."""
+    import time
+    rng = np.random.default_rng(n)
+    envs = [G.make_env(n), G.make_env(n)]
+    for env in envs:
+        env.reset(seeds=torch.arange(n) + 3, num_orders=30)
+    hb = torch.zeros(8, n, dtype=torch.uint8).pin_memory()
+    bs = envs[1].server_start(hb, autoreset=True,
+                              buffers=G.vec_env.Buffers(1, n, envs[1].device, infos=True, next_obs=True))
+    assert envs[1].last_kernel() == "k_step_server"
+    bl = G.vec_env.Buffers(1, n, envs[0].device, infos=True, next_obs=True)
+    nact = np.array([3, 8, 3, 3, 3, 3, 3, 3]).reshape(8, 1)
+    for t in range(420):
+        acts = (rng.integers(0, 256, (8, n)) * nact >> 8).astype(np.uint8)
+        acts[rng.random((8, n)) < 0.05] = 255
+        weird = rng.random((8, n)) < 0.02
+        acts[weird] = rng.integers(3, 255, size=weird.sum())
+        hb.numpy()[:] = acts
+        envs[0].step(torch.from_numpy(acts).cuda(), buffers=bl)
+        envs[1].server_step()                       # returns with its outputs written
+        torch.cuda.current_stream().synchronize()   # (a device-wide sync would wait for the resident kernel)
+        for k in G.native.OUT_FIELDS:
+            x, y = getattr(bl, k, None), getattr(bs, k, None)
+            if x is not None:
+                assert x.cpu().numpy().tobytes() == y.cpu().numpy().tobytes(), (t, k)
+        if t == 150:
+            v0, v1 = envs[0].read_env(n - 1), envs[1].read_env(n - 1)   # stops the server
+            assert bytes(v0) == bytes(v1)
+        if t == 300:
+            assert torch.equal(envs[0].snapshot(), envs[1].snapshot())
+        if t == 350:
+            time.sleep(0.02)                                             # past the idle relaunch and exit
+    envs[1].server_stop()
+    assert torch.equal(envs[0].snapshot(), envs[1].snapshot())
+
+
 def test_agent_order_and_absent_agents(G):
     """Non-canonical dict order and missing agents against the oracle (FJSPSimulation.py:172-205)."""
     n, steps = 64, 200
