@@ -58,7 +58,8 @@ def parse():
                     help="wall budget of each CPU baseline leg (single thread, all cores)")
     ap.add_argument("--no-step-mode", action="store_true", help="skip the one-launch-per-step measurement")
     ap.add_argument("--no-dropin", action="store_true",
-                    help="skip the reference-API (FJSPParallelEnv.step, one env) latency measurement")
+                    help="skip the host-driven legs: the reference-API (FJSPParallelEnv.step, one env) latency and "
+                         "the host-action vector step (launch path and step server)")
     ap.add_argument("--workload", choices=["step", "a2c"], default="step",
                     help="step: env-step throughput (the headline metric); a2c: the batched A2C "
                          "training loop (BASELINE configs 4/5; one bench step = one A2C batch)")
@@ -553,7 +554,7 @@ def main():
                     "kernel": env.last_kernel(), "algo_bytes_per_env_step": ALGO_BYTES_STEP,
                     "achieved_GBs": ALGO_BYTES_STEP * N / (kms * 1e-3) / 1e9,
                     "note": "one launch per step, actions u8[8][N] resident in HBM (rank 0)"}
-        if rank == 0:
+        if rank == 0 and not args.no_dropin:
             per_step["host_actions"] = host_action_step(env, dev, N)
 
     # the reference-API path itself (FJSPParallelEnv.step with dict actions, one env)

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT="$PWD/gpurun_out/prof"
 mkdir -p "$OUT"
-ARGS="${BENCH_ARGS:---no-cpu-baseline --no-a2c --no-scale --no-chunk-compare}"
+ARGS="${BENCH_ARGS:---no-cpu-baseline --no-a2c --no-scale --no-chunk-compare --no-dropin}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py $ARGS > "$OUT/kt.log" 2>&1
 rc=$?; echo "kt rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d "$OUT/fetch" -o fetch --output-format csv -- python3 bench.py $ARGS > "$OUT/fetch.log" 2>&1
