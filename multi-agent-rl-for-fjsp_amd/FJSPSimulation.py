@@ -77,11 +77,6 @@ class _Packed:
                 setattr(self.out_obs, name, base + off)
         self.ref_full, self.ref_obs = ctypes.byref(self.out_full), ctypes.byref(self.out_obs)
 
-    def snapshot(self):
-        """This step's record as fresh arrays (the next launch overwrites the pinned one)."""
-        c = self.np.copy()
-        return {name: c[off: off + dt.itemsize * n].view(dt) for name, (off, dt, n) in self.layout.items()}
-
 
 class _AGVView:
     """simulation.agv as a2c.py:298-305 reads it: position and carrying_tray come from the last
@@ -191,7 +186,7 @@ class FJSPSimulation:
         self._bind_stream()
         nat.check(self._L.fjsp_reset(self._h, None, None, 0, self._packed.ref_obs))
         self._wait()
-        self._take_obs(self._packed.snapshot())
+        self._take_obs(self._packed.view)
 
     # ------------------------------------------------------------------ internals
     def _bind_stream(self):
@@ -223,7 +218,7 @@ class FJSPSimulation:
         self._pushed_rc, self._pushed_weights = rc, dict(d)
 
     def _take_obs(self, p):
-        self._last_i32 = p["obs_i32"]
+        self._last_i32 = p["obs_i32"]   # the record's view: the AGV reads see the latest observation
         self._last_obs = obs_dicts(p["obs_i32"], p["obs_i8"], p["obs_f32"], p["masks"])
         return self._last_obs
 
@@ -251,7 +246,7 @@ class FJSPSimulation:
         self.sim_time = 0
         self._orders_total = int(n)
         self._viewcache = None
-        obs = self._take_obs(self._packed.snapshot())
+        obs = self._take_obs(self._packed.view)
         return obs, {a: {} for a in AGENTS}
 
     def step(self, actions):
@@ -281,7 +276,7 @@ class FJSPSimulation:
         else:
             nat.check(self._L.fjsp_step(self._h, self._act_ptr, ord_arr, 0, self._packed.ref_full))
             self._wait()
-        p = self._packed.snapshot()
+        p = self._packed.view   # every value leaves the pinned record as Python numbers or fresh arrays
         self._viewcache = None
         obs = self._take_obs(p)
         rw = p["rewards"].tolist()

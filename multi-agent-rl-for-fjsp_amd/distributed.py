@@ -130,10 +130,13 @@ def adv_stats_slab(adv, group=None):
                          torch.full((A,), float(T * N), dtype=torch.float64, device=adv.device)], dim=1)
     if active(group):
         dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
+        count = int(s[0, 2].item())                      # every rank's samples (one host sync)
+    else:
+        count = T * N                                    # known here: no host sync
     n = s[0, 2]
     mean = s[:, 0] / n
     var = (s[:, 1] - n * mean * mean) / (n - 1)
-    return int(n.item()), mean.float(), var.clamp_min(0).sqrt().float()
+    return count, mean.float(), var.clamp_min(0).sqrt().float()
 
 
 def allreduce_grads(params, group=None):
