@@ -556,6 +556,10 @@ def main():
                     "note": "one launch per step, actions u8[8][N] resident in HBM (rank 0)"}
         if rank == 0 and not args.no_dropin:
             per_step["host_actions"] = host_action_step(env, dev, N)
+            ps = load_pmc(f"server_{N}envs")   # the resident server's HBM bytes (scripts/diag_server_pmc.py)
+            if ps and ps.get("hbm_bytes_per_env_step"):
+                per_step["host_actions"]["server_traffic_bytes_per_env_step"] = ps["hbm_bytes_per_env_step"]
+                per_step["host_actions"]["server_traffic_source"] = f"profiles/pmc_server_{N}envs.json"
 
     # the reference-API path itself (FJSPParallelEnv.step with dict actions, one env)
     dropin = None
