@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
-"""A/B of the collect's actor-workgroup order (option policy_xmap, csrc/fjsp_policy.hip actor_block):
-one learner per order, each captured with its order, replayed in alternation (256 x N per batch,
-ms per batch), and the rollout slabs compared byte for byte across orders after every batch (the
-order changes which workgroup computes what, never a value).
+"""A/B of a library-wide policy-launch option (fjsp_set_option(NULL, name, v), csrc/fjsp_policy.hip:
+policy_xmap, policy_split, policy_dedup, policy_touch): one learner per value, each captured with
+its value, replayed in alternation (256 x N per batch, ms per batch), and the rollout slabs
+compared byte for byte across values after every batch (the options change which workgroup
+computes what, never a value).
 
-usage: python scripts/ab_collect_xmap.py [N] [reps] [orders, e.g. 0+1+2]"""
+usage: python scripts/ab_collect_xmap.py [N] [reps] [values, e.g. 0+1+2] [option, default policy_xmap]"""
 import importlib
 import json
 import os
@@ -19,10 +20,10 @@ A = importlib.import_module("multi-agent-rl-for-fjsp_amd.a2c_vec")
 V = importlib.import_module("multi-agent-rl-for-fjsp_amd.vec_env")
 
 
-def main(n=4096, reps=10, orders=(0, 1, 2), init="random", T=256):
+def main(n=4096, reps=10, orders=(0, 1, 2), init="random", T=256, option="policy_xmap"):
     learners = {}
     for x in orders:
-        A.nat.check(A.nat.lib().fjsp_set_option(None, b"policy_xmap", x))   # library-wide, read per launch
+        A.nat.check(A.nat.lib().fjsp_set_option(None, option.encode(), x))   # library-wide, read per launch
         L = A.VecMultiAgentA2C(V.FJSPVecEnv(n), batch_size=T, seed=3)
         if init == "trained":
             L.load_state_dicts(A.load_npz_weights(os.path.join(REPO, "tests", "golden", "trained_policy.npz")))
@@ -49,7 +50,7 @@ def main(n=4096, reps=10, orders=(0, 1, 2), init="random", T=256):
         for x in orders:
             learners[x].roll_over()
     med = {x: sorted(v)[len(v) // 2] for x, v in ms.items()}
-    return {"envs": n, "batch": T, "init": init, "collect_ms_median": med, "collect_ms": ms,
+    return {"option": option, "envs": n, "batch": T, "init": init, "collect_ms_median": med, "collect_ms": ms,
             "slabs_equal_across_orders": bool(equal)}
 
 
@@ -57,5 +58,6 @@ if __name__ == "__main__":
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     orders = tuple(int(x) for x in sys.argv[3].replace(",", "+").split("+")) if len(sys.argv) > 3 else (0, 1, 2)
+    option = sys.argv[4] if len(sys.argv) > 4 else "policy_xmap"
     for init in ("random", "trained"):
-        print(json.dumps(main(n, reps, orders, init)), flush=True)
+        print(json.dumps(main(n, reps, orders, init, option=option)), flush=True)
