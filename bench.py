@@ -182,27 +182,36 @@ def dropin_latency(dev, steps=2000, warm=200):
     loop(True, warm)
     launch_path, _ = loop(True, steps)
     sim.use_server = True
-    # the device part alone: one server request (doorbell + wait) on the facade's record
+    # the device part alone: one server request (doorbell + wait) on the facade's record, in the
+    # facade's inline mode (the action bytes in the doorbell's line) and with an actions buffer
     L, h = sim._L, sim._h
     nat = importlib.import_module("multi-agent-rl-for-fjsp_amd._native")
     env.reset(seed=1, options={"num_orders": 30})
-    nat.check(L.fjsp_server_start(h, sim._act_ptr, 0, sim._packed.ref_full))
-    for _ in range(100):
-        nat.check(L.fjsp_server_step(h))
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        nat.check(L.fjsp_server_step(h))
-    server_us = (time.perf_counter() - t0) / steps * 1e6
-    nat.check(L.fjsp_server_stop(h))
+
+    def requests(inline):
+        nat.check(L.fjsp_server_start(h, None if inline else sim._act_ptr, 0, sim._packed.ref_full))
+        req = (lambda: L.fjsp_server_step_actions(h, sim._act_ptr)) if inline else (lambda: L.fjsp_server_step(h))
+        for _ in range(100):
+            nat.check(req())
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            nat.check(req())
+        us = (time.perf_counter() - t0) / steps * 1e6
+        nat.check(L.fjsp_server_stop(h))
+        return us
+    server_buf_us = requests(False)
+    server_us = requests(True)   # leaves the facade's own configuration behind
     return {"dropin_n1_us_per_step": with_agv, "dropin_n1_no_agv_reads_us_per_step": no_agv,
             "dropin_n1_launch_path_us_per_step": launch_path, "server_request_us": server_us,
+            "server_request_actions_buffer_us": server_buf_us,
             "resets": resets, "steps": steps,
             "reference_us_per_step": REF_PY_STEP_US,
             "speedup_vs_reference": REF_PY_STEP_US / with_agv,
             "note": "FJSPParallelEnv.step(dict) + a2c.py:298-305's agv.position / carrying_tray reads, one env, "
                     "random actions, reset when env.agents empties; the step server carries the canonical-order "
                     "steps (launch_path: one fjsp_step launch + one synchronisation per step instead); "
-                    "server_request_us: one fjsp_server_step alone; reference: SURVEY.md App. E (1 core, same "
+                    "server_request_us: one fjsp_server_step_actions alone (inline mode, the facade's), "
+                    "server_request_actions_buffer_us: one fjsp_server_step reading an actions buffer; reference: SURVEY.md App. E (1 core, same "
                     "container class), not re-timed on this box (the reference never travels)"}
 
 

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define FJSP_ABI_VERSION 10
+#define FJSP_ABI_VERSION 11
 
 #define FJSP_NUM_AGENTS 8      /* pickup, agv, small, big, pkg_blue_1, pkg_blue_2, pkg_red, pkg_green */
 #define FJSP_OBS_I32 20        /* pickup 7 + agv 13 (position = 2) int32 observation fields */
@@ -213,9 +213,15 @@ int fjsp_step(fjsp_handle* h, const uint8_t* actions, const uint8_t* agent_order
  * snapshot, set_reward_weights, ...) first stops the server (its state is written back); the next
  * fjsp_server_step relaunches it with the same actions / outputs, as it does after 2 ms without a
  * request (the kernel itself leaves after 5 ms idle, so a device-wide synchronisation issued
- * between steps waits at most that long).  fjsp_server_stop: leave now. */
+ * between steps waits at most that long).  fjsp_server_stop: leave now.
+ * Inline mode (ABI 11; one-env handles, the N = 1 drop-in): fjsp_server_start(h, NULL, ...), then
+ * fjsp_server_step_actions(h, actions) with the step's 8 action bytes (any host memory): they ride
+ * in the doorbell's cache line, so the kernel's poll that sees the request already holds them (one
+ * bus round trip per step fewer).  fjsp_server_step on an inline server, or step_actions on one
+ * started with an actions buffer, is an error. */
 int fjsp_server_start(fjsp_handle* h, const uint8_t* actions, int32_t autoreset, const fjsp_out* out);
 int fjsp_server_step(fjsp_handle* h);
+int fjsp_server_step_actions(fjsp_handle* h, const uint8_t* actions);
 int fjsp_server_stop(fjsp_handle* h);
 
 /* K fused steps with on-device synthetic actions from the counter RNG

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
-from .spec import ACTION_NAMES, AGENTS, decode_result, obs_dicts
+from .spec import ACTION_NAMES, AGENTS, decode_result
 from .utils.ActionSpaces import ActionSpaces
 from .utils.ObservationSpaces import ObservationSpaces
 from .utils.RewardModel import RewardModel
@@ -157,6 +157,8 @@ class FJSPSimulation:
         self._venv = FJSPVecEnv(1, device=self.device, config=native_config(self.config))
         self._h = self._venv.handle
         self._L = nat.lib()
+        # the observation dicts built in C (csrc/fjsp_facade.c; spec.obs_dicts is its definition)
+        self._obs_dicts = nat.facade().obs_dicts
         # one launch per step: no per-launch event pair (fjsp_last_kernel_ms), the facade never reads it
         nat.check(self._L.fjsp_set_option(self._h, b"timing", 0))
         self._packed = _Packed()
@@ -219,7 +221,7 @@ class FJSPSimulation:
 
     def _take_obs(self, p):
         self._last_i32 = p["obs_i32"]   # the record's view: the AGV reads see the latest observation
-        self._last_obs = obs_dicts(p["obs_i32"], p["obs_i8"], p["obs_f32"], p["masks"])
+        self._last_obs = self._obs_dicts(p["obs_i32"], p["obs_i8"], p["obs_f32"], p["masks"])
         return self._last_obs
 
     def _info(self, i, a, act, word):
@@ -269,10 +271,10 @@ class FJSPSimulation:
         self._push_weights()
         self._bind_stream()
         if canon and self.use_server:
-            if not self._srv_on:
-                nat.check(self._L.fjsp_server_start(self._h, self._act_ptr, 0, self._packed.ref_full))
+            if not self._srv_on:   # inline mode: the 8 action bytes ride in the doorbell's cache line
+                nat.check(self._L.fjsp_server_start(self._h, None, 0, self._packed.ref_full))
                 self._srv_on = True
-            nat.check(self._L.fjsp_server_step(self._h))   # returns with the record written
+            nat.check(self._L.fjsp_server_step_actions(self._h, self._act_ptr))   # returns with the record written
         else:
             nat.check(self._L.fjsp_step(self._h, self._act_ptr, ord_arr, 0, self._packed.ref_full))
             self._wait()

@@ -5,8 +5,10 @@ the HIP kernels for gfx950.  If the library is missing or no GPU is visible, the
 loudly (FjspNativeError) — there is no CPU fallback.
 """
 import ctypes
+import importlib
 import os
 import subprocess
+import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
@@ -16,6 +18,10 @@ SRC = os.path.join(HERE, "csrc", "fjsp_hip.hip")
 SRCS = [SRC, os.path.join(HERE, "csrc", "fjsp_policy.hip"), os.path.join(HERE, "csrc", "fjsp_group.hip")]
 HEADERS = [os.path.join(HERE, "csrc", h) for h in ("fjsp_env.h", "fjsp_stepdev.h", "fjsp_stamps.h")] + [
     os.path.join(REPO, "include", "fjsp.h")]
+
+# the drop-in facade's host helper (CPython extension, no GPU code): csrc/fjsp_facade.c
+FACADE_SRC = os.path.join(HERE, "csrc", "fjsp_facade.c")
+FACADE_PATH = os.path.join(HERE, "_facade" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
@@ -70,12 +76,12 @@ EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_c
            "fjsp_a2c_critic_backward", "fjsp_gae_shared",
            "fjsp_a2c_policy_step", "fjsp_a2c_group_temp_bytes", "fjsp_a2c_group_sort", "fjsp_a2c_group_runs",
            "fjsp_a2c_run_sums_bytes", "fjsp_a2c_run_sums", "fjsp_a2c_critic_fused", "fjsp_a2c_shard_keys", "fjsp_a2c_record_head", "fjsp_a2c_pack_mfma", "fjsp_a2c_slab_stats",
-           "fjsp_server_start", "fjsp_server_step", "fjsp_server_stop"]
+           "fjsp_server_start", "fjsp_server_step", "fjsp_server_step_actions", "fjsp_server_stop"]
 POLICY_ACTOR_DPAD, POLICY_CRITIC_DPAD = 16, 48
 POLICY_ACTOR_FLOATS = 3 * 256 * 16 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 8 * 256 + 16
 POLICY_CRITIC_FLOATS = 3 * 256 * 48 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 3 * 128 * 256 // 2 + 128 + 128 + 16
 CRITIC_FUSED_PW = 2 * 256 + 2 * 128 + 4   # floats per tile of fjsp_a2c_critic_fused's partial sums
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _lib = None
 
@@ -87,9 +93,32 @@ def _stale():
     return any(os.path.getmtime(p) > t for p in SRCS + HEADERS)
 
 
+def build_facade(force=False):
+    """Compile the facade's CPython helper (_facade*.so) in-tree with gcc."""
+    if not force and os.path.exists(FACADE_PATH) and os.path.getmtime(FACADE_PATH) >= os.path.getmtime(FACADE_SRC):
+        return FACADE_PATH
+    import numpy
+    r = subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
+                        "-I" + sysconfig.get_paths()["include"], "-I" + numpy.get_include(), "-o", FACADE_PATH,
+                        FACADE_SRC], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise FjspNativeError("gcc failed on fjsp_facade.c:\n" + r.stderr[-4000:])
+    return FACADE_PATH
+
+
+def facade():
+    """The facade's host helper module (obs_dicts in C); fails loudly when it was not built."""
+    if not os.path.exists(FACADE_PATH):
+        raise FjspNativeError(
+            f"{FACADE_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    return importlib.import_module(__package__ + "._facade")
+
+
 def build(force=False, verbose=False):
     """Compile libfjsp.so for gfx950 in-tree (hipcc cross-compiles without a GPU): one hipcc
-    process per source file in parallel (no cross-file device calls), then one link."""
+    process per source file in parallel (no cross-file device calls), then one link; and the
+    facade's host helper."""
+    build_facade(force)
     if not force and not _stale():
         return LIB_PATH
     import tempfile
@@ -167,6 +196,7 @@ def lib():
         "fjsp_a2c_policy_step": (I, [P, P, P, P, P, P, U32, U32, I, P, P, I, ctypes.POINTER(fjsp_out), I, I, P]),
         "fjsp_server_start": (I, [P, P, I, ctypes.POINTER(fjsp_out)]),
         "fjsp_server_step": (I, [P]),
+        "fjsp_server_step_actions": (I, [P, P]),
         "fjsp_server_stop": (I, [P]),
         "fjsp_a2c_group_temp_bytes": (I, [ctypes.c_int64, ctypes.POINTER(U64)]),
         "fjsp_a2c_group_sort": (I, [P, I, ctypes.c_int64, ctypes.c_uint32, P, U64, P, P, P, P, P, P, P, P]),

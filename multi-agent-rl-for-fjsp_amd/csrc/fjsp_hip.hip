@@ -279,7 +279,8 @@ constexpr int SRV_MAX_WG = 256;   // 16 384 envs
 struct alignas(64) ServerCtl {
     uint32_t seq;                  // host: the step requested (monotonic)
     uint32_t stop;                 // host: leave now (the state words are written back)
-    uint32_t pad[14];
+    uint32_t inbox[4];             // host, one-env inline mode: (seq & 0xFFFF) << 16 | two action bytes each
+    uint32_t pad[10];
     uint32_t done[SRV_MAX_WG];     // kernel: the last seq each workgroup completed
     uint32_t exited[SRV_MAX_WG];   // kernel: the epoch of the launch that left
 };
@@ -287,9 +288,13 @@ struct alignas(64) ServerCtl {
 // Exit conditions every wave reaches: the stop word, or idle_ticks of the 100 MHz clock without a
 // new request (the host relaunches well before that: fjsp_server_step's restart_ms); a step itself
 // is bounded straight-line code.  Only lane 0 of workgroup 0 polls the host's words (system-scope
-// loads over the bus); it relays each request (and a stop) through two device words, relay[0] =
-// the request, relay[1] = stop, which the other workgroups' lane 0 poll in L2 (both set by the host
-// before the launch: relay[0] = start_seq, relay[1] = 0).
+// loads over the bus, all of one poll issued together: one bus round trip per poll); it relays
+// each request (and a stop) through two device words, relay[0] = the request, relay[1] = stop,
+// which the other workgroups' lane 0 poll in L2 (both set by the host before the launch:
+// relay[0] = start_seq, relay[1] = 0).  Inline mode (actions == nullptr, one env): the request's
+// eight action bytes ride in the doorbell's cache line (ctl->inbox, each word tagged with the
+// request's low 16 bits), so the poll that sees the request also has its actions — no second
+// round trip to read them.
 __global__ void __launch_bounds__(BLOCK) k_step_server(DevState S, Cfg C, ServerCtl* ctl, uint32_t* relay,
                                                        const uint8_t* actions, int autoreset, fjsp_out out,
                                                        uint32_t start_seq, uint32_t epoch, uint64_t idle_ticks) {
@@ -305,17 +310,31 @@ __global__ void __launch_bounds__(BLOCK) k_step_server(DevState S, Cfg C, Server
     const Tables T = tables_of(S, valid ? e : 0);
     uint32_t last = start_seq;
     uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const bool inline_act = actions == nullptr;
+    uint32_t ib[4] = {0u, 0u, 0u, 0u};
     for (;;) {
         uint32_t sq = last, quit = 0;
         if (lane == 0 && blockIdx.x == 0) {
             for (;;) {
-                sq = __hip_atomic_load(&ctl->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (sq != last) {
+                // relaxed loads issued together (the acquire fence below orders what follows)
+                sq = __hip_atomic_load(&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const uint32_t stop = __hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                bool got = sq != last;
+                if (inline_act) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        ib[k] = __hip_atomic_load(&ctl->inbox[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    // the host writes the inbox before seq: every tag = the next request's means
+                    // its actions are complete (a poll that saw seq but not yet the inbox polls again)
+                    const uint32_t tag = (last + 1u) & 0xFFFFu;
+                    got = (ib[0] >> 16) == tag && (ib[1] >> 16) == tag && (ib[2] >> 16) == tag && (ib[3] >> 16) == tag;
+                    sq = last + 1u;
+                }
+                if (got) {
                     __hip_atomic_store(&relay[0], sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
-                if (__hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                    __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+                if (stop || __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
                     __hip_atomic_store(&relay[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                     quit = 1;
                     break;
@@ -343,8 +362,13 @@ __global__ void __launch_bounds__(BLOCK) k_step_server(DevState S, Cfg C, Server
         last = sq;
         if (valid) {
             int act[NA];
+            if (inline_act) {   // one env: lane 0 of workgroup 0, which polled the inbox
 #pragma unroll
-            for (int a = 0; a < NA; a++) act[a] = actions[a * S.n + e];
+                for (int a = 0; a < NA; a++) act[a] = (int)((ib[a >> 1] >> (8 * (a & 1))) & 0xFFu);
+            } else {
+#pragma unroll
+                for (int a = 0; a < NA; a++) act[a] = actions[a * S.n + e];
+            }
             step_and_emit<true>(E, T, C, S, e, act, nullptr, autoreset, out, 0);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this lane's outputs reach host / device memory
@@ -2378,7 +2402,7 @@ static int server_launch(fjsp_handle* h) {
 
 int fjsp_server_start(fjsp_handle* h, const uint8_t* actions, int32_t autoreset, const fjsp_out* out) {
     if (!h) return fail("null handle");
-    if (!actions) return fail("null actions");
+    if (!actions && h->n != 1) return fail("fjsp_server_start: null actions (inline mode) needs a one-env handle");
     if (!h->has_reset) return fail("fjsp_server_start before fjsp_reset");
     if (h->n > SRV_MAX_WG * BLOCK) return fail("fjsp_server_start: at most 16384 envs per handle");
     SERVER_QUIESCE(h);
@@ -2400,9 +2424,24 @@ int fjsp_server_start(fjsp_handle* h, const uint8_t* actions, int32_t autoreset,
     return server_launch(h);
 }
 
+static int server_request(fjsp_handle* h, const uint8_t* inline_actions);
+
 int fjsp_server_step(fjsp_handle* h) {
     if (!h) return fail("null handle");
     if (!h->srv_configured) return fail("fjsp_server_step before fjsp_server_start");
+    if (!h->srv_actions) return fail("fjsp_server_step: the server runs in inline mode (fjsp_server_step_actions)");
+    return server_request(h, nullptr);
+}
+
+int fjsp_server_step_actions(fjsp_handle* h, const uint8_t* actions) {
+    if (!h) return fail("null handle");
+    if (!actions) return fail("null actions");
+    if (!h->srv_configured) return fail("fjsp_server_step_actions before fjsp_server_start");
+    if (h->srv_actions) return fail("fjsp_server_step_actions: the server was started with an actions buffer");
+    return server_request(h, actions);
+}
+
+static int server_request(fjsp_handle* h, const uint8_t* inline_actions) {
     const auto now = std::chrono::steady_clock::now();
     if (h->srv_running &&
         std::chrono::duration_cast<std::chrono::microseconds>(now - h->srv_last).count() > SRV_RESTART_US) {
@@ -2412,6 +2451,12 @@ int fjsp_server_step(fjsp_handle* h) {
         if (int rc = server_launch(h)) return rc;
     }
     const uint32_t seq = __atomic_load_n(&h->srv->seq, __ATOMIC_RELAXED) + 1u;
+    if (inline_actions) {   // the inbox before seq (the kernel accepts a request by the inbox tags)
+        const uint32_t tag = (seq & 0xFFFFu) << 16;
+        for (int k = 0; k < 4; k++)
+            __atomic_store_n(&h->srv->inbox[k], tag | inline_actions[2 * k] | ((uint32_t)inline_actions[2 * k + 1] << 8),
+                             __ATOMIC_RELEASE);
+    }
     __atomic_store_n(&h->srv->seq, seq, __ATOMIC_RELEASE);   // after the caller's action bytes
     const auto t0 = std::chrono::steady_clock::now();
     for (int w = 0; w < h->srv_nwg; w++) {

@@ -6,6 +6,7 @@ kernels write coalesced; ``.t()`` gives the [N, F] view a network consumes.
 """
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _native as nat
@@ -167,11 +168,18 @@ class FJSPVecEnv:
         """Start the step server (fjsp_server_start): a resident kernel that steps every env once
         per server_step() on a host doorbell, no launch or stream synchronisation per step.
         actions: u8 [8, N] the caller rewrites before every server_step (pinned host memory, or a
-        device tensor whose writes are complete); outputs go to `buffers` (T = 1)."""
-        if actions.dtype != torch.uint8 or not actions.is_contiguous() or tuple(actions.shape) != (NA, self.num_envs):
-            raise ValueError(f"actions must be a contiguous uint8 [8, {self.num_envs}] tensor")
-        if actions.device.type == "cpu" and not actions.is_pinned():
-            raise ValueError("host actions must be in pinned memory (the kernel reads them in place)")
+        device tensor whose writes are complete); outputs go to `buffers` (T = 1).  actions=None on
+        a one-env handle: inline mode, each server_step(actions) hands its 8 action bytes over in
+        the doorbell's cache line (fjsp_server_step_actions)."""
+        if actions is None:
+            if self.num_envs != 1:
+                raise ValueError("inline actions (actions=None) need a one-env handle")
+        else:
+            if actions.dtype != torch.uint8 or not actions.is_contiguous() or tuple(actions.shape) != (NA, self.num_envs):
+                raise ValueError(f"actions must be a contiguous uint8 [8, {self.num_envs}] tensor")
+            if actions.device.type == "cpu" and not actions.is_pinned():
+                raise ValueError("host actions must be in pinned memory (the kernel reads them in place)")
+        self._srv_inline = actions is None
         self._sync_stream()
         b = buffers or Buffers(1, self.num_envs, self.device, infos=False)
         self._srv_keep = (actions, b, b.struct())          # the kernel reads / writes these every step
@@ -179,10 +187,16 @@ class FJSPVecEnv:
                                               ctypes.byref(self._srv_keep[2])))
         return b
 
-    def server_step(self):
+    def server_step(self, actions=None):
         """One step of every env on the running (or relaunched) step server; returns when the
-        step's outputs are written."""
-        nat.check(nat.lib().fjsp_server_step(self._h))
+        step's outputs are written.  Inline mode: actions = the env's 8 action codes."""
+        if getattr(self, "_srv_inline", False):
+            a = np.ascontiguousarray(actions, dtype=np.uint8).reshape(-1)
+            if a.size != NA:
+                raise ValueError("inline server_step takes the env's 8 action codes")
+            nat.check(nat.lib().fjsp_server_step_actions(self._h, ctypes.c_void_p(a.ctypes.data)))
+        else:
+            nat.check(nat.lib().fjsp_server_step(self._h))
 
     def server_stop(self):
         nat.check(nat.lib().fjsp_server_stop(self._h))

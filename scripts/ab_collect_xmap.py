@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """A/B of a library-wide policy-launch option (fjsp_set_option(NULL, name, v), csrc/fjsp_policy.hip:
-policy_xmap, policy_split, policy_dedup, policy_touch): one learner per value, each captured with
+policy_xmap, policy_split, policy_dedup): one learner per value, each captured with
 its value, replayed in alternation (256 x N per batch, ms per batch), and the rollout slabs
 compared byte for byte across values after every batch (the options change which workgroup
 computes what, never a value).

@@ -44,15 +44,25 @@ for t in range(steps):
     L.fjsp_step(h, sim._act_ptr, None, 0, sim._packed.ref_full)
     L.fjsp_sync(h)
 launch_sync = (time.perf_counter() - t0) / steps * 1e6
-# the step server's request alone (doorbell + wait), the path the facade takes
-L.fjsp_server_start(h, sim._act_ptr, 0, sim._packed.ref_full)
-for t in range(100):
-    L.fjsp_server_step(h)
-t0 = time.perf_counter()
-for t in range(steps):
-    L.fjsp_server_step(h)
-server_step = (time.perf_counter() - t0) / steps * 1e6
-L.fjsp_server_stop(h)
+# the step server's request alone (doorbell + wait): the facade's inline mode (the action bytes
+# in the doorbell's cache line), then with an actions buffer read by the kernel
+
+
+def requests(inline):
+    L.fjsp_server_start(h, None if inline else sim._act_ptr, 0, sim._packed.ref_full)
+    req = (lambda: L.fjsp_server_step_actions(h, sim._act_ptr)) if inline else (lambda: L.fjsp_server_step(h))
+    for t in range(100):
+        assert req() == 0
+    t0 = time.perf_counter()
+    for t in range(steps):
+        assert req() == 0
+    us = (time.perf_counter() - t0) / steps * 1e6
+    L.fjsp_server_stop(h)
+    return us
+
+
+server_buf = requests(False)
+server_step = requests(True)   # the facade's own configuration again
 env.reset(seed=1, options={"num_orders": 30})
 pr = cProfile.Profile()
 pr.enable()
@@ -60,5 +70,6 @@ loop(steps)
 pr.disable()
 s = io.StringIO()
 pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
-print(json.dumps({"us_per_step": plain, "launch_plus_sync_us": launch_sync, "server_step_us": server_step}))
+print(json.dumps({"us_per_step": plain, "launch_plus_sync_us": launch_sync, "server_step_us": server_step,
+                  "server_step_actions_buffer_us": server_buf}))
 print(s.getvalue(), file=sys.stderr)

@@ -20,7 +20,7 @@ def test_library_exports_every_symbol():
     L = G.native.lib()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.fjsp_abi_version() == G.native.ABI_VERSION == 10
+    assert L.fjsp_abi_version() == G.native.ABI_VERSION == 11
 
 
 def test_config_validation_without_gpu():

@@ -115,19 +115,21 @@ def test_step_vs_fused(G):
         masks = r["next_masks"][0]
 
 
-@pytest.mark.parametrize("n", [1, 100, 4096])
-def test_step_server_equals_step(G, n):
+@pytest.mark.parametrize("n,inline", [(1, False), (1, True), (100, False), (4096, False)])
+def test_step_server_equals_step(G, n, inline):
     """The step server (fjsp_server_*: a resident kernel stepped through a host doorbell) ==
-    fjsp_step launch by launch: random, absent and out-of-range actions from pinned host memory,
+    fjsp_step launch by launch: random, absent and out-of-range actions from pinned host memory
+    (inline: the one env's 8 action bytes in the doorbell's cache line, fjsp_server_step_actions),
     auto-resets, every output of every step; other calls on the handle in between (read_env,
-    snapshot: the server leaves and is relaunched), a pause past the idle relaunch, the final state."""
+    snapshot: the server leaves and is relaunched), a pause past the idle relaunch, the final state;
+    inline, also past the 16-bit wrap of the inbox's request tags."""
     import time
-    rng = np.random.default_rng(n)
+    rng = np.random.default_rng(n + inline)
     envs = [G.make_env(n), G.make_env(n)]
     for env in envs:
         env.reset(seeds=torch.arange(n) + 3, num_orders=30)
     hb = torch.zeros(8, n, dtype=torch.uint8).pin_memory()
-    bs = envs[1].server_start(hb, autoreset=True,
+    bs = envs[1].server_start(None if inline else hb, autoreset=True,
                               buffers=G.vec_env.Buffers(1, n, envs[1].device, infos=True, next_obs=True))
     assert envs[1].last_kernel() == "k_step_server"
     bl = G.vec_env.Buffers(1, n, envs[0].device, infos=True, next_obs=True)
@@ -139,7 +141,7 @@ def test_step_server_equals_step(G, n):
         acts[weird] = rng.integers(3, 255, size=weird.sum())
         hb.numpy()[:] = acts
         envs[0].step(torch.from_numpy(acts).cuda(), buffers=bl)
-        envs[1].server_step()                       # returns with its outputs written
+        envs[1].server_step(acts[:, 0] if inline else None)   # returns with its outputs written
         torch.cuda.current_stream().synchronize()   # (a device-wide sync would wait for the resident kernel)
         for k in G.native.OUT_FIELDS:
             x, y = getattr(bl, k, None), getattr(bs, k, None)
@@ -152,6 +154,19 @@ def test_step_server_equals_step(G, n):
             assert torch.equal(envs[0].snapshot(), envs[1].snapshot())
         if t == 350:
             time.sleep(0.02)                                             # past the idle relaunch and exit
+    if inline:   # 66 000 more requests: the tags wrap past 0xFFFF; a fixed action stream on both
+        ad = torch.zeros(8, 1, dtype=torch.uint8, device=envs[0].device)
+        for t in range(66000):
+            a = (t * 2654435761) >> 7 & 0xFF
+            row = np.array([a % 3, a % 8, (a >> 3) % 3, (a >> 4) % 3, (a >> 5) % 2, 1, 0, (a >> 6) % 2], np.uint8)
+            ad.copy_(torch.from_numpy(row).view(8, 1), non_blocking=False)
+            envs[0].step(ad, buffers=bl)
+            envs[1].server_step(row)
+        torch.cuda.current_stream().synchronize()
+        for k in G.native.OUT_FIELDS:
+            x, y = getattr(bl, k, None), getattr(bs, k, None)
+            if x is not None:
+                assert x.cpu().numpy().tobytes() == y.cpu().numpy().tobytes(), ("wrap", k)
     envs[1].server_stop()
     assert torch.equal(envs[0].snapshot(), envs[1].snapshot())
 
