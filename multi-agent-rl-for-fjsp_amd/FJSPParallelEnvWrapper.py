@@ -48,7 +48,8 @@ class FJSPParallelEnv(_Base):
 
     def step(self, actions):
         obs, rewards, terms, truncs, infos = self.simulation.step(actions)
-        self.agents = [a for a in self.agents if not terms.get(a, False) and not truncs.get(a, False)]
+        if True in terms.values() or True in truncs.values():   # (the filter is a no-op otherwise)
+            self.agents = [a for a in self.agents if not terms.get(a, False) and not truncs.get(a, False)]
         return obs, rewards, terms, truncs, infos
 
     def state(self):

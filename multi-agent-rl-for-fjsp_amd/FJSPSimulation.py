@@ -157,8 +157,12 @@ class FJSPSimulation:
         self._venv = FJSPVecEnv(1, device=self.device, config=native_config(self.config))
         self._h = self._venv.handle
         self._L = nat.lib()
-        # the observation dicts built in C (csrc/fjsp_facade.c; spec.obs_dicts is its definition)
-        self._obs_dicts = nat.facade().obs_dicts
+        # the observation dicts built in C (csrc/fjsp_facade.c; spec.obs_dicts is its definition),
+        # and the common step (a canonical dict of plain ints on the step server) in one C call
+        F = nat.facade()
+        self._obs_dicts = F.obs_dicts
+        self._fast_step = F.step
+        self._stepper = None
         # one launch per step: no per-launch event pair (fjsp_last_kernel_ms), the facade never reads it
         nat.check(self._L.fjsp_set_option(self._h, b"timing", 0))
         self._packed = _Packed()
@@ -251,8 +255,30 @@ class FJSPSimulation:
         obs = self._take_obs(self._packed.view)
         return obs, {a: {} for a in AGENTS}
 
+    def _make_stepper(self):
+        P = self._packed
+        fn = ctypes.cast(self._L.fjsp_server_step_actions, ctypes.c_void_p).value
+        offs = [P.layout[k][0] for k in ("obs_i32", "obs_i8", "obs_f32", "masks", "rewards", "term", "trunc",
+                                         "results", "orders_completed", "packaged", "sim_time")]
+        return nat.facade().stepper(self._h.value, fn, self._act_host.data_ptr(), P.host.data_ptr(), offs,
+                                    decode_result)
+
     def step(self, actions):
         """FJSPSimulation.step (FJSPSimulation.py:144-242)."""
+        if self._srv_on and self.use_server:
+            # the common case in C (_facade.step: the eight agents in dict order, plain int actions);
+            # anything else returns None untouched and takes the path below
+            self._push_weights()
+            self._bind_stream()
+            r = self._fast_step(self._stepper, actions)
+            if r is not None:
+                if type(r) is int:
+                    nat.check(r)
+                obs, rewards, terms, truncs, infos, self.sim_time, self.total_products_packaged = r
+                self._last_obs = obs
+                self._viewcache = None
+                self.current_step += 1
+                return obs, rewards, terms, truncs, infos
         codes = self._act_np
         codes.fill(255)   # an agent absent from the dict does not act
         order = []
@@ -273,6 +299,7 @@ class FJSPSimulation:
         if canon and self.use_server:
             if not self._srv_on:   # inline mode: the 8 action bytes ride in the doorbell's cache line
                 nat.check(self._L.fjsp_server_start(self._h, None, 0, self._packed.ref_full))
+                self._stepper = self._make_stepper()
                 self._srv_on = True
             nat.check(self._L.fjsp_server_step_actions(self._h, self._act_ptr))   # returns with the record written
         else:

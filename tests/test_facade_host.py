@@ -82,3 +82,83 @@ def test_obs_dicts_c_rejects_short_buffers(F):
         F.obs_dicts(z[:19], np.zeros(12, np.int8), np.zeros(6, np.float32), np.zeros(29, np.int8))
     with pytest.raises(ValueError):
         F.obs_dicts(z, np.zeros(12, np.int8), np.zeros(6, np.float32), np.zeros(28, np.int8))
+
+
+def _layout():
+    """FJSPSimulation._Packed's record layout (fields 8-byte aligned), without pinned memory."""
+    FS = importlib.import_module("multi-agent-rl-for-fjsp_amd.FJSPSimulation")
+    off, lay = 0, {}
+    for name, dt, n in FS._Packed.FIELDS:
+        off = (off + 7) & ~7
+        lay[name] = (off, np.dtype(dt), n)
+        off += np.dtype(dt).itemsize * n
+    return lay, (off + 7) & ~7
+
+
+def test_fast_step_matches_python_path(F):
+    """_facade.step (the facade's common step in C) against FJSPSimulation.step's Python
+    construction of the same record: the server function is a ctypes callback that checks the
+    action bytes and writes a golden-trace step into the record; every returned object equals the
+    Python path's (obs dicts, rewards, terminations, truncations, infos with the decoded action
+    results); dicts that are not the common case return None without calling the server; a
+    nonzero server return code is handed back."""
+    import ctypes
+    lay, nbytes = _layout()
+    rec = np.zeros(nbytes, np.uint8)
+    act = np.zeros(8, np.uint8)
+    view = {k: rec[o: o + dt.itemsize * n].view(dt) for k, (o, dt, n) in lay.items()}
+    d = np.load(os.path.join(G.REPO, "tests", "golden", "traces.npz"))
+    name = "masked_s1"
+    calls = []
+    state = {"t": 0, "rc": 0}
+
+    def server(h, a):
+        t = state["t"]
+        calls.append(bytes(act))
+        for k, src in (("obs_i32", "obs_i32"), ("obs_i8", "obs_i8"), ("obs_f32", "obs_f32"), ("masks", "masks"),
+                       ("rewards", "rewards"), ("results", "results")):
+            view[k][:] = d[f"{name}_{src}"][t]
+        view["term"][0] = d[f"{name}_term"][t]
+        view["trunc"][0] = d[f"{name}_trunc"][t]
+        view["orders_completed"][0] = d[f"{name}_orders_completed"][t]
+        view["packaged"][0] = d[f"{name}_packaged"][t]
+        view["sim_time"][0] = d[f"{name}_sim_time"][t]
+        return state["rc"]
+
+    cb = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)(server)
+    offs = [lay[k][0] for k in ("obs_i32", "obs_i8", "obs_f32", "masks", "rewards", "term", "trunc", "results",
+                                "orders_completed", "packaged", "sim_time")]
+    st = F.stepper(1, ctypes.cast(cb, ctypes.c_void_p).value, act.ctypes.data, rec.ctypes.data, offs, S.decode_result)
+    acts = d[f"{name}_actions"]
+    for t in range(0, 60):
+        state["t"] = t
+        a = {ag: int(acts[t][i]) for i, ag in enumerate(S.AGENTS)}
+        r = F.step(st, a)
+        assert calls[-1] == bytes(np.asarray(acts[t], np.uint8)), t
+        obs, rewards, terms, truncs, infos, sim_time, packaged = r
+        _same(obs, S.obs_dicts(view["obs_i32"], view["obs_i8"], view["obs_f32"], view["masks"]))
+        assert rewards == dict(zip(S.AGENTS, view["rewards"].tolist()))
+        assert all(type(x) is float for x in rewards.values())
+        assert terms == {ag: bool(view["term"][0]) for ag in S.AGENTS}
+        assert truncs == {ag: bool(view["trunc"][0]) for ag in S.AGENTS}
+        assert sim_time == float(view["sim_time"][0]) and type(sim_time) is float
+        assert packaged == int(view["packaged"][0]) and type(packaged) is int
+        oc = int(view["orders_completed"][0])
+        for i, ag in enumerate(S.AGENTS):
+            want = {"action_result": S.decode_result(ag, a[ag], int(view["results"][i])), "sim_time": sim_time,
+                    "orders_completed": oc, "total_products_packaged": packaged}
+            assert infos[ag] == want and list(infos[ag]) == list(want), (t, ag)
+        infos["agv"]["action_result"]["mutated"] = 1          # a fresh copy each step, not the cache's
+    n = len(calls)
+    good = {ag: 0 for ag in S.AGENTS}
+    for bad in (dict(reversed(list(good.items()))),                       # another dict order
+                {k: v for k, v in good.items() if k != "agv"},            # an agent missing
+                dict(good, extra=1),                                      # an extra key
+                dict(good, agv=np.int64(1)), dict(good, agv=True), dict(good, agv=1.0),
+                dict(good, agv=254), dict(good, agv=-1), dict(good, agv=1 << 70), list(good.items())):
+        assert F.step(st, bad) is None
+    assert len(calls) == n                                               # none of them reached the server
+    state["rc"] = -3
+    assert F.step(st, good) == -3
+    with pytest.raises(TypeError):
+        F.step(st)
