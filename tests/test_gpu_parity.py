@@ -115,22 +115,34 @@ def test_step_vs_fused(G):
         masks = r["next_masks"][0]
 
 
-@pytest.mark.parametrize("n,inline", [(1, False), (1, True), (100, False), (4096, False)])
-def test_step_server_equals_step(G, n, inline):
+def _pinned_buffers(G, n):
+    b = G.vec_env.Buffers(1, n, "cpu", infos=True, next_obs=True)
+    for k in G.native.OUT_FIELDS:
+        t = getattr(b, k, None)
+        if t is not None:
+            setattr(b, k, t.pin_memory())
+    return b
+
+
+@pytest.mark.parametrize("n,inline,host_out", [(1, False, False), (1, True, False), (100, False, False),
+                                               (4096, False, False), (4096, False, True)])
+def test_step_server_equals_step(G, n, inline, host_out):
     """The step server (fjsp_server_*: a resident kernel stepped through a host doorbell) ==
     fjsp_step launch by launch: random, absent and out-of-range actions from pinned host memory
     (inline: the one env's 8 action bytes in the doorbell's cache line, fjsp_server_step_actions),
     auto-resets, every output of every step; other calls on the handle in between (read_env,
     snapshot: the server leaves and is relaunched), a pause past the idle relaunch, the final state;
-    inline, also past the 16-bit wrap of the inbox's request tags."""
+    inline, also past the 16-bit wrap of the inbox's request tags; host_out: the server writes its
+    outputs straight into pinned host memory."""
     import time
-    rng = np.random.default_rng(n + inline)
+    rng = np.random.default_rng(n + inline + 2 * host_out)
     envs = [G.make_env(n), G.make_env(n)]
     for env in envs:
         env.reset(seeds=torch.arange(n) + 3, num_orders=30)
     hb = torch.zeros(8, n, dtype=torch.uint8).pin_memory()
     bs = envs[1].server_start(None if inline else hb, autoreset=True,
-                              buffers=G.vec_env.Buffers(1, n, envs[1].device, infos=True, next_obs=True))
+                              buffers=_pinned_buffers(G, n) if host_out else
+                              G.vec_env.Buffers(1, n, envs[1].device, infos=True, next_obs=True))
     assert envs[1].last_kernel() == "k_step_server"
     bl = G.vec_env.Buffers(1, n, envs[0].device, infos=True, next_obs=True)
     nact = np.array([3, 8, 3, 3, 3, 3, 3, 3]).reshape(8, 1)
