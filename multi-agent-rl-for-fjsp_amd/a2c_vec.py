@@ -1206,7 +1206,7 @@ class VecMultiAgentA2C:
 
     def __init__(self, env, batch_size=256, gamma=0.99, lamb=0.95, lr_actor=3e-4, lr_critic=1e-3,
                  use_gae=True, entropy_coef=0.01, max_grad_norm=0.5, hidden=256, seed=None, group=None,
-                 use_graph=True, fused_policy=True, exchange="allreduce", dedup=True):
+                 use_graph=None, fused_policy=True, exchange="allreduce", dedup=True):
         self.env = env
         self.device = env.device
         self.N = env.num_envs
@@ -1235,7 +1235,8 @@ class VecMultiAgentA2C:
         self.critic_loss_history = []
         self.episode_end_timesteps = []
         self._bufs = None
-        self.use_graph = bool(use_graph) and self.device.type == "cuda"
+        # None: decided per collect (_graph_on); True / False: always / never replay a captured graph
+        self.use_graph = None if use_graph is None else bool(use_graph) and self.device.type == "cuda"
         # fused policy kernel (csrc/fjsp_policy.hip): one launch per vector step
         self.fused_policy = bool(fused_policy) and self.device.type == "cuda" and hidden == 256
         # ... with the env step inside the same launch (fjsp_a2c_policy_step; False: the policy
@@ -1390,7 +1391,7 @@ class VecMultiAgentA2C:
         the buffers and parameters are static, Adam updates the weights in place."""
         self._rng_host += 1
         self._rng.fill_(_s64(self._rng_host))   # re-keys the sampling of the (captured) batch
-        if action_fn is None and self.use_graph:
+        if action_fn is None and self._graph_on():
             if self._graph is not None and self._graph_det == deterministic:
                 self._graph.replay()
                 return
@@ -1400,6 +1401,16 @@ class VecMultiAgentA2C:
                 return
         self._collect_eager(deterministic, action_fn)
         self._eager_batches += 1
+
+    def _graph_on(self):
+        """use_graph None (the default): replay a captured graph of the batch, except for the fused
+        collect on two or more env-group streams, whose launches are issued eagerly: the groups'
+        step chains then overlap more than in the graph's replay (collect 6.2-6.5 against 6.8-7.1 ms
+        per 256 x 4 096 batch, slabs byte-equal; profiles/r06/a2c/collect_graph_ab.json), and one
+        launch per group and step keeps the host ahead of the GPU."""
+        if self.use_graph is not None:
+            return self.use_graph
+        return self.device.type == "cuda" and not (self.fused_step and len(self._collect_groups()) >= 2)
 
     def _capture(self, deterministic):
         L = nat.lib()
