@@ -344,7 +344,7 @@ def a2c_throughput(env, N, world, batches, warmup, batch_size, num_orders, dist=
            "critic_loss_last": learner.critic_loss_history[-1], "update_dedup": bool(dedup),
            "exchange": exchange if world > 1 else None, "init": init,
            "note": "collect = one k_policy_step launch per vector step and env group (fused MFMA predict + "
-                   "the env step of each 64-env tile, features and masks written in HBM; hipGraph-captured) -> "
+                   "the env step of each 64-env tile, features and masks written in HBM; two env-group streams) -> "
                    "fp64 GAE kernel -> grouped full-batch update (8 actors + critic, Adam); reference a2c.py "
                    "loop: ~130 env-steps/s on one CPU core (SURVEY.md)"}
     if world > 1:
