@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define FJSP_ABI_VERSION 11
+#define FJSP_ABI_VERSION 12
 
 #define FJSP_NUM_AGENTS 8      /* pickup, agv, small, big, pkg_blue_1, pkg_blue_2, pkg_red, pkg_green */
 #define FJSP_OBS_I32 20        /* pickup 7 + agv 13 (position = 2) int32 observation fields */
@@ -376,6 +376,17 @@ int fjsp_a2c_record_head(const float* pu, int32_t umax, const int64_t* inv, int3
 int fjsp_a2c_critic_fused(const float* x, int32_t n, const float* critic_w, const float* w3t, const float* w2t,
                           const double* coef, float* h1, float* h2, float* g3, float* g2, float* g1, float* part,
                           double* loss, float* values, void* stream);
+/* The critic's weight gradients over the batch's distinct states (the backward of
+ * networks.CentralizedCriticNetwork's Linear layers, a2c.py:692-699 critic_loss.backward(); ABI 12;
+ * replaces three split-K f32 GEMMs): out f32 [m][ldo] columns < nout = g^T x over U rows,
+ * g f32 [U][ldg] (m features: 256 or 128, fjsp_a2c_critic_fused's g1 / g2 / g3), x f32 [U][ldx]
+ * (nx features, nx % 4 == 0: the 40-word rows of fjsp_a2c_group_keys (layer 1, nx <= 64, m = 256)
+ * or h1 / h2 (68 <= nx <= 256)); nout <= nx.  f32-level products (three bf16 planes, six plane
+ * products, as fjsp_a2c_policy), split over P workgroups of 32-sample stages whose partials
+ * part f32 [P][m][npad] (npad = 256 if nx > 64 else 64) are summed in a fixed order in f64:
+ * deterministic.  g, x 16-byte aligned.  Stream-ordered. */
+int fjsp_a2c_wgrad(const float* g, int32_t m, int64_t ldg, const float* x, int32_t nx, int64_t ldx, int64_t U,
+                   float* part, int32_t P, float* out, int32_t nout, int64_t ldo, void* stream);
 /* The critic's backward through its two 256-wide ReLU layers for the A2C update (a2c.py:692-699
  * critic_loss.backward(); a2c_vec._CriticGrouped): g3 f32 [n][128] (layer 3's pre-activation
  * gradient, fjsp_a2c_value_head_grad), h1 / h2 from fjsp_a2c_critic_forward, w3t / w2t = W3^T

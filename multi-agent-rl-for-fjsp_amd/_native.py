@@ -76,12 +76,12 @@ EXPORTS = ["fjsp_abi_version", "fjsp_last_error", "fjsp_default_config", "fjsp_c
            "fjsp_a2c_critic_backward", "fjsp_gae_shared",
            "fjsp_a2c_policy_step", "fjsp_a2c_group_temp_bytes", "fjsp_a2c_group_sort", "fjsp_a2c_group_runs",
            "fjsp_a2c_run_sums_bytes", "fjsp_a2c_run_sums", "fjsp_a2c_critic_fused", "fjsp_a2c_shard_keys", "fjsp_a2c_record_head", "fjsp_a2c_pack_mfma", "fjsp_a2c_slab_stats",
-           "fjsp_server_start", "fjsp_server_step", "fjsp_server_step_actions", "fjsp_server_stop"]
+           "fjsp_a2c_wgrad", "fjsp_server_start", "fjsp_server_step", "fjsp_server_step_actions", "fjsp_server_stop"]
 POLICY_ACTOR_DPAD, POLICY_CRITIC_DPAD = 16, 48
 POLICY_ACTOR_FLOATS = 3 * 256 * 16 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 8 * 256 + 16
 POLICY_CRITIC_FLOATS = 3 * 256 * 48 // 2 + 256 + 3 * 256 * 256 // 2 + 256 + 3 * 128 * 256 // 2 + 128 + 128 + 16
 CRITIC_FUSED_PW = 2 * 256 + 2 * 128 + 4   # floats per tile of fjsp_a2c_critic_fused's partial sums
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _lib = None
 
@@ -208,6 +208,7 @@ def lib():
         "fjsp_a2c_record_head": (I, [P, I, P, I, I, P, P, P, ctypes.c_float, ctypes.c_float, P, P, P]),
         "fjsp_a2c_pack_mfma": (I, [P, I, I, I, I, P, P]),
         "fjsp_a2c_slab_stats": (I, [P, P, I, I, P, P, P, P]),
+        "fjsp_a2c_wgrad": (I, [P, I, ctypes.c_int64, P, I, ctypes.c_int64, ctypes.c_int64, P, I, P, I, ctypes.c_int64, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

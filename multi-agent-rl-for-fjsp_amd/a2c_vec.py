@@ -99,8 +99,33 @@ class _LinearSplitK(torch.autograd.Function):
 
 
 def _critic_wgrad(gy, x, nx=None):
-    """A critic layer's weight gradient gy^T x[:, :nx] (split-K GEMM)."""
+    """A critic layer's weight gradient gy^T x[:, :nx]: on the GPU one fjsp_a2c_wgrad launch (the
+    samples' contraction on the matrix cores, f32-level products, deterministic; r06), else the
+    split-K GEMM."""
+    if gy.is_cuda and wgrad_kernel_on:
+        return critic_wgrad(gy, x, nx)
     return _splitk_wgrad(gy, x if nx is None else x[:, :nx])
+
+
+wgrad_kernel_on = True   # False: the critic's weight gradients as split-K hipBLASLt GEMMs (A/B)
+
+
+def critic_wgrad(g, x, nout=None, parts=None):
+    """fjsp_a2c_wgrad: g f32 [U, m] (m = 256 / 128), x f32 [U, nx] rows (both contiguous, nx % 4 == 0)
+    -> g^T x[:, :nout] f32 [m, nout]."""
+    U, m = g.shape
+    nx = x.shape[1]
+    nout = nx if nout is None else nout
+    g, x = g.contiguous(), x.contiguous()
+    npad = 256 if nx > 64 else 64
+    if parts is None:   # one workgroup per CU (the double-buffered images take 90-144 KB of LDS)
+        parts = 256
+    part = torch.empty(parts, m, npad, dtype=torch.float32, device=g.device)
+    out = torch.empty(m, nout, dtype=torch.float32, device=g.device)
+    V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    nat.check(nat.lib().fjsp_a2c_wgrad(V(g), m, m, V(x), nx, nx, U, V(part), parts, V(out), nout, nout,
+                                       ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)))
+    return out
 
 
 def _splitk_wgrad(gy, x):

@@ -1299,6 +1299,180 @@ k_critic_fused(PolicyArgs A, CriticFused F) {
     masked_grad_out(a[0], m1, F.g1, HID, part, col, n, 32 * wave, lane);
 }
 
+// The critic's weight gradients gW = G^T X over the batch's distinct states (r06; the backward of
+// networks.CentralizedCriticNetwork's Linear layers, a2c.py:683-699): G f32 [U][M] (k_critic_fused's
+// g1 / g2 / g3, sample-major), X f32 [U][nx] (x / h1 / h2) -> gW [M][nx].  The contraction runs over
+// the samples, so both MFMA operands need 8 consecutive SAMPLES of one feature per lane while the
+// rows hold consecutive features.  Each workgroup owns a contiguous run of 16-sample stages
+// (split-K) and its whole [M][NPAD] output in the accumulators of its 8 waves (TM x TN 32 x 32 tiles
+// each).  Per stage, waves 0-3 load the G tile and waves 4-7 the X tile (4 samples x 4 features per
+// lane, 128-byte row segments; one stage ahead into registers), split them into the three bf16
+// planes and write them TRANSPOSED into LDS images [plane][feature][16 samples] (48-byte rows: the
+// fragment reads of every ds_read_b128 lane group hit distinct banks); the images are double
+// buffered, so the split and the stores of stage s + 1 run beside the MFMAs of stage s with one
+// barrier per stage.  Six plane products per 16-deep block (mfma6: f32-level products, as the
+// forward).  The per-workgroup partials are summed in a fixed order (k_wgrad_reduce, f64):
+// deterministic.  Replaces three split-K hipBLASLt f32 GEMMs with both operands' K strided.
+constexpr int WG_KS = 16;                  // samples per stage: one 16-deep block
+constexpr int WG_ROW = 24;                 // bf16 per LDS image row (16 samples + 8 of padding)
+// one stage of F features (F % 4 == 0, F <= 256) -> registers: lane t (0..255 of its wave half)
+// holds the 4 x 4 block (samples 4 (t & 3) .., features 4 (t >> 2) ..).  Buffer loads through a
+// descriptor over the workgroup's rows: the lane's 32-bit offsets are fixed for the launch and the
+// stage advances a scalar offset; rows past U (past the descriptor's range) and features past F
+// (an offset outside it) load zeros.  (64-bit per-lane address arithmetic for plain loads made the
+// compiler wait for every load in flight at each stage instead of for the oldest stage's.)
+struct WgSrc {
+    __amdgpu_buffer_rsrc_t rsrc;
+    int voff[4];
+};
+__device__ __forceinline__ WgSrc wg_src(const float* src, int64_t ld, int F, int64_t r0, int64_t U, int t) {
+    WgSrc w;
+    const int64_t rem = (U - r0) * ld * 4;
+    const int bytes = rem <= 0 ? 0 : rem > 0x7FFFFF00ll ? 0x7FFFFF00 : (int)rem;
+    w.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src + r0 * ld), (short)0, bytes, 0x00020000);
+    const int sq = t & 3, fq = t >> 2;
+#pragma unroll
+    for (int i = 0; i < 4; i++) w.voff[i] = 4 * fq < F ? (int)(((4 * sq + i) * ld + 4 * fq) * 4) : 0x7FFFFFF0;
+    return w;
+}
+__device__ __forceinline__ void wg_load(const WgSrc& w, int soff, float4 (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(w.rsrc, w.voff[i], soff, 0);
+        v[i] = make_float4(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[2]), __uint_as_float(r[3]));
+    }
+}
+__device__ __forceinline__ float f4c(const float4& v, int c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
+// the block's planes into an image [NP][rows][WG_ROW]: per feature 4 samples = 8 bytes per plane
+__device__ __forceinline__ void wg_store(const float4 (&v)[4], int F, int t, __bf16* s, int plane) {
+    const int sq = t & 3, fq = t >> 2;
+    if (4 * fq >= F) return;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        bf16x4 ph, pm, pl;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            __bf16 x0, x1, x2;
+            split3(f4c(v[i], c), x0, x1, x2);
+            ph[i] = x0;
+            pm[i] = x1;
+            pl[i] = x2;
+        }
+        const int o = (4 * fq + c) * WG_ROW + 4 * sq;
+        *reinterpret_cast<bf16x4*>(s + o) = ph;
+        *reinterpret_cast<bf16x4*>(s + plane + o) = pm;
+        *reinterpret_cast<bf16x4*>(s + 2 * plane + o) = pl;
+    }
+}
+// D: stages in flight per lane (register sets; the loads of stage s + D are issued when stage s + 1
+// is stored, so D - 1 stages of loads wait under the MFMAs: one stage in flight per CU left the
+// kernel at ~2 TB/s, latency-bound)
+template <int M, int NPAD, int TM, int TN, int D>
+__global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_wgrad(const float* __restrict__ g, int64_t ldg, const float* __restrict__ x, int64_t ldx, int nx, int64_t U,
+        float* __restrict__ part) {
+    static_assert((M / 32 / TM) * (NPAD / 32 / TN) == NWAVE, "one tile group per wave");
+    constexpr int PG = M * WG_ROW, PX = NPAD * WG_ROW;   // plane sizes (bf16)
+    constexpr int BUF = NP * (PG + PX);                  // one stage's images
+    __shared__ __attribute__((aligned(16))) __bf16 s_img[2 * BUF];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool ldr_g = wave < 4;                         // this wave's share of the loads: G or X
+    const int t = tid & 255;
+    constexpr int WN = NPAD / 32 / TN;
+    const int mb0 = (wave / WN) * TM, nb0 = (wave % WN) * TN;
+    // this workgroup's stages
+    const int64_t stages = (U + WG_KS - 1) / WG_KS, P = gridDim.x;
+    const int64_t per = (stages + P - 1) / P, s0 = (int64_t)blockIdx.x * per;
+    const int64_t s1 = s0 + per < stages ? s0 + per : stages;
+    if (nx < NPAD)   // the X image rows past nx stay zero for the whole launch
+        for (int b = 0; b < 2; b++)
+            for (int i = tid; i < NP * PX / 2; i += NTHR)
+                reinterpret_cast<uint32_t*>(s_img + b * BUF + NP * PG)[i] = 0u;
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.0f;
+    const int64_t ld = ldr_g ? ldg : ldx;
+    const int F = ldr_g ? M : nx;
+    const int img = ldr_g ? 0 : NP * PG, pls = ldr_g ? PG : PX;
+    const WgSrc ws = wg_src(ldr_g ? g : x, ld, F, s0 * WG_KS, U, t);
+    const int sstride = (int)(WG_KS * ld * 4);      // bytes per stage
+    float4 v[D][4];   // register set k holds the stages s0 + k (mod D)
+    if (s0 < s1) {
+        // loads are unconditional (past the workgroup's stages they read zeros or unused rows, in
+        // bounds): a conditional load's register merge made the compiler wait for it at once
+#pragma unroll
+        for (int k = 0; k < D; k++) wg_load(ws, k * sstride, v[k]);
+        __syncthreads();                            // the zeroed rows before the stores
+        wg_store(v[0], F, t, s_img + img, pls);
+        wg_load(ws, D * sstride, v[0]);
+    }
+    __syncthreads();
+    const int h = lane >> 5, r32 = lane & 31;
+    for (int64_t sb = s0; sb < s1; sb += D) {
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            const int64_t s = sb + d;
+            if (s >= s1) break;
+            const __bf16* cg = s_img + (int)((s - s0) & 1) * BUF;
+            const __bf16* cx = cg + NP * PG;
+            bf16x8 a[TM][NP];
+#pragma unroll
+            for (int i = 0; i < TM; i++) {
+                const int o = (32 * (mb0 + i) + r32) * WG_ROW + 8 * h;
+#pragma unroll
+                for (int p = 0; p < NP; p++) a[i][p] = *reinterpret_cast<const bf16x8*>(cg + p * PG + o);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                bf16x8 b[NP];
+                const int o = (32 * (nb0 + j) + r32) * WG_ROW + 8 * h;
+#pragma unroll
+                for (int p = 0; p < NP; p++) b[p] = *reinterpret_cast<const bf16x8*>(cx + p * PX + o);
+#pragma unroll
+                for (int i = 0; i < TM; i++) acc[i][j] = mfma6(a[i], b, acc[i][j]);
+            }
+            // stage s + 1 into the other buffer, stage s + 1 + D's loads out
+            const int k = (d + 1) % D;
+            if (s + 1 < s1) wg_store(v[k], F, t, s_img + (int)((s + 1 - s0) & 1) * BUF + img, pls);
+            wg_load(ws, (int)(s + 1 + D - s0) * sstride, v[k]);
+            __syncthreads();
+        }
+    }
+    // the partial [M][NPAD] of this workgroup: C/D row (r & 3) + 8 (r >> 2) + 4 h, column lane & 31
+    float* pp = part + (size_t)blockIdx.x * M * NPAD;
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                pp[(size_t)(32 * (mb0 + i) + (r & 3) + 8 * (r >> 2) + 4 * h) * NPAD + 32 * (nb0 + j) + r32] = acc[i][j][r];
+}
+// out [M][ldo] (columns < nout) = the sum of the P partials in partial order, in f64
+__global__ void __launch_bounds__(256) k_wgrad_reduce(const float* __restrict__ part, int P, int M, int npad, int nout,
+                                                      float* __restrict__ out, int64_t ldo) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= M * nout) return;
+    const int m = i / nout, c = i - m * nout;
+    const float* p = part + (size_t)m * npad + c;
+    const size_t stride = (size_t)M * npad;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int q = 0;
+    for (; q + 4 <= P; q += 4) {
+        s0 += p[(size_t)q * stride];
+        s1 += p[(size_t)(q + 1) * stride];
+        s2 += p[(size_t)(q + 2) * stride];
+        s3 += p[(size_t)(q + 3) * stride];
+    }
+    for (; q < P; q++) s0 += p[(size_t)q * stride];
+    out[(size_t)m * ldo + c] = (float)((s0 + s1) + (s2 + s3));
+}
+
 // Keys of the A2C update's grouping of repeated inputs (a2c_vec.row_keys, the same hash): per
 // sample s = t * n + e of feats f32 [T][38][n], key a < 8 over actor a's 13 padded input columns
 // (its OBS_DIMS[a] a2c features, then zeros), key 8 over all 38; k = fmix64(k * MUL + bits(x_c)
@@ -1957,6 +2131,37 @@ extern "C" int fjsp_a2c_critic_fused(const float* x, int32_t n, const float* cri
     PolicyArgs A{x, nullptr, n, nullptr, critic_w, nullptr, 0u, 0u, 0, nullptr, values, nullptr, (n + TC - 1) / TC, 0};
     const CriticFused F{coef, w3t, w2t, h1, h2, g3, g2, g1, part, loss, values};
     hipLaunchKernelGGL(k_critic_fused, dim3((unsigned)A.nc), dim3(NTHR), 0, (hipStream_t)stream, A, F);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        fjsp_internal_fail(hipGetErrorString(err));
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int fjsp_a2c_wgrad(const float* g, int32_t m, int64_t ldg, const float* x, int32_t nx, int64_t ldx, int64_t U,
+                              float* part, int32_t P, float* out, int32_t nout, int64_t ldo, void* stream) {
+    if (U <= 0 || P <= 0) return fjsp_internal_fail("fjsp_a2c_wgrad: U and P must be > 0");
+    if (!g || !x || !part || !out) return fjsp_internal_fail("fjsp_a2c_wgrad: null buffer");
+    if (((uintptr_t)g | (uintptr_t)x) & 15u || (ldg & 3) || (ldx & 3) || (nx & 3) || ldg < m || ldx < nx)
+        return fjsp_internal_fail("fjsp_a2c_wgrad: g and x must be 16-byte aligned rows (ld % 4 == 0, nx % 4 == 0)");
+    if (nout <= 0 || nout > nx || ldo < nout) return fjsp_internal_fail("fjsp_a2c_wgrad: 0 < nout <= nx, ldo >= nout");
+    const hipStream_t st = (hipStream_t)stream;
+    int npad;
+    if (m == 256 && nx > 64 && nx <= 256) {
+        npad = 256;
+        hipLaunchKernelGGL((k_wgrad<256, 256, 2, 4, 2>), dim3((unsigned)P), dim3(NTHR), 0, st, g, ldg, x, ldx, nx, U, part);
+    } else if (m == 128 && nx > 64 && nx <= 256) {
+        npad = 256;
+        hipLaunchKernelGGL((k_wgrad<128, 256, 2, 2, 4>), dim3((unsigned)P), dim3(NTHR), 0, st, g, ldg, x, ldx, nx, U, part);
+    } else if (m == 256 && nx <= 64) {
+        npad = 64;
+        hipLaunchKernelGGL((k_wgrad<256, 64, 1, 2, 4>), dim3((unsigned)P), dim3(NTHR), 0, st, g, ldg, x, ldx, nx, U, part);
+    } else {
+        return fjsp_internal_fail("fjsp_a2c_wgrad: (m, nx) must be (256, 68..256), (128, 68..256) or (256, 4..64)");
+    }
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((m * nout + 255) / 256)), dim3(256), 0, st, part, P, m, npad, nout,
+                       out, ldo);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
         fjsp_internal_fail(hipGetErrorString(err));

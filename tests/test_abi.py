@@ -20,7 +20,7 @@ def test_library_exports_every_symbol():
     L = G.native.lib()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.fjsp_abi_version() == G.native.ABI_VERSION == 11
+    assert L.fjsp_abi_version() == G.native.ABI_VERSION == 12
 
 
 def test_config_validation_without_gpu():
@@ -109,6 +109,29 @@ def test_update_kernels_validate_arguments_without_gpu():
     assert L.fjsp_a2c_slab_stats(a, a, 0, 4, a, a, a, None) != 0
     assert L.fjsp_a2c_shard_keys(a, a, a, 0, 4, a, a, a, None) != 0
     assert L.fjsp_a2c_shard_keys(a, None, a, 4, 4, a, a, a, None) != 0
+
+
+def test_wgrad_validates_arguments_without_gpu():
+    """fjsp_a2c_wgrad (ABI 12) rejects empty batches, null buffers, unaligned or ragged rows and
+    unsupported layer shapes before launching."""
+    L = G.native.lib()
+    P = ctypes.c_void_p
+    a = P(1 << 20)
+    ok = [a, 256, 256, a, 256, 256, 1000, a, 256, a, 256, 256, None]
+
+    def bad(i, v, msg):
+        b = list(ok)
+        b[i] = v
+        assert L.fjsp_a2c_wgrad(*b) != 0 and msg in L.fjsp_last_error(), (i, v)
+    bad(6, 0, b"must be > 0")
+    bad(8, 0, b"must be > 0")
+    bad(3, None, b"null")
+    bad(9, None, b"null")
+    bad(0, P((1 << 20) + 4), b"16-byte aligned")
+    bad(4, 38, b"16-byte aligned")            # nx % 4 != 0
+    bad(2, 128, b"16-byte aligned")           # ldg < m
+    bad(10, 300, b"nout")
+    bad(1, 64, b"(m, nx)")
 
 
 def test_library_wide_policy_options_without_gpu():

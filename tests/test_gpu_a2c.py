@@ -798,6 +798,32 @@ def test_critic_onepass_matches_float64(M):
         assert eo <= max(3 * et, 3e-3), (eo, et)
 
 
+@pytest.mark.parametrize("m,nx,nout,U", [(256, 256, 256, 70001), (128, 256, 256, 33), (256, 40, 38, 70001),
+                                         (256, 40, 38, 5), (256, 256, 256, 540017), (128, 256, 256, 540017)])
+def test_wgrad_kernel_matches_float64(M, m, nx, nout, U):
+    """fjsp_a2c_wgrad (a2c_vec.critic_wgrad: the critic's weight gradients g^T x over the distinct
+    states on the matrix cores, split-bf16 products, r06) against float64 for the three layer
+    shapes (layer 1 reads the 40-word rows and keeps 38 columns), ragged sample counts (not a
+    multiple of the 32-sample stage, fewer stages than workgroups) and a full update's state count:
+    relative Frobenius error within max(3x the split-K f32 GEMM's, 2e-6), and bit-identical on a
+    second call (the partials are added in a fixed order)."""
+    A = M["A"]
+    torch.manual_seed(5)
+    g = torch.randn(U, m, device="cuda") * (torch.rand(U, m, device="cuda") > 0.5)
+    if nx == 40:
+        x = torch.nn.functional.pad(torch.rand(U, 38, device="cuda") * 30, (0, 2)).contiguous()
+    else:
+        x = torch.relu(torch.randn(U, nx, device="cuda"))
+    ref = g.double().t() @ x[:, :nout].double()
+    gw = A.critic_wgrad(g, x, nout)
+    assert gw.shape == (m, nout)
+    e = float((gw.double() - ref).norm() / ref.norm())
+    et = float((A._splitk_wgrad(g, x[:, :nout]).double() - ref).norm() / ref.norm())
+    assert e <= max(3 * et, 2e-6), (e, et)
+    assert torch.equal(gw, A.critic_wgrad(g, x, nout))
+    assert torch.equal(gw, A._critic_wgrad(g, x, nout if nout != nx else None))
+
+
 def test_prefix_at_equals_full_prefix_sum_on_gpu(M):
     """_prefix_at (the run sums' prefix values at the run ends only, the f64 cast inside the scan)
     is bit-identical to the full f64 prefix sum gathered at the same positions, on the GPU's scan."""
