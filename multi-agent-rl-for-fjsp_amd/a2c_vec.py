@@ -120,12 +120,21 @@ def critic_wgrad(g, x, nout=None, parts=None):
     npad = 256 if nx > 64 else 64
     if parts is None:   # one workgroup per CU (the double-buffered images take 90-144 KB of LDS)
         parts = 256
+    # the kernel's buffer offsets are 32-bit: longer batches in chunks, summed in order
+    rows = min(WGRAD_MAX_ROWS, (0x7FFFFF00 // (4 * max(m, nx))) - 5 * parts * 16)
     part = torch.empty(parts, m, npad, dtype=torch.float32, device=g.device)
-    out = torch.empty(m, nout, dtype=torch.float32, device=g.device)
     V = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    nat.check(nat.lib().fjsp_a2c_wgrad(V(g), m, m, V(x), nx, nx, U, V(part), parts, V(out), nout, nout,
-                                       ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)))
+    st = ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)
+    out = None
+    for r0 in range(0, U, rows):
+        n = min(rows, U - r0)
+        o = torch.empty(m, nout, dtype=torch.float32, device=g.device)
+        nat.check(nat.lib().fjsp_a2c_wgrad(V(g[r0:]), m, m, V(x[r0:]), nx, nx, n, V(part), parts, V(o), nout, nout, st))
+        out = o if out is None else out.add_(o)
     return out
+
+
+WGRAD_MAX_ROWS = 1 << 40   # chunk size cap (tests lower it to exercise the chunked path)
 
 
 def _splitk_wgrad(gy, x):

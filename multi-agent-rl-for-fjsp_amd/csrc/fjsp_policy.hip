@@ -1315,12 +1315,14 @@ k_critic_fused(PolicyArgs A, CriticFused F) {
 // deterministic.  Replaces three split-K hipBLASLt f32 GEMMs with both operands' K strided.
 constexpr int WG_KS = 16;                  // samples per stage: one 16-deep block
 constexpr int WG_ROW = 24;                 // bf16 per LDS image row (16 samples + 8 of padding)
+constexpr int WG_MAXD = 4;                 // the deepest load pipeline of the k_wgrad instances
+constexpr int WG_VPM = 2;                  // split VALU per MFMA in the interleave
 // one stage of F features (F % 4 == 0, F <= 256) -> registers: lane t (0..255 of its wave half)
 // holds the 4 x 4 block (samples 4 (t & 3) .., features 4 (t >> 2) ..).  Buffer loads through a
-// descriptor over the workgroup's rows: the lane's 32-bit offsets are fixed for the launch and the
-// stage advances a scalar offset; rows past U (past the descriptor's range) and features past F
-// (an offset outside it) load zeros.  (64-bit per-lane address arithmetic for plain loads made the
-// compiler wait for every load in flight at each stage instead of for the oldest stage's.)
+// descriptor over the rows from the workgroup's first stage on; the lane's offsets within a stage
+// are fixed for the launch.  Rows past U (outside the descriptor) and features past F (an offset
+// outside it) load zeros.  (64-bit per-lane address arithmetic for plain loads, and loads under a
+// branch, made the compiler wait for every load in flight at each stage.)
 struct WgSrc {
     __amdgpu_buffer_rsrc_t rsrc;
     int voff[4];
@@ -1335,18 +1337,21 @@ __device__ __forceinline__ WgSrc wg_src(const float* src, int64_t ld, int F, int
     for (int i = 0; i < 4; i++) w.voff[i] = 4 * fq < F ? (int)(((4 * sq + i) * ld + 4 * fq) * 4) : 0x7FFFFFF0;
     return w;
 }
-__device__ __forceinline__ void wg_load(const WgSrc& w, int soff, float4 (&v)[4]) {
+// off: the stage's byte offset, added in the lane offsets (the descriptor's range check then sees it)
+__device__ __forceinline__ void wg_load(const WgSrc& w, int off, float4 (&v)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        const auto r = __builtin_amdgcn_raw_buffer_load_b128(w.rsrc, w.voff[i], soff, 0);
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(w.rsrc, (int)((unsigned)w.voff[i] + (unsigned)off), 0, 0);
         v[i] = make_float4(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[2]), __uint_as_float(r[3]));
     }
 }
 __device__ __forceinline__ float f4c(const float4& v, int c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
-// the block's planes into an image [NP][rows][WG_ROW]: per feature 4 samples = 8 bytes per plane
-__device__ __forceinline__ void wg_store(const float4 (&v)[4], int F, int t, __bf16* s, int plane) {
+// the block's planes into an image [NP][256 rows][WG_ROW]: per feature 4 samples = 8 bytes per
+// plane.  Every lane stores (lanes past F store the zeros they loaded: the image rows past F are
+// zero), so the stores and the MFMAs share one basic block and interleave
+__device__ __forceinline__ void wg_store(const float4 (&v)[4], int t, __bf16* s) {
+    constexpr int plane = 256 * WG_ROW;
     const int sq = t & 3, fq = t >> 2;
-    if (4 * fq >= F) return;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
         bf16x4 ph, pm, pl;
@@ -1364,16 +1369,16 @@ __device__ __forceinline__ void wg_store(const float4 (&v)[4], int F, int t, __b
         *reinterpret_cast<bf16x4*>(s + 2 * plane + o) = pl;
     }
 }
-// D: stages in flight per lane (register sets; the loads of stage s + D are issued when stage s + 1
-// is stored, so D - 1 stages of loads wait under the MFMAs: one stage in flight per CU left the
-// kernel at ~2 TB/s, latency-bound)
+// D: stages in flight per lane (register sets; the loads of stage j + D are issued when stage j + 1
+// is stored, so D - 1 stages of loads wait under the MFMAs; one stage in flight left the kernel
+// latency-bound at ~2 TB/s)
 template <int M, int NPAD, int TM, int TN, int D>
 __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_wgrad(const float* __restrict__ g, int64_t ldg, const float* __restrict__ x, int64_t ldx, int nx, int64_t U,
         float* __restrict__ part) {
     static_assert((M / 32 / TM) * (NPAD / 32 / TN) == NWAVE, "one tile group per wave");
-    constexpr int PG = M * WG_ROW, PX = NPAD * WG_ROW;   // plane sizes (bf16)
-    constexpr int BUF = NP * (PG + PX);                  // one stage's images
+    constexpr int PL = 256 * WG_ROW;                     // plane size (bf16): 256 rows, whatever M / nx
+    constexpr int BUF = 2 * NP * PL;                     // one stage's two images (G, X)
     __shared__ __attribute__((aligned(16))) __bf16 s_img[2 * BUF];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1381,14 +1386,10 @@ k_wgrad(const float* __restrict__ g, int64_t ldg, const float* __restrict__ x, i
     const int t = tid & 255;
     constexpr int WN = NPAD / 32 / TN;
     const int mb0 = (wave / WN) * TM, nb0 = (wave % WN) * TN;
-    // this workgroup's stages
-    const int64_t stages = (U + WG_KS - 1) / WG_KS, P = gridDim.x;
-    const int64_t per = (stages + P - 1) / P, s0 = (int64_t)blockIdx.x * per;
-    const int64_t s1 = s0 + per < stages ? s0 + per : stages;
-    if (nx < NPAD)   // the X image rows past nx stay zero for the whole launch
-        for (int b = 0; b < 2; b++)
-            for (int i = tid; i < NP * PX / 2; i += NTHR)
-                reinterpret_cast<uint32_t*>(s_img + b * BUF + NP * PG)[i] = 0u;
+    // this workgroup's stages b, b + P, b + 2P, ...: at any time the workgroups stream one window of
+    // rows (contiguous runs per workgroup measured the same)
+    const int64_t stages = (U + WG_KS - 1) / WG_KS, P = gridDim.x, b = blockIdx.x;
+    const int nj = stages > b ? (int)((stages - b + P - 1) / P) : 0;
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; i++)
@@ -1397,49 +1398,54 @@ k_wgrad(const float* __restrict__ g, int64_t ldg, const float* __restrict__ x, i
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] = 0.0f;
     const int64_t ld = ldr_g ? ldg : ldx;
-    const int F = ldr_g ? M : nx;
-    const int img = ldr_g ? 0 : NP * PG, pls = ldr_g ? PG : PX;
-    const WgSrc ws = wg_src(ldr_g ? g : x, ld, F, s0 * WG_KS, U, t);
-    const int sstride = (int)(WG_KS * ld * 4);      // bytes per stage
-    float4 v[D][4];   // register set k holds the stages s0 + k (mod D)
-    if (s0 < s1) {
-        // loads are unconditional (past the workgroup's stages they read zeros or unused rows, in
-        // bounds): a conditional load's register merge made the compiler wait for it at once
+    const int img = ldr_g ? 0 : NP * PL;
+    const WgSrc ws = wg_src(ldr_g ? g : x, ld, ldr_g ? M : nx, b * WG_KS, U, t);
+    const int sstride = (int)(P * WG_KS * ld * 4);  // bytes from one of this workgroup's stages to the next
+    float4 v[D][4];   // register set k holds the stages j = k (mod D)
+    if (nj > 0) {
+        // loads are unconditional (past the last stage they read zeros): a conditional load's
+        // register merge made the compiler wait for it at once
 #pragma unroll
         for (int k = 0; k < D; k++) wg_load(ws, k * sstride, v[k]);
-        __syncthreads();                            // the zeroed rows before the stores
-        wg_store(v[0], F, t, s_img + img, pls);
+        wg_store(v[0], t, s_img + img);
         wg_load(ws, D * sstride, v[0]);
     }
     __syncthreads();
     const int h = lane >> 5, r32 = lane & 31;
-    for (int64_t sb = s0; sb < s1; sb += D) {
+    for (int jb = 0; jb < nj; jb += D) {
 #pragma unroll
         for (int d = 0; d < D; d++) {
-            const int64_t s = sb + d;
-            if (s >= s1) break;
-            const __bf16* cg = s_img + (int)((s - s0) & 1) * BUF;
-            const __bf16* cx = cg + NP * PG;
+            const int j = jb + d;
+            if (j >= nj) break;
+            const __bf16* cg = s_img + (j & 1) * BUF;
+            const __bf16* cx = cg + NP * PL;
             bf16x8 a[TM][NP];
 #pragma unroll
             for (int i = 0; i < TM; i++) {
                 const int o = (32 * (mb0 + i) + r32) * WG_ROW + 8 * h;
 #pragma unroll
-                for (int p = 0; p < NP; p++) a[i][p] = *reinterpret_cast<const bf16x8*>(cg + p * PG + o);
+                for (int p = 0; p < NP; p++) a[i][p] = *reinterpret_cast<const bf16x8*>(cg + p * PL + o);
             }
 #pragma unroll
-            for (int j = 0; j < TN; j++) {
-                bf16x8 b[NP];
-                const int o = (32 * (nb0 + j) + r32) * WG_ROW + 8 * h;
+            for (int jj = 0; jj < TN; jj++) {
+                bf16x8 bb[NP];
+                const int o = (32 * (nb0 + jj) + r32) * WG_ROW + 8 * h;
 #pragma unroll
-                for (int p = 0; p < NP; p++) b[p] = *reinterpret_cast<const bf16x8*>(cx + p * PX + o);
+                for (int p = 0; p < NP; p++) bb[p] = *reinterpret_cast<const bf16x8*>(cx + p * PL + o);
 #pragma unroll
-                for (int i = 0; i < TM; i++) acc[i][j] = mfma6(a[i], b, acc[i][j]);
+                for (int i = 0; i < TM; i++) acc[i][jj] = mfma6(a[i], bb, acc[i][jj]);
             }
-            // stage s + 1 into the other buffer, stage s + 1 + D's loads out
+            // stage j + 1 into the other buffer (past the last stage: zeros nobody reads), stage
+            // j + 1 + D's loads out, the split and stores interleaved with this stage's MFMAs
             const int k = (d + 1) % D;
-            if (s + 1 < s1) wg_store(v[k], F, t, s_img + (int)((s + 1 - s0) & 1) * BUF + img, pls);
-            wg_load(ws, (int)(s + 1 + D - s0) * sstride, v[k]);
+            wg_store(v[k], t, s_img + ((j + 1) & 1) * BUF + img);
+            wg_load(ws, (j + 1 + D) * sstride, v[k]);
+#pragma unroll
+            for (int q = 0; q < TM * TN * 6; q++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);          // one MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, WG_VPM, 0);     // VALU of the split
+                if (q % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // an LDS store
+            }
             __syncthreads();
         }
     }
@@ -2146,6 +2152,10 @@ extern "C" int fjsp_a2c_wgrad(const float* g, int32_t m, int64_t ldg, const floa
     if (((uintptr_t)g | (uintptr_t)x) & 15u || (ldg & 3) || (ldx & 3) || (nx & 3) || ldg < m || ldx < nx)
         return fjsp_internal_fail("fjsp_a2c_wgrad: g and x must be 16-byte aligned rows (ld % 4 == 0, nx % 4 == 0)");
     if (nout <= 0 || nout > nx || ldo < nout) return fjsp_internal_fail("fjsp_a2c_wgrad: 0 < nout <= nx, ldo >= nout");
+    // buffer-load offsets are 32-bit: the rows, plus the stages read ahead past the last one
+    const int64_t ldm = ldg > ldx ? ldg : ldx;
+    if ((U + (int64_t)(WG_MAXD + 1) * P * WG_KS) * ldm * 4 > 0x7FFFFF00ll || (int64_t)P * WG_KS * ldm * 4 > 0x7FFFFFFFll)
+        return fjsp_internal_fail("fjsp_a2c_wgrad: U * ld * 4 must stay below 2 GiB (split the batch)");
     const hipStream_t st = (hipStream_t)stream;
     int npad;
     if (m == 256 && nx > 64 && nx <= 256) {

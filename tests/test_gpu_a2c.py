@@ -822,6 +822,15 @@ def test_wgrad_kernel_matches_float64(M, m, nx, nout, U):
     assert e <= max(3 * et, 2e-6), (e, et)
     assert torch.equal(gw, A.critic_wgrad(g, x, nout))
     assert torch.equal(gw, A._critic_wgrad(g, x, nout if nout != nx else None))
+    if U > 100000:   # the chunked path (batches past the kernel's 2 GiB offset range): the same sum
+        old = A.WGRAD_MAX_ROWS
+        try:
+            A.WGRAD_MAX_ROWS = U // 3 + 5
+            gc = A.critic_wgrad(g, x, nout)
+        finally:
+            A.WGRAD_MAX_ROWS = old
+        ec = float((gc.double() - ref).norm() / ref.norm())
+        assert ec <= max(3 * et, 2e-6), (ec, et)
 
 
 def test_prefix_at_equals_full_prefix_sum_on_gpu(M):
