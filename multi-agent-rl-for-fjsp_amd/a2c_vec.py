@@ -90,7 +90,7 @@ class _LinearSplitK(torch.autograd.Function):
             gy, gb = _relu_bias_grad(gy.contiguous(), y)            # one pass (HIP kernel)
         elif ctx.relu:
             gy = torch.ops.aten.threshold_backward(gy, y, 0.0)      # relu' from the output
-        gW = _splitk_wgrad(gy, x)
+        gW = critic_wgrad(gy, x) if _wgrad_fits(gy, x) else _splitk_wgrad(gy, x)
         gx = None
         if ctx.needs_input_grad[0]:
             # one output (the value head): an outer product, elementwise (a K = 1 GEMM is slow)
@@ -108,6 +108,16 @@ def _critic_wgrad(gy, x, nx=None):
 
 
 wgrad_kernel_on = True   # False: the critic's weight gradients as split-K hipBLASLt GEMMs (A/B)
+
+
+def _wgrad_fits(gy, x):
+    """fjsp_a2c_wgrad takes this gy^T x (contiguous rows, a supported layer shape): the critic's
+    layers and the long-batch actor's 256-wide hidden layer (_LinearSplitK)."""
+    if not (gy.is_cuda and wgrad_kernel_on and gy.dim() == 2 and x.dim() == 2 and gy.is_contiguous()
+            and x.is_contiguous() and x.shape[1] % 4 == 0):
+        return False
+    m, nx = gy.shape[1], x.shape[1]
+    return (m in (128, 256) and 68 <= nx <= 256) or (m == 256 and 4 <= nx <= 64)
 
 
 def critic_wgrad(g, x, nout=None, parts=None):
@@ -267,7 +277,7 @@ class _CriticOnePass(torch.autograd.Function):
     def backward(ctx, gl):
         grads = critic_onepass_grads(*ctx.parts)
         ctx.parts = None
-        return (None, None) + tuple(g * gl for g in grads)
+        return (None, None) + tuple(torch._foreach_mul(list(grads), gl))
 
 
 @torch.no_grad()
@@ -464,11 +474,11 @@ class ActorStack(nn.Module):
         h = torch.relu(torch.baddbmm(self.b2[ridx], self.W2[ridx], h))
         pr = torch.softmax(torch.baddbmm(self.b3[ridx], self.W3[ridx], h) + self.logit_pad[ridx], dim=1)
         pb = self.agent_probs(big, xb)
-        out = [None] * NA
-        out[big] = torch.nn.functional.pad(pb, (0, umax - ub))
-        for i, a in enumerate(rest):
-            out[a] = torch.nn.functional.pad(pr[i], (0, umax - u2))
-        return torch.stack(out)
+        # rest is range(NA) without big, in order: the stacked agents around the big one (three
+        # launches; eight pads and a stack before)
+        pr = torch.nn.functional.pad(pr, (0, umax - u2))
+        pb = torch.nn.functional.pad(pb, (0, umax - ub))[None]
+        return torch.cat([pr[:big], pb, pr[big:]])
 
     def forward_grouped(self, x, keys=None):
         """forward on x [8, 13, S], each actor run once per distinct observation of its agent,
@@ -1072,10 +1082,8 @@ class A2CLosses:
 def clip_per_agent_(actors, max_norm):
     """torch.nn.utils.clip_grad_norm_ applied to each agent's actor separately (a2c.py:675-679)."""
     grads = [p.grad for p in actors.parameters() if p.grad is not None]
-    sq = torch.zeros(NA, dtype=torch.float32, device=grads[0].device)
-    for g in grads:
-        sq += g.reshape(NA, -1).pow(2).sum(dim=1)
-    norm = sq.sqrt()
+    # every agent's gradients as one row, one norm launch (was three launches per parameter)
+    norm = torch.linalg.vector_norm(torch.cat([g.reshape(NA, -1) for g in grads], dim=1), dim=1)
     coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
     for g in grads:
         g.mul_(coef.view(NA, *([1] * (g.dim() - 1))))
