@@ -171,7 +171,9 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
  * tables and the pre-draw run k_step_ag, the env's agents split over eight wavefronts of its
  * workgroup; identical results); "ag_envs" (0/16/32/64, default 0 = auto: envs per k_step_ag
  * workgroup, lanes >= ag_envs idle; auto = 64 for launches of fewer than 64 steps, else the
- * fewest that give every workgroup a CU of its own; identical results); "env_id_base" (0..2^32-1, default 0: the handle is the shard [value, value + N) of a
+ * fewest that give every workgroup a CU of its own; identical results); "step_envs" (0/16/32/64,
+ * default 0 = 64; ABI 12: envs per k_step workgroup (fjsp_step), lanes >= step_envs idle;
+ * identical results); "env_id_base" (0..2^32-1, default 0: the handle is the shard [value, value + N) of a
  * larger job — every env's MT19937 stream is re-seeded to np.random.seed(value + e), exactly
  * the stream env value + e of one big handle starts from; stream-ordered); "spin_cap"
  * (256..2^31-1, default 2^22: sleep iterations, checked every 256 a wave of a multi-wave step kernel waits for another

@@ -221,15 +221,18 @@ __device__ __forceinline__ void step_and_emit_staged(Env& E, const Tables& T, co
     FJSP_STAMP(E, 6);
 }
 
-template <bool CANON>
+// EPW: envs per workgroup (64, 32 or 16; lanes >= EPW idle; option "step_envs").  Fewer envs per
+// wave would shorten the union of the lanes' branches and spread 4 096 envs over all 256 CUs; it
+// measured slower (fjsp_step), so 64 stays the default.
+template <bool CANON, int EPW>
 __global__ void __launch_bounds__(BLOCK) k_step(DevState S, Cfg C, const uint8_t* __restrict__ actions, uint64_t order_packed,
                                                 int autoreset, fjsp_out out) {
     FJSP_DIAG(
     const uint64_t t_entry = __builtin_amdgcn_s_memtime();
     )
     __shared__ double s_lut[RLUT_SIZE];
-    const int e = blockIdx.x * BLOCK + threadIdx.x;
-    const bool valid = e < S.n;
+    const int e = blockIdx.x * EPW + threadIdx.x;
+    const bool valid = (int)threadIdx.x < EPW && e < S.n;
     // the state and action loads are issued before the reward table's: one HBM round trip
     Env E;
     int act[NA];
@@ -2018,6 +2021,7 @@ struct fjsp_handle {
     int use_pg;      // pre-draw wave in the pipelined kernel (fjsp_set_option "predraw")
     int use_ag;      // agent-group pipeline k_step_ag for uniform-random actions (fjsp_set_option "agents")
     int ag_epw;      // k_step_ag envs per workgroup: 64 / 32 / 16, 0 = auto (fjsp_set_option "ag_envs")
+    int step_epw;    // k_step envs per workgroup: 64 / 32 / 16, 0 = 64 (fjsp_set_option "step_envs")
     const char* last_kernel;   // name of the last step kernel launched (fjsp_last_kernel)
     uint32_t env_id_base;      // global id of env 0 (fjsp_set_option "env_id_base")
     // fjsp_a2c_policy_step's tile hand-off: [ntiles] arrival counters (zero between launches),
@@ -2174,6 +2178,7 @@ int fjsp_create(const fjsp_config* cfg, int32_t num_envs, int32_t device, void* 
     h->use_pg = 1;
     h->use_ag = 1;
     h->ag_epw = 0;
+    h->step_epw = 0;
     h->dcfg.step_size = c.step_size;
     h->dcfg.max_steps = c.max_episode_steps;
     h->dcfg.tray_cap = c.tray_capacity;
@@ -2274,6 +2279,11 @@ int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
     if (!strcmp(name, "pipeline")) { h->use_pipe = value != 0; return 0; }
     if (!strcmp(name, "predraw")) { h->use_pg = value != 0; return 0; }
     if (!strcmp(name, "agents")) { h->use_ag = value != 0; return 0; }
+    if (!strcmp(name, "step_envs")) {
+        if (value != 0 && value != 16 && value != 32 && value != 64) return fail("step_envs must be 0, 16, 32 or 64");
+        h->step_epw = (int)value;
+        return 0;
+    }
     if (!strcmp(name, "ag_envs")) {
         if (value != 0 && value != 16 && value != 32 && value != 64) return fail("ag_envs must be 0, 16, 32 or 64");
         h->ag_epw = (int)value;
@@ -2351,17 +2361,33 @@ int fjsp_step(fjsp_handle* h, const uint8_t* actions, const uint8_t* agent_order
         }
     }
     DeviceGuard g(h->device);
-    dim3 grid((h->n + BLOCK - 1) / BLOCK);
+    // 64 envs per workgroup unless the option says otherwise: at 4 096 envs 16- / 32-env
+    // workgroups (all 256 CUs busy) measured slower, 8.58 / 8.32 against 7.61 us per launch
+    // (profiles/r06/kstep/ab_step_envs_4096.json): the step is not bound by its lanes' branch union
+    const int epw = h->step_epw ? h->step_epw : 64;
+    const dim3 grid((h->n + epw - 1) / epw);
+    const fjsp_out o = out ? *out : kNoOut;
     if (h->timing) HIPCHK(hipEventRecord(h->ev0, h->stream));
+#define FJSP_LAUNCH_STEP(CN)                                                                                      \
+    do {                                                                                                           \
+        if (epw == 16)                                                                                             \
+            hipLaunchKernelGGL((k_step<CN, 16>), grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, packed, \
+                               autoreset, o);                                                                      \
+        else if (epw == 32)                                                                                        \
+            hipLaunchKernelGGL((k_step<CN, 32>), grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, packed, \
+                               autoreset, o);                                                                      \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_step<CN, 64>), grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, packed, \
+                               autoreset, o);                                                                      \
+    } while (0)
     if (canon) {
         h->last_kernel = "k_step<canon>";
-        hipLaunchKernelGGL(k_step<true>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, packed, autoreset,
-                           out ? *out : kNoOut);
+        FJSP_LAUNCH_STEP(true);
     } else {
         h->last_kernel = "k_step<ordered>";
-        hipLaunchKernelGGL(k_step<false>, grid, dim3(BLOCK), 0, h->stream, h->S, h->dcfg, actions, packed, autoreset,
-                           out ? *out : kNoOut);
+        FJSP_LAUNCH_STEP(false);
     }
+#undef FJSP_LAUNCH_STEP
     HIPCHK(hipGetLastError());
     if (h->timing) {
         HIPCHK(hipEventRecord(h->ev1, h->stream));

@@ -2,7 +2,7 @@
 reference-API path) between library builds: N envs, interleaved rounds of 200 launches, HIP-event
 time per launch (median of rounds), outputs of the first round byte-compared.
 
-usage: python scripts/ab_kstep.py [N] [rounds] lib ..."""
+usage: python scripts/ab_kstep.py [N] [rounds] lib[:option=value] ...  (e.g. libfjsp.so:step_envs=16)"""
 import ctypes
 import json
 import os
@@ -22,7 +22,8 @@ specs = sys.argv[3:]
 P = ctypes.c_void_p
 stream = torch.cuda.current_stream()
 variants = []
-for path in specs:
+for spec in specs:
+    path, _, opt = spec.partition(":")
     L = ctypes.CDLL(os.path.abspath(path))
     L.fjsp_create.argtypes = [ctypes.POINTER(nat.fjsp_config), ctypes.c_int32, ctypes.c_int32, P, ctypes.POINTER(P)]
     L.fjsp_reset.argtypes = [P, P, P, ctypes.c_int32, ctypes.POINTER(nat.fjsp_out)]
@@ -32,10 +33,13 @@ for path in specs:
     cfg = nat.default_config()
     assert L.fjsp_create(ctypes.byref(cfg), N, 0, P(stream.cuda_stream), ctypes.byref(h)) == 0
     assert L.fjsp_set_option(h, b"timing", 0) == 0
+    if opt:
+        k, val = opt.split("=")
+        assert L.fjsp_set_option(h, k.encode(), int(val)) == 0, opt
     seeds = torch.arange(N, dtype=torch.int32, device="cuda")
     assert L.fjsp_reset(h, P(seeds.data_ptr()), None, 30, None) == 0
     buf = V.Buffers(1, N, torch.device("cuda"), infos=False)
-    variants.append({"spec": path, "L": L, "h": h, "buf": buf, "ms": []})
+    variants.append({"spec": spec, "L": L, "h": h, "buf": buf, "ms": []})
 g = torch.Generator(device="cuda").manual_seed(5)
 acts = [torch.randint(0, 3, (8, N), dtype=torch.uint8, device="cuda", generator=g) for _ in range(200)]
 first = []
@@ -49,7 +53,9 @@ for r in range(ROUNDS + 1):
         e1.record(stream)
         torch.cuda.synchronize()
         if r == 0:
-            first.append(v["buf"].rewards.cpu().numpy().tobytes() + v["buf"].obs_i32.cpu().numpy().tobytes())
+            b = v["buf"]
+            first.append(b"".join(t.cpu().numpy().tobytes() for t in (b.rewards, b.obs_i32, b.obs_i8, b.obs_f32, b.masks,
+                                                                       b.term, b.trunc)))
         else:
             v["ms"].append(e0.elapsed_time(e1) / len(acts))
 out = {"N": N, "launches_per_round": len(acts), "rounds": ROUNDS,

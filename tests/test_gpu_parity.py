@@ -115,6 +115,32 @@ def test_step_vs_fused(G):
         masks = r["next_masks"][0]
 
 
+@pytest.mark.parametrize("n", [1, 100, 4133])
+def test_step_envs_per_workgroup_byte_equal(G, n):
+    """k_step (fjsp_step, one launch per step) on 16-, 32- and 64-env workgroups (option
+    "step_envs", default 64) writes the same bytes: 160 steps of random actions with auto-resets,
+    partial workgroups (4 133 envs)."""
+    steps = 160
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    nact = torch.tensor([3, 8, 3, 3, 3, 3, 3, 3], dtype=torch.uint8, device="cuda")[:, None]
+    acts = [torch.randint(0, 8, (8, n), dtype=torch.uint8, device="cuda", generator=gen) % nact for _ in range(steps)]
+    runs = {}
+    for epw in (64, 32, 16, 0):
+        env = G.make_env(n)
+        G.native.check(G.native.lib().fjsp_set_option(env.handle, b"step_envs", epw))
+        env.reset(seeds=torch.arange(n), num_orders=30)
+        outs = []
+        for t in range(steps):
+            r = env.step(acts[t])
+            outs.append(b"".join(getattr(r, k).cpu().numpy().tobytes() for k in
+                                 ("obs_i32", "obs_i8", "obs_f32", "masks", "rewards", "term", "trunc", "status")))
+        runs[epw] = outs
+    for epw in (32, 16, 0):
+        for t in range(steps):
+            assert runs[epw][t] == runs[64][t], (epw, t)
+    assert G.native.lib().fjsp_set_option(env.handle, b"step_envs", 8) != 0
+
+
 def _pinned_buffers(G, n):
     b = G.vec_env.Buffers(1, n, "cpu", infos=True, next_obs=True)
     for k in G.native.OUT_FIELDS:
