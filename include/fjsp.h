@@ -183,7 +183,8 @@ int fjsp_set_stream(fjsp_handle* h, void* hip_stream);
  * step, so that the other waves' bounded waits give up and the give-up path runs).  spin_cap and test_stall are not part of a snapshot.
  * Library-wide (h may be NULL; ABI 10): "policy_xmap" (0..3, default 0), "policy_dedup" (0/1,
  * default 1), "policy_split" (0/1, default 1) — the variants of the A2C policy launches listed at
- * fjsp_a2c_policy; identical results.  Nothing is read from the process environment. */
+ * fjsp_a2c_policy; "wgrad_waves" (8/16, default 16; ABI 12) — fjsp_a2c_wgrad's workgroups of 8 or
+ * 16 waves; identical results.  Nothing is read from the process environment. */
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value);
 int fjsp_num_envs(const fjsp_handle* h);
 /* Bytes of device state per env (HBM footprint of the SoA state). */

@@ -2271,8 +2271,8 @@ extern "C" int fjsp_internal_policy_option(const char* name, int64_t value);   /
 int fjsp_set_option(fjsp_handle* h, const char* name, int64_t value) {
     if (!name) return fail("null argument");
     // library-wide options (h may be null): the A2C policy launches' variants
-    if (!strncmp(name, "policy_", 7)) return fjsp_internal_policy_option(name, value);
-    if (!h) return fail("null handle (only the policy_* options are library-wide)");
+    if (!strncmp(name, "policy_", 7) || !strcmp(name, "wgrad_waves")) return fjsp_internal_policy_option(name, value);
+    if (!h) return fail("null handle (only the policy_* and wgrad_waves options are library-wide)");
     SERVER_QUIESCE(h);
     if (!strcmp(name, "fused_lds")) { h->use_lds = value < 0 ? -1 : value != 0; return 0; }
     if (!strcmp(name, "staged_stores")) { h->use_staged = value != 0; return 0; }

@@ -1317,6 +1317,7 @@ constexpr int WG_KS = 16;                  // samples per stage: one 16-deep blo
 constexpr int WG_ROW = 24;                 // bf16 per LDS image row (16 samples + 8 of padding)
 constexpr int WG_MAXD = 4;                 // the deepest load pipeline of the k_wgrad instances
 constexpr int WG_VPM = 2;                  // split VALU per MFMA in the interleave
+int g_wgrad_waves = 16;                    // k_wgrad16 (16) or k_wgrad (8 waves): library-wide option "wgrad_waves"
 // one stage of F features (F % 4 == 0, F <= 256) -> registers: lane t (0..255 of its wave half)
 // holds the 4 x 4 block (samples 4 (t & 3) .., features 4 (t >> 2) ..).  Buffer loads through a
 // descriptor over the rows from the workgroup's first stage on; the lane's offsets within a stage
@@ -1450,6 +1451,117 @@ k_wgrad(const float* __restrict__ g, int64_t ldg, const float* __restrict__ x, i
         }
     }
     // the partial [M][NPAD] of this workgroup: C/D row (r & 3) + 8 (r >> 2) + 4 h, column lane & 31
+    float* pp = part + (size_t)blockIdx.x * M * NPAD;
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                pp[(size_t)(32 * (mb0 + i) + (r & 3) + 8 * (r >> 2) + 4 * h) * NPAD + 32 * (nb0 + j) + r32] = acc[i][j][r];
+}
+// k_wgrad on 16 waves (the default; 4 per SIMD, 128 registers each): every wave loads (waves 0-7
+// the G tile, 8-15 the X tile, 2 samples x 4 features per lane), holds TM x TN accumulator tiles and
+// runs its A fragments one row tile at a time; more waves per SIMD hide the loads, the split and
+// the stage barrier behind each other's MFMAs (the 8-wave kernel's W2 instance left the matrix
+// cores 63 % idle): W2 / W3 / W1 0.35 / 0.215 / 0.157 against 0.40 / 0.24 / 0.18 ms at 540 k
+// states, bit-identical (the same products per accumulator in the same order).
+__device__ __forceinline__ void wg_load2(const WgSrc& w, int off, float4 (&v)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(w.rsrc, (int)((unsigned)w.voff[i] + (unsigned)off), 0, 0);
+        v[i] = make_float4(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[2]), __uint_as_float(r[3]));
+    }
+}
+__device__ __forceinline__ WgSrc wg_src2(const float* src, int64_t ld, int F, int64_t r0, int64_t U, int t) {
+    WgSrc w;
+    const int64_t rem = (U - r0) * ld * 4;
+    const int bytes = rem <= 0 ? 0 : rem > 0x7FFFFF00ll ? 0x7FFFFF00 : (int)rem;
+    w.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src + r0 * ld), (short)0, bytes, 0x00020000);
+    const int sp = t & 7, fq = t >> 3;   // samples 2 sp, 2 sp + 1; features 4 fq ..
+#pragma unroll
+    for (int i = 0; i < 2; i++) w.voff[i] = 4 * fq < F ? (int)(((2 * sp + i) * ld + 4 * fq) * 4) : 0x7FFFFFF0;
+    w.voff[2] = w.voff[3] = 0;
+    return w;
+}
+__device__ __forceinline__ void wg_store2(const float4 (&v)[2], int t, __bf16* s) {
+    constexpr int plane = 256 * WG_ROW;
+    const int sp = t & 7, fq = t >> 3;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        __bf16 h0, m0, l0, h1, m1, l1;
+        split3(f4c(v[0], c), h0, m0, l0);
+        split3(f4c(v[1], c), h1, m1, l1);
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        const int o = (4 * fq + c) * WG_ROW + 2 * sp;
+        *reinterpret_cast<bf16x2*>(s + o) = bf16x2{h0, h1};
+        *reinterpret_cast<bf16x2*>(s + plane + o) = bf16x2{m0, m1};
+        *reinterpret_cast<bf16x2*>(s + 2 * plane + o) = bf16x2{l0, l1};
+    }
+}
+template <int M, int NPAD, int TM, int TN, int D>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 4)))
+k_wgrad16(const float* __restrict__ g, int64_t ldg, const float* __restrict__ x, int64_t ldx, int nx, int64_t U,
+          float* __restrict__ part) {
+    static_assert((M / 32 / TM) * (NPAD / 32 / TN) == 16, "one tile group per wave");
+    constexpr int WN = NPAD / 32 / TN;
+    constexpr int PL = 256 * WG_ROW, BUF = 2 * NP * PL;
+    __shared__ __attribute__((aligned(16))) __bf16 s_img[2 * BUF];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool ldr_g = wave < 8;
+    const int t = tid & 511;
+    const int mb0 = (wave / WN) * TM, nb0 = (wave % WN) * TN;
+    const int64_t stages = (U + WG_KS - 1) / WG_KS, P = gridDim.x, b = blockIdx.x;
+    const int nj = stages > b ? (int)((stages - b + P - 1) / P) : 0;
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.0f;
+    const int64_t ld = ldr_g ? ldg : ldx;
+    const int img = ldr_g ? 0 : NP * PL;
+    const WgSrc ws = wg_src2(ldr_g ? g : x, ld, ldr_g ? M : nx, b * WG_KS, U, t);
+    const int sstride = (int)(P * WG_KS * ld * 4);
+    float4 v[D][2];
+    if (nj > 0) {
+#pragma unroll
+        for (int k = 0; k < D; k++) wg_load2(ws, k * sstride, v[k]);
+        wg_store2(v[0], t, s_img + img);
+        wg_load2(ws, D * sstride, v[0]);
+    }
+    __syncthreads();
+    const int h = lane >> 5, r32 = lane & 31;
+    for (int jb = 0; jb < nj; jb += D) {
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            const int j = jb + d;
+            if (j >= nj) break;
+            const __bf16* cg = s_img + (j & 1) * BUF;
+            const __bf16* cx = cg + NP * PL;
+#pragma unroll
+            for (int i = 0; i < TM; i++) {
+                bf16x8 a[NP];
+                const int oa = (32 * (mb0 + i) + r32) * WG_ROW + 8 * h;
+#pragma unroll
+                for (int p = 0; p < NP; p++) a[p] = *reinterpret_cast<const bf16x8*>(cg + p * PL + oa);
+#pragma unroll
+                for (int jj = 0; jj < TN; jj++) {
+                    bf16x8 bb[NP];
+                    const int o = (32 * (nb0 + jj) + r32) * WG_ROW + 8 * h;
+#pragma unroll
+                    for (int p = 0; p < NP; p++) bb[p] = *reinterpret_cast<const bf16x8*>(cx + p * PL + o);
+                    acc[i][jj] = mfma6(a, bb, acc[i][jj]);
+                }
+            }
+            const int k = (d + 1) % D;
+            wg_store2(v[k], t, s_img + ((j + 1) & 1) * BUF + img);
+            wg_load2(ws, (j + 1 + D) * sstride, v[k]);
+            __syncthreads();
+        }
+    }
     float* pp = part + (size_t)blockIdx.x * M * NPAD;
 #pragma unroll
     for (int i = 0; i < TM; i++)
@@ -1933,6 +2045,11 @@ extern "C" int fjsp_internal_policy_option(const char* name, int64_t value) {
         return 0;
     }
     if (!strcmp(name, "policy_dedup")) { g_policy_dedup = value != 0; return 0; }
+    if (!strcmp(name, "wgrad_waves")) {
+        if (value != 8 && value != 16) return fjsp_internal_fail("wgrad_waves must be 8 or 16");
+        g_wgrad_waves = (int)value;
+        return 0;
+    }
     if (!strcmp(name, "policy_split")) { g_policy_split = value != 0; return 0; }
     return fjsp_internal_fail("unknown option");
 }
@@ -2160,13 +2277,22 @@ extern "C" int fjsp_a2c_wgrad(const float* g, int32_t m, int64_t ldg, const floa
     int npad;
     if (m == 256 && nx > 64 && nx <= 256) {
         npad = 256;
-        hipLaunchKernelGGL((k_wgrad<256, 256, 2, 4, 2>), dim3((unsigned)P), dim3(NTHR), 0, st, g, ldg, x, ldx, nx, U, part);
+        if (g_wgrad_waves == 16)
+            hipLaunchKernelGGL((k_wgrad16<256, 256, 2, 2, 1>), dim3((unsigned)P), dim3(1024), 0, st, g, ldg, x, ldx, nx, U, part);
+        else
+            hipLaunchKernelGGL((k_wgrad<256, 256, 2, 4, 2>), dim3((unsigned)P), dim3(NTHR), 0, st, g, ldg, x, ldx, nx, U, part);
     } else if (m == 128 && nx > 64 && nx <= 256) {
         npad = 256;
-        hipLaunchKernelGGL((k_wgrad<128, 256, 2, 2, 4>), dim3((unsigned)P), dim3(NTHR), 0, st, g, ldg, x, ldx, nx, U, part);
+        if (g_wgrad_waves == 16)
+            hipLaunchKernelGGL((k_wgrad16<128, 256, 1, 2, 2>), dim3((unsigned)P), dim3(1024), 0, st, g, ldg, x, ldx, nx, U, part);
+        else
+            hipLaunchKernelGGL((k_wgrad<128, 256, 2, 2, 4>), dim3((unsigned)P), dim3(NTHR), 0, st, g, ldg, x, ldx, nx, U, part);
     } else if (m == 256 && nx <= 64) {
         npad = 64;
-        hipLaunchKernelGGL((k_wgrad<256, 64, 1, 2, 4>), dim3((unsigned)P), dim3(NTHR), 0, st, g, ldg, x, ldx, nx, U, part);
+        if (g_wgrad_waves == 16)
+            hipLaunchKernelGGL((k_wgrad16<256, 64, 1, 1, 3>), dim3((unsigned)P), dim3(1024), 0, st, g, ldg, x, ldx, nx, U, part);
+        else
+            hipLaunchKernelGGL((k_wgrad<256, 64, 1, 2, 4>), dim3((unsigned)P), dim3(NTHR), 0, st, g, ldg, x, ldx, nx, U, part);
     } else {
         return fjsp_internal_fail("fjsp_a2c_wgrad: (m, nx) must be (256, 68..256), (128, 68..256) or (256, 4..64)");
     }

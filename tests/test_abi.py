@@ -132,6 +132,8 @@ def test_wgrad_validates_arguments_without_gpu():
     bad(2, 128, b"16-byte aligned")           # ldg < m
     bad(10, 300, b"nout")
     bad(1, 64, b"(m, nx)")
+    assert L.fjsp_set_option(None, b"wgrad_waves", 12) != 0
+    assert L.fjsp_set_option(None, b"wgrad_waves", 8) == 0 and L.fjsp_set_option(None, b"wgrad_waves", 16) == 0
 
 
 def test_library_wide_policy_options_without_gpu():

@@ -822,6 +822,12 @@ def test_wgrad_kernel_matches_float64(M, m, nx, nout, U):
     assert e <= max(3 * et, 2e-6), (e, et)
     assert torch.equal(gw, A.critic_wgrad(g, x, nout))
     assert torch.equal(gw, A._critic_wgrad(g, x, nout if nout != nx else None))
+    L = A.nat.lib()
+    try:   # the 8-wave kernel (library-wide option "wgrad_waves"): the same bits
+        assert L.fjsp_set_option(None, b"wgrad_waves", 8) == 0
+        assert torch.equal(gw, A.critic_wgrad(g, x, nout))
+    finally:
+        assert L.fjsp_set_option(None, b"wgrad_waves", 16) == 0
     if U > 100000:   # the chunked path (batches past the kernel's 2 GiB offset range): the same sum
         old = A.WGRAD_MAX_ROWS
         try:
