@@ -1465,7 +1465,9 @@ k_wgrad(const float* __restrict__ g, int64_t ldg, const float* __restrict__ x, i
 // runs its A fragments one row tile at a time; more waves per SIMD hide the loads, the split and
 // the stage barrier behind each other's MFMAs (the 8-wave kernel's W2 instance left the matrix
 // cores 63 % idle): W2 / W3 / W1 0.35 / 0.215 / 0.157 against 0.40 / 0.24 / 0.18 ms at 540 k
-// states, bit-identical (the same products per accumulator in the same order).
+// states, bit-identical (the same products per accumulator in the same order); W2 on 1 x 4 tiles
+// per wave (fewer fragment reads and registers): 0.38 against 0.47 ms for 2 x 2 on dense random
+// operands, equal (0.35) on the update's half-zero gradients.
 __device__ __forceinline__ void wg_load2(const WgSrc& w, int off, float4 (&v)[2]) {
 #pragma unroll
     for (int i = 0; i < 2; i++) {
@@ -2278,7 +2280,7 @@ extern "C" int fjsp_a2c_wgrad(const float* g, int32_t m, int64_t ldg, const floa
     if (m == 256 && nx > 64 && nx <= 256) {
         npad = 256;
         if (g_wgrad_waves == 16)
-            hipLaunchKernelGGL((k_wgrad16<256, 256, 2, 2, 1>), dim3((unsigned)P), dim3(1024), 0, st, g, ldg, x, ldx, nx, U, part);
+            hipLaunchKernelGGL((k_wgrad16<256, 256, 1, 4, 1>), dim3((unsigned)P), dim3(1024), 0, st, g, ldg, x, ldx, nx, U, part);
         else
             hipLaunchKernelGGL((k_wgrad<256, 256, 2, 4, 2>), dim3((unsigned)P), dim3(NTHR), 0, st, g, ldg, x, ldx, nx, U, part);
     } else if (m == 128 && nx > 64 && nx <= 256) {
